@@ -1,0 +1,665 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY -- the CPU restatement used as the parity
+checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+The product path (trivy_amd/) never imports this module.
+
+A line-by-line restatement (in Python, on top of oracle/goregex.py) of the
+reference's secret-scanning path:
+
+  ParseConfig / convertSeverity   pkg/fanal/secret/scanner.go:277-318
+  NewScanner                      scanner.go:320-364
+  Scanner.Scan                    scanner.go:377-463
+  FindLocations / FindSubmatch    scanner.go:102-148
+  AllowLocation / getMatchSub..   scanner.go:150-168
+  MatchKeywords                   scanner.go:174-186 (bytes.ToLower semantics)
+  AllowRules / ExcludeBlock       scanner.go:196-275
+  censorLocation / toFinding      scanner.go:465-488
+  findLocation                    scanner.go:490-558
+  sort.Slice                      go1.23.4 sort/zsortfunc.go (pdqsort_func)
+  SecretAnalyzer.Analyze/Required pkg/fanal/analyzer/secret/secret.go:103-190
+  IsBinary / ExtractPrintable     pkg/fanal/utils/utils.go:68-86, 111-143
+
+Parity pinning: tests/test_oracle_golden.py checks this oracle against all 40
+cases of scanner_test.go, the analyzer tests and the integration golden
+(tests/golden/*.json, generated from the reference by tests/golden/make_fixtures.py).
+Strings in results are `str` decoded from Go byte strings with
+'surrogateescape' (an invalid byte survives as one lone surrogate).
+"""
+import json
+import os
+import unicodedata  # noqa: F401  (documented dependency of str.lower per char)
+
+import yaml
+
+from .goregex import GoRegexp
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+BUILTIN_JSON = os.path.join(_HERE, "..", "trivy_amd", "data", "builtin_rules.json")
+
+
+def _s(b):
+    return b.decode("utf-8", "surrogateescape")
+
+
+# --------------------------------------------------------------------- rules
+class Rule:
+    def __init__(self, id="", category="", title="", severity="", regex=None, keywords=None,
+                 path=None, allow_rules=None, exclude_block=None, secret_group_name=""):
+        self.id, self.category, self.title, self.severity = id, category, title, severity
+        self.regex = regex                  # GoRegexp or None
+        self.keywords = keywords or []
+        self.path = path                    # GoRegexp or None
+        self.allow_rules = allow_rules or []
+        self.exclude_block = exclude_block or []   # list of GoRegexp
+        self.secret_group_name = secret_group_name
+
+    # scanner.go:170-172
+    def match_path(self, path):
+        return self.path is None or self.path.match_string(path)
+
+    # scanner.go:174-186
+    def match_keywords(self, content):
+        if not self.keywords:
+            return True
+        lower = go_bytes_to_lower(content)
+        for kw in self.keywords:
+            if go_str_to_lower(kw).encode("utf-8", "surrogateescape") in lower:
+                return True
+        return False
+
+    def allow_path(self, path):
+        return allow_rules_allow_path(self.allow_rules, path)
+
+    def allow(self, match):
+        return allow_rules_allow(self.allow_rules, match)
+
+
+class AllowRule:
+    def __init__(self, id="", description="", regex=None, path=None):
+        self.id, self.description, self.regex, self.path = id, description, regex, path
+
+
+def allow_rules_allow_path(rules, path):      # scanner.go:205-212
+    return any(r.path is not None and r.path.match_string(path) for r in rules)
+
+
+def allow_rules_allow(rules, match):          # scanner.go:214-221
+    return any(r.regex is not None and r.regex.match_string(match) for r in rules)
+
+
+# ------------------------------------------------------- Go case conversion
+def _go_rune_lower(ch):
+    # unicode.ToLower: simple (1:1) lowercase mapping; str.lower() of a single
+    # char equals it except for U+0130 (full mapping "i̇"; Go gives 'i').
+    if ch == "İ":
+        return "i"
+    lo = ch.lower()
+    return lo if len(lo) == 1 else ch
+
+
+def go_bytes_to_lower(b):
+    """bytes.ToLower: ASCII fast path, else Map(unicode.ToLower) where each
+    invalid byte becomes U+FFFD (bytes.Map writes RuneError's encoding)."""
+    if b.isascii():
+        return b.lower()
+    out = []
+    for ch in b.decode("utf-8", "surrogateescape"):
+        if 0xDC80 <= ord(ch) <= 0xDCFF:
+            out.append("�")
+        else:
+            out.append(_go_rune_lower(ch))
+    return "".join(out).encode("utf-8")
+
+
+def go_str_to_lower(s):
+    if s.isascii():
+        return s.lower()
+    return "".join("�" if 0xDC80 <= ord(c) <= 0xDCFF else _go_rune_lower(c) for c in s)
+
+
+# ------------------------------------------------------------- config / init
+class ConfigError(Exception):
+    pass
+
+
+def _compile(v):
+    if v is None:
+        return None
+    try:
+        return GoRegexp(str(v))
+    except Exception as e:  # regexp compile error (scanner.go:80-83)
+        raise ConfigError("regexp compile error: %s" % e)
+
+
+def _allow_rules(lst):
+    out = []
+    for a in lst or []:
+        out.append(AllowRule(id=str(a.get("id", "") or ""), description=str(a.get("description", "") or ""),
+                             regex=_compile(a.get("regex")), path=_compile(a.get("path"))))
+    return out
+
+
+def _exclude(blk):
+    if not blk:
+        return []
+    return [_compile(r) for r in (blk.get("regexes") or [])]
+
+
+def convert_severity(sev):            # scanner.go:309-318
+    if sev.lower() in ("low", "medium", "high", "critical", "unknown"):
+        return sev.upper()
+    return "UNKNOWN"
+
+
+def parse_config(path):
+    """scanner.go:277-307. Returns None for '' or a missing file."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        doc = yaml.safe_load(f) or {}
+    cfg = {
+        "enable_builtin_rule_ids": [str(x) for x in (doc.get("enable-builtin-rules") or [])],
+        "disable_rule_ids": [str(x) for x in (doc.get("disable-rules") or [])],
+        "disable_allow_rule_ids": [str(x) for x in (doc.get("disable-allow-rules") or [])],
+        "custom_allow_rules": _allow_rules(doc.get("allow-rules")),
+        "exclude_block": _exclude(doc.get("exclude-block")),
+        "custom_rules": [],
+    }
+    for r in doc.get("rules") or []:
+        cfg["custom_rules"].append(Rule(
+            id=str(r.get("id", "") or ""), category=str(r.get("category", "") or ""),
+            title=str(r.get("title", "") or ""),
+            severity=convert_severity(str(r.get("severity", "") or "")),
+            regex=_compile(r.get("regex")), keywords=[str(k) for k in (r.get("keywords") or [])],
+            path=_compile(r.get("path")), allow_rules=_allow_rules(r.get("allow-rules")),
+            exclude_block=_exclude(r.get("exclude-block")),
+            secret_group_name=str(r.get("secret-group-name", "") or "")))
+    return cfg
+
+
+_BUILTIN = None
+
+
+def builtin():
+    global _BUILTIN
+    if _BUILTIN is None:
+        d = json.load(open(BUILTIN_JSON))
+        rules = [Rule(id=r["id"], category=r["category"], title=r["title"], severity=r["severity"],
+                      regex=GoRegexp(r["regex"]), keywords=r["keywords"],
+                      secret_group_name=r["secret_group_name"]) for r in d["rules"]]
+        allows = [AllowRule(id=a["id"], description=a["description"],
+                            regex=_compile(a["regex"]), path=_compile(a["path"]))
+                  for a in d["allow_rules"]]
+        _BUILTIN = (rules, allows)
+    return _BUILTIN
+
+
+class Scanner:
+    """NewScanner (scanner.go:320-364) + Scan (scanner.go:377-463)."""
+
+    def __init__(self, config=None):
+        b_rules, b_allow = builtin()
+        if config is None:
+            self.rules, self.allow_rules, self.exclude_block = list(b_rules), list(b_allow), []
+            return
+        enabled = list(b_rules)
+        if config["enable_builtin_rule_ids"]:
+            enabled = [r for r in b_rules if r.id in config["enable_builtin_rule_ids"]]
+        enabled = enabled + config["custom_rules"]
+        self.rules = [r for r in enabled if r.id not in config["disable_rule_ids"]]
+        allows = list(b_allow) + config["custom_allow_rules"]
+        self.allow_rules = [a for a in allows if a.id not in config["disable_allow_rule_ids"]]
+        self.exclude_block = config["exclude_block"]
+
+    def allow_path(self, path):
+        return allow_rules_allow_path(self.allow_rules, path)
+
+    def _allow_location(self, rule, content, s, e):
+        m = content[s:e]
+        return allow_rules_allow(self.allow_rules, m) or rule.allow(m)
+
+    def find_locations(self, rule, content, prepared):      # scanner.go:102-148
+        if rule.regex is None:
+            return []
+        locs = []
+        if rule.secret_group_name:
+            names = rule.regex.subexp_names
+            for mi in rule.regex.find_all(content, prepared, submatch=True):
+                if self._allow_location(rule, content, mi[0], mi[1]):
+                    continue
+                for i, n in enumerate(names):
+                    if n == rule.secret_group_name:
+                        locs.append((mi[2 * i], mi[2 * i + 1]))
+            return locs
+        for s, e in rule.regex.find_all(content, prepared):
+            if self._allow_location(rule, content, s, e):
+                continue
+            locs.append((s, e))
+        return locs
+
+    def scan(self, file_path, content, binary=False):
+        """Returns types.Secret as a dict {FilePath, Findings}."""
+        if self.allow_path(file_path):
+            return {"FilePath": file_path, "Findings": []}
+        prepared = None
+        censored = None
+        matched = []
+        gblocks = _Blocks(content, self.exclude_block)
+        for rule in self.rules:
+            if not rule.match_path(file_path):
+                continue
+            if rule.allow_path(file_path):
+                continue
+            if not rule.match_keywords(content):
+                continue
+            if prepared is None:
+                prepared = GoRegexp.prepare(content)
+            locs = self.find_locations(rule, content, prepared)
+            if not locs:
+                continue
+            lblocks = _Blocks(content, rule.exclude_block)
+            for loc in locs:
+                if gblocks.match(loc) or lblocks.match(loc):
+                    continue
+                matched.append((rule, loc))
+                if censored is None:
+                    censored = bytearray(content)
+                censored = censor_location(loc, censored)
+        findings = []
+        for rule, loc in matched:
+            f = to_finding(rule, loc, censored)
+            if binary:
+                f["Match"] = 'Binary file %s matches a rule %s' % (go_quote(file_path), go_quote(rule.title))
+                f["Code"] = {"Lines": []}
+            findings.append(f)
+        if not findings:
+            return {"FilePath": "", "Findings": []}
+        go_sort_slice(findings, lambda a, b: a["RuleID"] < b["RuleID"] if a["RuleID"] != b["RuleID"]
+                      else _go_str_less(a["Match"], b["Match"]))
+        return {"FilePath": file_path, "Findings": findings}
+
+
+def _go_str_less(a, b):
+    # Go compares strings bytewise
+    return a.encode("utf-8", "surrogateescape") < b.encode("utf-8", "surrogateescape")
+
+
+def go_quote(s):
+    """fmt %q of a Go string (strconv.Quote), enough for file paths/titles."""
+    out = ['"']
+    for ch in s:
+        o = ord(ch)
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif 0xDC80 <= o <= 0xDCFF:
+            out.append("\\x%02x" % (o - 0xDC00))
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\r":
+            out.append("\\r")
+        elif o < 0x20 or o == 0x7f:
+            out.append("\\x%02x" % o)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+class _Blocks:                          # scanner.go:237-275 (lazy find)
+    def __init__(self, content, regexes):
+        self.content, self.regexes, self.locs = content, regexes, None
+
+    def match(self, loc):
+        if self.locs is None:
+            self.locs = []
+            for rx in self.regexes:
+                for s, e in rx.find_all(self.content):
+                    self.locs.append((s, e))
+        s, e = loc
+        return any(bs <= s and e <= be for bs, be in self.locs)
+
+
+def censor_location(loc, buf):          # scanner.go:465-473
+    s, e = loc
+    buf[s:e] = b"*" * (e - s)
+    return buf
+
+
+def to_finding(rule, loc, content):     # scanner.go:475-488
+    start_line, end_line, code, match_line = find_location(loc[0], loc[1], content)
+    return {
+        "RuleID": rule.id, "Category": rule.category,
+        "Severity": "UNKNOWN" if rule.severity == "" else rule.severity,
+        "Title": rule.title, "StartLine": start_line, "EndLine": end_line,
+        "Code": code, "Match": match_line,
+    }
+
+
+def find_location(start, end, content):  # scanner.go:495-558
+    content = bytes(content)
+    start_line_num = content.count(b"\n", 0, start)
+    ls = content.rfind(b"\n", 0, start)
+    line_start = 0 if ls == -1 else ls + 1
+    le = content.find(b"\n", start)
+    line_end = len(content) if le == -1 else le
+    if line_end - line_start > 100:
+        line_start = line_start if start - line_start - 30 < 0 else start - 30
+        line_end = line_end if end + 20 > line_end else end + 20
+    match_line = _s(content[line_start:line_end])
+    end_line_num = start_line_num + content.count(b"\n", start, end)
+    lines = content.split(b"\n")
+    code_start = max(start_line_num - 2, 0)
+    code_end = min(end_line_num + 2, len(lines))
+    out = []
+    found_first = False
+    for i, raw in enumerate(lines[code_start:code_end]):
+        real = code_start + i
+        in_cause = start_line_num <= real <= end_line_num
+        if len(raw) > 100:
+            s = match_line if in_cause else _s(raw[:100])
+        else:
+            s = _s(raw)
+        out.append({"Number": code_start + i + 1, "Content": s, "IsCause": in_cause,
+                    "Annotation": "", "Truncated": False, "Highlighted": s,
+                    "FirstCause": (not found_first) and in_cause, "LastCause": False})
+        found_first = found_first or in_cause
+    for ln in reversed(out):
+        if ln["IsCause"]:
+            ln["LastCause"] = True
+            break
+    return start_line_num + 1, end_line_num + 1, {"Lines": out}, match_line
+
+
+# --------------------------------------------------------------- Go sort.Slice
+def go_sort_slice(data, less):
+    """sort.Slice == pdqsort_func(data, 0, n, bits.Len(n)) (go1.23 zsortfunc.go)."""
+    n = len(data)
+    _pdq(data, less, 0, n, n.bit_length())
+
+
+def _ins(d, lt, a, b):
+    for i in range(a + 1, b):
+        j = i
+        while j > a and lt(d[j], d[j - 1]):
+            d[j], d[j - 1] = d[j - 1], d[j]
+            j -= 1
+
+
+def _sift(d, lt, lo, hi, first):
+    root = lo
+    while True:
+        child = 2 * root + 1
+        if child >= hi:
+            return
+        if child + 1 < hi and lt(d[first + child], d[first + child + 1]):
+            child += 1
+        if not lt(d[first + root], d[first + child]):
+            return
+        d[first + root], d[first + child] = d[first + child], d[first + root]
+        root = child
+
+
+def _heap(d, lt, a, b):
+    first, lo, hi = a, 0, b - a
+    for i in range((hi - 1) // 2, -1, -1):
+        _sift(d, lt, i, hi, first)
+    for i in range(hi - 1, -1, -1):
+        d[first], d[first + i] = d[first + i], d[first]
+        _sift(d, lt, lo, i, first)
+
+
+_INC, _DEC, _UNK = 1, 2, 0
+
+
+def _pdq(d, lt, a, b, limit):
+    was_balanced, was_partitioned = True, True
+    while True:
+        length = b - a
+        if length <= 12:
+            _ins(d, lt, a, b)
+            return
+        if limit == 0:
+            _heap(d, lt, a, b)
+            return
+        if not was_balanced:
+            _break_patterns(d, a, b)
+            limit -= 1
+        pivot, hint = _choose_pivot(d, lt, a, b)
+        if hint == _DEC:
+            _reverse(d, a, b)
+            pivot = (b - 1) - (pivot - a)
+            hint = _INC
+        if was_balanced and was_partitioned and hint == _INC:
+            if _partial_ins(d, lt, a, b):
+                return
+        if a > 0 and not lt(d[a - 1], d[pivot]):
+            a = _partition_equal(d, lt, a, b, pivot)
+            continue
+        mid, already = _partition(d, lt, a, b, pivot)
+        was_partitioned = already
+        left, right = mid - a, b - mid
+        thr = length // 8
+        if left < right:
+            was_balanced = left >= thr
+            _pdq(d, lt, a, mid, limit)
+            a = mid + 1
+        else:
+            was_balanced = right >= thr
+            _pdq(d, lt, mid + 1, b, limit)
+            b = mid
+
+
+def _partition(d, lt, a, b, pivot):
+    d[a], d[pivot] = d[pivot], d[a]
+    i, j = a + 1, b - 1
+    while i <= j and lt(d[i], d[a]):
+        i += 1
+    while i <= j and not lt(d[j], d[a]):
+        j -= 1
+    if i > j:
+        d[j], d[a] = d[a], d[j]
+        return j, True
+    d[i], d[j] = d[j], d[i]
+    i += 1
+    j -= 1
+    while True:
+        while i <= j and lt(d[i], d[a]):
+            i += 1
+        while i <= j and not lt(d[j], d[a]):
+            j -= 1
+        if i > j:
+            break
+        d[i], d[j] = d[j], d[i]
+        i += 1
+        j -= 1
+    d[j], d[a] = d[a], d[j]
+    return j, False
+
+
+def _partition_equal(d, lt, a, b, pivot):
+    d[a], d[pivot] = d[pivot], d[a]
+    i, j = a + 1, b - 1
+    while True:
+        while i <= j and not lt(d[a], d[i]):
+            i += 1
+        while i <= j and lt(d[a], d[j]):
+            j -= 1
+        if i > j:
+            break
+        d[i], d[j] = d[j], d[i]
+        i += 1
+        j -= 1
+    return i
+
+
+def _partial_ins(d, lt, a, b):
+    i = a + 1
+    for _ in range(5):
+        while i < b and not lt(d[i], d[i - 1]):
+            i += 1
+        if i == b:
+            return True
+        if b - a < 50:
+            return False
+        d[i], d[i - 1] = d[i - 1], d[i]
+        if i - a >= 2:
+            j = i - 1
+            while j >= 1:
+                if not lt(d[j], d[j - 1]):
+                    break
+                d[j], d[j - 1] = d[j - 1], d[j]
+                j -= 1
+        if b - i >= 2:
+            j = i + 1
+            while j < b:
+                if not lt(d[j], d[j - 1]):
+                    break
+                d[j], d[j - 1] = d[j - 1], d[j]
+                j += 1
+    return False
+
+
+def _break_patterns(d, a, b):
+    length = b - a
+    if length >= 8:
+        r = length
+        modulus = 1 << length.bit_length()
+        idx = a + (length // 4) * 2 - 1
+        for i in range(3):
+            r ^= (r << 13) & 0xFFFFFFFFFFFFFFFF
+            r ^= r >> 7
+            r ^= (r << 17) & 0xFFFFFFFFFFFFFFFF
+            other = r & (modulus - 1)
+            if other >= length:
+                other -= length
+            d[idx - 1 + i], d[a + other] = d[a + other], d[idx - 1 + i]
+
+
+def _choose_pivot(d, lt, a, b):
+    ln = b - a
+    swaps = [0]
+    i, j, k = a + ln // 4 * 1, a + ln // 4 * 2, a + ln // 4 * 3
+
+    def order2(x, y):
+        if lt(d[y], d[x]):
+            swaps[0] += 1
+            return y, x
+        return x, y
+
+    def median(x, y, z):
+        x, y = order2(x, y)
+        y, z = order2(y, z)
+        x, y = order2(x, y)
+        return y
+    if ln >= 8:
+        if ln >= 50:
+            i = median(i - 1, i, i + 1)
+            j = median(j - 1, j, j + 1)
+            k = median(k - 1, k, k + 1)
+        j = median(i, j, k)
+    if swaps[0] == 0:
+        return j, _INC
+    if swaps[0] == 12:
+        return j, _DEC
+    return j, _UNK
+
+
+def _reverse(d, a, b):
+    i, j = a, b - 1
+    while i < j:
+        d[i], d[j] = d[j], d[i]
+        i += 1
+        j -= 1
+
+
+# ------------------------------------------------- analyzer (content prep)
+SKIP_FILES = ["go.mod", "go.sum", "package-lock.json", "yarn.lock", "pnpm-lock.yaml",
+              "Pipfile.lock", "Gemfile.lock"]
+SKIP_DIRS = [".git", "node_modules"]
+SKIP_EXTS = [".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg", ".socket", ".deb",
+             ".rpm", ".zip", ".gz", ".gzip", ".tar"]
+
+
+def go_ext(name):
+    """filepath.Ext"""
+    i = len(name) - 1
+    while i >= 0 and name[i] != "/":
+        if name[i] == ".":
+            return name[i:]
+        i -= 1
+    return ""
+
+
+def is_binary(head_bytes):              # utils.go:68-86
+    for b in head_bytes[:300]:
+        if b < 7 or b == 11 or (13 < b < 27) or (27 < b < 0x20) or b == 0x7F:
+            return True
+    return False
+
+
+def _latin1_printable(b):
+    # unicode.IsPrint(rune(b)) for b in 0..255: graphic L/M/N/P/S or U+0020
+    if b == 0x20:
+        return True
+    ch = chr(b)
+    cat = unicodedata.category(ch)
+    return cat[0] in "LMNPS"
+
+
+def extract_printable_bytes(data):      # utils.go:111-143
+    out = bytearray()
+    cur = bytearray()
+    for b in data:
+        if _latin1_printable(b):
+            cur.append(b)
+            continue
+        if len(cur) > 4:
+            cur.append(0x0A)
+            out += cur
+        cur = bytearray()
+    if len(cur) > 4:
+        cur.append(0x0A)
+        out += cur
+    return bytes(out)
+
+
+class SecretAnalyzer:
+    """pkg/fanal/analyzer/secret/secret.go (Init, Analyze, Required)."""
+
+    def __init__(self, config_path=""):
+        self.config_path = config_path
+        self.scanner = Scanner(parse_config(config_path))
+
+    def required(self, file_path, size):          # secret.go:152-190
+        if size < 10:
+            return False
+        d, name = os.path.split(file_path)
+        dirs = (d + "/" if d else "").split("/")
+        if any(sd in dirs for sd in SKIP_DIRS):
+            return False
+        if name in SKIP_FILES:
+            return False
+        if os.path.basename(self.config_path) == file_path:
+            return False
+        if go_ext(name) in SKIP_EXTS:
+            return False
+        if self.scanner.allow_path(file_path):
+            return False
+        return True
+
+    def analyze(self, file_path, raw, dir_="."):   # secret.go:103-150
+        binary = is_binary(raw[:300])
+        if binary and go_ext(file_path) != ".pyc":
+            return None
+        if not binary:
+            content = raw.replace(b"\r", b"")
+        else:
+            content = extract_printable_bytes(raw)
+        fp = file_path if dir_ else "/" + file_path
+        res = self.scanner.scan(fp, content, binary)
+        if not res["Findings"]:
+            return None
+        return [res]
