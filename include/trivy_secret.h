@@ -1,0 +1,171 @@
+/*
+ * trivy_secret.h -- C-ABI of the MI355X-native secret-scanning engine
+ * (drop-in for mmorel-35/trivy pkg/fanal/secret).
+ *
+ * Reference interface each entry point replaces (paths relative to the
+ * reference repository):
+ *
+ *   tsg_ruleset_compile     secret.ParseConfig + secret.NewScanner
+ *                           pkg/fanal/secret/scanner.go:277-307, 320-364
+ *   tsg_ruleset_allow_path  (Global).AllowPath        scanner.go:56-59
+ *   tsg_builtin_rules_json  secret.GetBuiltinRules     builtin-rules.go:87-89
+ *   tsg_engine_create       (no reference analogue: binds the compiled
+ *                           rules to one GPU; the reference's regexes are
+ *                           compiled inside ParseConfig/NewScanner)
+ *   tsg_scan_batch          N x (*Scanner).Scan(ScanArgs) -> types.Secret
+ *                           scanner.go:366-463, batched as proposed in
+ *                           SURVEY.md 8(b); ScanArgs{FilePath, Content,
+ *                           Binary} = (paths[i], data[off[i]:off[i+1]],
+ *                           binary[i])
+ *   tsg_result_*            types.Secret / SecretFinding / Code / Line
+ *                           pkg/fanal/types/secret.go:5-20, misconf.go:48-61
+ *
+ * Conventions
+ *   - status: 0 = OK, negative = error; tsg_last_error() returns a
+ *     thread-local message for the last failing call on this thread.
+ *   - strings crossing the boundary are Go byte strings: pointer + length,
+ *     not necessarily valid UTF-8, not NUL-terminated unless stated.
+ *   - ownership: the caller owns every input buffer until the call returns;
+ *     the library owns every tsg_* object until its *_free/_destroy call.
+ *   - threading: a tsg_ruleset is immutable and may be shared; a tsg_engine
+ *     serialises calls internally (one HIP stream per engine).
+ *   - there is no CPU fallback: tsg_engine_create fails with
+ *     TSG_ERR_NO_DEVICE when no MI355X (HIP device) is visible.
+ */
+#ifndef TRIVY_SECRET_H_
+#define TRIVY_SECRET_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSG_OK 0
+#define TSG_ERR_INVALID (-1)
+#define TSG_ERR_CONFIG (-2)     /* ParseConfig error: yaml/regexp compile error */
+#define TSG_ERR_NO_DEVICE (-3)
+#define TSG_ERR_HIP (-4)
+#define TSG_ERR_INTERNAL (-5)
+
+typedef struct tsg_ruleset tsg_ruleset;
+typedef struct tsg_engine tsg_engine;
+typedef struct tsg_result tsg_result;
+
+/* One types.Line (misconf.go:51-60). */
+typedef struct tsg_line {
+  int64_t number;
+  const char* content; size_t content_len;
+  int32_t is_cause;
+  const char* annotation; size_t annotation_len;
+  int32_t truncated;
+  const char* highlighted; size_t highlighted_len;
+  int32_t first_cause;
+  int32_t last_cause;
+} tsg_line;
+
+/* One types.SecretFinding (secret.go:10-20); Layer is left to the caller. */
+typedef struct tsg_finding {
+  const char* rule_id; size_t rule_id_len;
+  const char* category; size_t category_len;
+  const char* severity; size_t severity_len;
+  const char* title; size_t title_len;
+  int64_t start_line;
+  int64_t end_line;
+  const char* match; size_t match_len;
+  uint32_t num_lines;
+} tsg_finding;
+
+typedef struct tsg_stats {
+  double k1_ms, k2_ms, h2d_ms, d2h_ms, host_ms, total_ms;
+  uint64_t bytes, files, hits, candidates, confirm_files, findings;
+  uint32_t k1_blocks, k1_threads, chunk_bytes;
+  int32_t table_in_lds;
+} tsg_stats;
+
+const char* tsg_last_error(void);
+const char* tsg_version(void);
+
+/* ParseConfig + NewScanner.  config_json: the trivy-secret.yaml document
+ * decoded to JSON with the YAML keys (rules, allow-rules, exclude-block,
+ * enable-builtin-rules, disable-rules, disable-allow-rules), or NULL for the
+ * builtin rules only (ParseConfig returned nil). */
+int tsg_ruleset_compile(const char* config_json, size_t config_len, tsg_ruleset** out);
+void tsg_ruleset_free(tsg_ruleset* rs);
+int tsg_ruleset_num_rules(const tsg_ruleset* rs);
+/* rule id of rule i (NUL-terminated, owned by rs) */
+const char* tsg_ruleset_rule_id(const tsg_ruleset* rs, int i);
+/* Global.AllowPath(path): 1 allowed, 0 not */
+int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t path_len);
+/* Compile report of the GPU prefilter (NUL-terminated, owned by the engine). */
+const char* tsg_engine_report(const tsg_engine* e);
+/* Builtin rule data as JSON (NUL-terminated, static). */
+const char* tsg_builtin_rules_json(void);
+
+int tsg_device_count(void);
+int tsg_engine_create(const tsg_ruleset* rs, int device, tsg_engine** out);
+void tsg_engine_destroy(tsg_engine* e);
+/* host worker threads for exact confirmation (0 = min(16, hardware)) */
+void tsg_engine_set_threads(tsg_engine* e, int threads);
+
+/* Pinned host buffers for the PCIe feed. */
+int tsg_alloc_pinned(size_t bytes, void** out);
+void tsg_free_pinned(void* p);
+
+/* Scan a batch of nfiles files packed back to back in `data`
+ * (offsets[0] = 0, offsets[nfiles] = total bytes).  paths[i] has length
+ * path_lens[i] (or is NUL-terminated when path_lens is NULL).  binary may be
+ * NULL (all false).  The batch is copied to HBM, scanned by the GPU kernels,
+ * and confirmed exactly on the host.  result[i] == Scanner.Scan(args[i]). */
+int tsg_scan_batch(tsg_engine* e, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                   const char* const* paths, const uint32_t* path_lens, const uint8_t* binary,
+                   tsg_result** out);
+/* Same, with the batch already resident in HBM at d_data (16-byte aligned,
+ * readable for 16 bytes past the end); h_data is the host copy used by the
+ * exact confirmer. */
+int tsg_scan_batch_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data,
+                            const uint64_t* offsets, uint32_t nfiles, const char* const* paths,
+                            const uint32_t* path_lens, const uint8_t* binary, tsg_result** out);
+/* Run only the two GPU passes; the result carries stats and candidates but no
+ * findings (used to time the kernels in isolation). */
+int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data,
+                           const uint64_t* offsets, uint32_t nfiles, tsg_result** out);
+
+uint32_t tsg_result_num_files(const tsg_result* r);
+/* types.Secret.FilePath of file i ("" for types.Secret{}) */
+int tsg_result_file_path(const tsg_result* r, uint32_t file, const char** path, size_t* len);
+uint32_t tsg_result_num_findings(const tsg_result* r, uint32_t file);
+int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_finding* out);
+int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out);
+/* nonzero when the reference would panic on this file (non-participating
+ * secret group, scanner.go:155-168 + 465-473) */
+int tsg_result_file_error(const tsg_result* r, uint32_t file);
+/* Whole result as a JSON array of types.Secret (Go field names); invalid
+ * UTF-8 bytes are written as \udcXX escapes.  Free with tsg_free. */
+int tsg_result_json(const tsg_result* r, char** json, size_t* len);
+int tsg_result_stats(const tsg_result* r, tsg_stats* out);
+/* Raw GPU candidates of file i for rule j (sorted starts); for tests. */
+int tsg_result_candidates(const tsg_result* r, uint32_t file, uint32_t rule, const uint64_t** starts, size_t* n);
+void tsg_result_free(tsg_result* r);
+void tsg_free(void* p);
+
+/* Host exact confirmer evaluated on every (file, rule) pair with no GPU
+ * prefilter (the reference algorithm restated in C++).  For tests of the
+ * confirmer; never used by tsg_scan_batch. */
+int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                            uint32_t nfiles, const char* const* paths, const uint32_t* path_lens,
+                            const uint8_t* binary, int threads, tsg_result** out);
+/* CPU model of the GPU tables (K1+K2 semantics) feeding the confirmer; for
+ * tests of the compiled prefilter without a GPU.  Never used by tsg_scan_batch. */
+int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                         uint32_t nfiles, const char* const* paths, const uint32_t* path_lens,
+                         const uint8_t* binary, tsg_result** out);
+/* Prefilter compile report without a GPU (NUL-terminated; free with tsg_free). */
+int tsg_prefilter_report(const tsg_ruleset* rs, char** out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRIVY_SECRET_H_ */

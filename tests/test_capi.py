@@ -1,0 +1,54 @@
+"""The C-ABI library loads and exports every entry point include/trivy_secret.h declares."""
+import ctypes
+import os
+import re
+
+from trivy_amd import _lib
+
+HDR = os.path.join(os.path.dirname(__file__), "..", "include", "trivy_secret.h")
+
+
+def declared_functions():
+    text = open(HDR).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tsg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(L, n), n
+    # and the ctypes signature table covers the header exactly
+    assert sorted(n for n, _, _ in _lib.SIGNATURES) == names
+
+
+def test_version_and_builtins():
+    L = _lib.lib()
+    assert b"gfx950" in L.tsg_version()
+    import json
+    rules = json.loads(L.tsg_builtin_rules_json().decode())["rules"]
+    assert len(rules) == 87
+
+
+def test_ruleset_compile_errors_are_reported():
+    L = _lib.lib()
+    rs = ctypes.c_void_p()
+    bad = b'{"rules": [{"id": "x", "regex": "a(b"}]}'
+    rc = L.tsg_ruleset_compile(bad, len(bad), ctypes.byref(rs))
+    assert rc == -2
+    assert b"regexp compile error" in L.tsg_last_error()
+
+
+def test_engine_create_without_gpu_fails_loudly():
+    L = _lib.lib()
+    if L.tsg_device_count() > 0:
+        return
+    rs = ctypes.c_void_p()
+    _lib.check(L.tsg_ruleset_compile(None, 0, ctypes.byref(rs)))
+    e = ctypes.c_void_p()
+    rc = L.tsg_engine_create(rs, 0, ctypes.byref(e))
+    assert rc == -3
+    assert b"no HIP device" in L.tsg_last_error()
+    L.tsg_ruleset_free(rs)

@@ -1,0 +1,43 @@
+"""CPU parity of the product's host pieces against the oracle on the
+reference's own test inputs (no GPU needed):
+  * the C++ exact confirmer run on every (file, rule) pair
+    (tsg_scan_host_reference), and
+  * the CPU model of the compiled GPU tables feeding the confirmer
+    (tsg_scan_table_model) -- the same plans the HIP kernels produce.
+Both must equal the reference's expected types.Secret exactly."""
+import json
+import os
+
+import pytest
+
+from trivy_amd import secret as S
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+SCANNER = json.load(open(os.path.join(G, "scanner_cases.json")))
+INTEG = json.load(open(os.path.join(G, "integration_cases.json")))
+CASES = [("scanner", c) for c in SCANNER] + [("integration", c) for c in INTEG]
+
+
+def _run(kind, case, mode):
+    cwd = os.getcwd()
+    os.chdir(os.path.join(G, kind))
+    try:
+        cfg = S.ParseConfig(case["config"])
+        content = open(case["input"], "rb").read().replace(b"\r", b"")
+        sc = S.Scanner(cfg)
+        args = [S.ScanArgs(case["path"], content)]
+        if mode == "host":
+            return S.scan_host_reference(sc, args)[0]
+        return S.scan_table_model(sc, args)[0]
+    finally:
+        os.chdir(cwd)
+
+
+@pytest.mark.parametrize("kind,case", CASES, ids=[c["name"] for _, c in CASES])
+def test_host_reference_matches_golden(kind, case):
+    assert _run(kind, case, "host") == case["want"]
+
+
+@pytest.mark.parametrize("kind,case", CASES, ids=[c["name"] for _, c in CASES])
+def test_table_model_matches_golden(kind, case):
+    assert _run(kind, case, "model") == case["want"]

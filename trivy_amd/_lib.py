@@ -1,0 +1,126 @@
+"""ctypes binding of libtrivysecret.so (include/trivy_secret.h).
+
+The library is built in-tree by trivy_amd/build.py; importing this module
+never builds or JIT-compiles anything and fails loudly when the .so is
+missing.
+"""
+import ctypes
+import json
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtrivysecret.so")
+
+c_char_pp = ctypes.POINTER(ctypes.c_char_p)
+
+
+class TsgStats(ctypes.Structure):
+    _fields_ = [("k1_ms", ctypes.c_double), ("k2_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("bytes", ctypes.c_uint64), ("files", ctypes.c_uint64), ("hits", ctypes.c_uint64),
+                ("candidates", ctypes.c_uint64), ("confirm_files", ctypes.c_uint64), ("findings", ctypes.c_uint64),
+                ("k1_blocks", ctypes.c_uint32), ("k1_threads", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
+                ("table_in_lds", ctypes.c_int32)]
+
+
+# (name, restype, argtypes) for every entry point declared in include/trivy_secret.h
+SIGNATURES = [
+    ("tsg_last_error", ctypes.c_char_p, []),
+    ("tsg_version", ctypes.c_char_p, []),
+    ("tsg_ruleset_compile", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_ruleset_free", None, [ctypes.c_void_p]),
+    ("tsg_ruleset_num_rules", ctypes.c_int, [ctypes.c_void_p]),
+    ("tsg_ruleset_rule_id", ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_int]),
+    ("tsg_ruleset_allow_path", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tsg_engine_report", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("tsg_builtin_rules_json", ctypes.c_char_p, []),
+    ("tsg_device_count", ctypes.c_int, []),
+    ("tsg_engine_create", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_engine_destroy", None, [ctypes.c_void_p]),
+    ("tsg_engine_set_threads", None, [ctypes.c_void_p, ctypes.c_int]),
+    ("tsg_alloc_pinned", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_free_pinned", None, [ctypes.c_void_p]),
+    ("tsg_scan_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                       c_char_pp, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_scan_batch_resident", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_uint32, c_char_pp, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prefilter_resident", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_result_num_files", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("tsg_result_file_path", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
+                                             ctypes.POINTER(ctypes.c_size_t)]),
+    ("tsg_result_num_findings", ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_uint32]),
+    ("tsg_result_finding", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    ("tsg_result_line", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p]),
+    ("tsg_result_file_error", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    ("tsg_result_json", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_size_t)]),
+    ("tsg_result_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TsgStats)]),
+    ("tsg_result_candidates", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
+    ("tsg_result_free", None, [ctypes.c_void_p]),
+    ("tsg_free", None, [ctypes.c_void_p]),
+    ("tsg_scan_host_reference", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                c_char_pp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_scan_table_model", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             c_char_pp, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prefilter_report", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libtrivysecret.so is not built (run __graft_entry__.build() or "
+                               "python -m trivy_amd.build); there is no fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class TsgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("tsg error %d: %s" % (code, msg))
+        self.code = code
+
+
+def check(rc):
+    if rc != 0:
+        raise TsgError(rc, lib().tsg_last_error().decode("utf-8", "replace"))
+
+
+def result_json(res):
+    """tsg_result -> list of types.Secret dicts (strings: surrogateescape'd)."""
+    L = lib()
+    buf = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    check(L.tsg_result_json(res, ctypes.byref(buf), ctypes.byref(n)))
+    try:
+        raw = ctypes.string_at(buf, n.value)
+    finally:
+        L.tsg_free(buf)
+    return json.loads(raw.decode("utf-8"))
+
+
+def result_stats(res):
+    st = TsgStats()
+    check(lib().tsg_result_stats(res, ctypes.byref(st)))
+    return {k: getattr(st, k) for k, _ in TsgStats._fields_}
+
+
+def pack_paths(paths):
+    enc = [p.encode("utf-8", "surrogateescape") if isinstance(p, str) else bytes(p) for p in paths]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    lens = (ctypes.c_uint32 * max(len(enc), 1))(*[len(e) for e in enc])
+    return arr, lens, enc

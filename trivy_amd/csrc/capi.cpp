@@ -1,0 +1,379 @@
+// C-ABI (include/trivy_secret.h) over the ruleset, the GPU engine and the
+// host confirmer.
+#include "../../include/trivy_secret.h"
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "engine.h"
+#include "prefilter.h"
+#include "scanner.h"
+
+using namespace tsg;
+
+extern "C" const char* tsg_builtin_json_ptr();   // scanner.cpp
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& m) { g_err = m; return code; }
+}  // namespace
+
+struct tsg_ruleset {
+  std::shared_ptr<Ruleset> rs;
+};
+
+struct tsg_engine {
+  std::unique_ptr<Engine> eng;
+  std::mutex mu;
+  std::string report;
+};
+
+struct tsg_result {
+  std::vector<Secret> files;
+  ScanStats stats;
+  std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
+};
+
+extern "C" {
+
+const char* tsg_last_error(void) { return g_err.c_str(); }
+const char* tsg_version(void) { return "trivy-secret-mi355x 0.1 (gfx950)"; }
+
+int tsg_ruleset_compile(const char* config_json, size_t config_len, tsg_ruleset** out) {
+  if (!out) return fail(TSG_ERR_INVALID, "out is NULL");
+  std::string err;
+  auto rs = std::make_shared<Ruleset>();
+  if (config_json) {
+    JValue cfg;
+    std::string text(config_json, config_len);
+    if (!json_parse(text, &cfg, &err)) return fail(TSG_ERR_CONFIG, "secrets config decode error: " + err);
+    if (!build_ruleset(cfg.is_null() ? nullptr : &cfg, rs.get(), &err)) return fail(TSG_ERR_CONFIG, err);
+  } else if (!build_ruleset(nullptr, rs.get(), &err)) {
+    return fail(TSG_ERR_CONFIG, err);
+  }
+  *out = new tsg_ruleset{rs};
+  return TSG_OK;
+}
+
+void tsg_ruleset_free(tsg_ruleset* rs) { delete rs; }
+
+int tsg_ruleset_num_rules(const tsg_ruleset* rs) { return rs ? static_cast<int>(rs->rs->rules.size()) : 0; }
+
+const char* tsg_ruleset_rule_id(const tsg_ruleset* rs, int i) {
+  if (!rs || i < 0 || i >= static_cast<int>(rs->rs->rules.size())) return nullptr;
+  return rs->rs->rules[i].id.c_str();
+}
+
+int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len) {
+  if (!rs) return fail(TSG_ERR_INVALID, "ruleset is NULL");
+  for (const auto& a : rs->rs->allow_rules) {
+    if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path), len)) return 1;
+  }
+  return 0;
+}
+
+int tsg_device_count(void) { return device_count(); }
+
+int tsg_engine_create(const tsg_ruleset* rs, int device, tsg_engine** out) {
+  if (!rs || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string err;
+  auto eng = Engine::create(rs->rs, device, &err);
+  if (!eng) return fail(device_count() <= 0 ? TSG_ERR_NO_DEVICE : TSG_ERR_HIP, err);
+  auto* e = new tsg_engine();
+  e->report = eng->prefilter().report;
+  e->eng = std::move(eng);
+  *out = e;
+  return TSG_OK;
+}
+
+void tsg_engine_destroy(tsg_engine* e) { delete e; }
+
+void tsg_engine_set_threads(tsg_engine* e, int threads) { if (e) e->eng->set_threads(threads); }
+
+const char* tsg_engine_report(const tsg_engine* e) { return e ? e->report.c_str() : ""; }
+
+int tsg_alloc_pinned(size_t bytes, void** out);
+void tsg_free_pinned(void* p);
+
+static int do_scan(tsg_engine* e, const void* d_data, const uint8_t* h_data, const uint64_t* offsets,
+                   uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, const uint8_t* binary,
+                   tsg_result** out) {
+  if (!e || !out || !offsets || (nfiles && !paths) || (!h_data && nfiles)) return fail(TSG_ERR_INVALID, "NULL argument");
+  BatchInput in;
+  in.h_data = h_data;
+  in.d_data = d_data;
+  in.offsets = offsets;
+  in.nfiles = nfiles;
+  in.paths = paths;
+  in.path_lens = path_lens;
+  in.binary = binary;
+  auto* r = new tsg_result();
+  std::string err;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->eng->scan(in, &r->files, &r->stats, &err)) { delete r; return fail(TSG_ERR_HIP, err); }
+  }
+  *out = r;
+  return TSG_OK;
+}
+
+int tsg_scan_batch(tsg_engine* e, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                   const char* const* paths, const uint32_t* path_lens, const uint8_t* binary, tsg_result** out) {
+  return do_scan(e, nullptr, data, offsets, nfiles, paths, path_lens, binary, out);
+}
+
+int tsg_scan_batch_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data, const uint64_t* offsets,
+                            uint32_t nfiles, const char* const* paths, const uint32_t* path_lens,
+                            const uint8_t* binary, tsg_result** out) {
+  if (!d_data) return fail(TSG_ERR_INVALID, "d_data is NULL");
+  return do_scan(e, d_data, h_data, offsets, nfiles, paths, path_lens, binary, out);
+}
+
+int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data, const uint64_t* offsets,
+                           uint32_t nfiles, tsg_result** out) {
+  if (!e || !out || !offsets) return fail(TSG_ERR_INVALID, "NULL argument");
+  BatchInput in;
+  in.h_data = h_data;
+  in.d_data = d_data;
+  in.offsets = offsets;
+  in.nfiles = nfiles;
+  auto* r = new tsg_result();
+  std::string err;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->eng->prefilter_only(in, nullptr, &r->cands, &r->stats, &err)) { delete r; return fail(TSG_ERR_HIP, err); }
+  }
+  r->files.resize(nfiles);
+  *out = r;
+  return TSG_OK;
+}
+
+uint32_t tsg_result_num_files(const tsg_result* r) { return r ? static_cast<uint32_t>(r->files.size()) : 0; }
+
+int tsg_result_file_path(const tsg_result* r, uint32_t f, const char** path, size_t* len) {
+  if (!r || f >= r->files.size()) return fail(TSG_ERR_INVALID, "file index out of range");
+  *path = r->files[f].file_path.data();
+  *len = r->files[f].file_path.size();
+  return TSG_OK;
+}
+
+uint32_t tsg_result_num_findings(const tsg_result* r, uint32_t f) {
+  if (!r || f >= r->files.size()) return 0;
+  return static_cast<uint32_t>(r->files[f].findings.size());
+}
+
+int tsg_result_file_error(const tsg_result* r, uint32_t f) {
+  if (!r || f >= r->files.size()) return 0;
+  return r->files[f].error;
+}
+
+int tsg_result_finding(const tsg_result* r, uint32_t f, uint32_t k, tsg_finding* out) {
+  if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
+  const Finding& x = r->files[f].findings[k];
+  out->rule_id = x.rule_id.data(); out->rule_id_len = x.rule_id.size();
+  out->category = x.category.data(); out->category_len = x.category.size();
+  out->severity = x.severity.data(); out->severity_len = x.severity.size();
+  out->title = x.title.data(); out->title_len = x.title.size();
+  out->start_line = x.start_line;
+  out->end_line = x.end_line;
+  out->match = x.match.data(); out->match_len = x.match.size();
+  out->num_lines = static_cast<uint32_t>(x.code.size());
+  return TSG_OK;
+}
+
+int tsg_result_line(const tsg_result* r, uint32_t f, uint32_t k, uint32_t l, tsg_line* out) {
+  if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
+  const Finding& x = r->files[f].findings[k];
+  if (l >= x.code.size()) return fail(TSG_ERR_INVALID, "line index out of range");
+  const Line& ln = x.code[l];
+  out->number = ln.number;
+  out->content = ln.content.data(); out->content_len = ln.content.size();
+  out->is_cause = ln.is_cause;
+  out->annotation = ln.annotation.data(); out->annotation_len = ln.annotation.size();
+  out->truncated = ln.truncated;
+  out->highlighted = ln.highlighted.data(); out->highlighted_len = ln.highlighted.size();
+  out->first_cause = ln.first_cause;
+  out->last_cause = ln.last_cause;
+  return TSG_OK;
+}
+
+static void json_str(std::string* o, const std::string& s) {
+  o->push_back('"');
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(s.data());
+  size_t i = 0, n = s.size();
+  char buf[16];
+  while (i < n) {
+    uint8_t c = p[i];
+    if (c < 0x80) {
+      if (c == '"') *o += "\\\"";
+      else if (c == '\\') *o += "\\\\";
+      else if (c == '\n') *o += "\\n";
+      else if (c == '\r') *o += "\\r";
+      else if (c == '\t') *o += "\\t";
+      else if (c < 0x20 || c == 0x7f) { snprintf(buf, sizeof buf, "\\u%04x", c); *o += buf; }
+      else o->push_back(static_cast<char>(c));
+      ++i;
+      continue;
+    }
+    int32_t r; int w;
+    re::decode_rune(p + i, n - i, &r, &w);
+    if (r == 0xFFFD && w == 1) { snprintf(buf, sizeof buf, "\\udc%02x", c); *o += buf; i += 1; continue; }
+    o->append(s, i, w);
+    i += w;
+  }
+  o->push_back('"');
+}
+
+int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
+  if (!r || !json) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string o = "[";
+  for (size_t f = 0; f < r->files.size(); ++f) {
+    const Secret& s = r->files[f];
+    if (f) o += ",";
+    o += "{\"FilePath\":";
+    json_str(&o, s.file_path);
+    o += ",\"Findings\":[";
+    for (size_t k = 0; k < s.findings.size(); ++k) {
+      const Finding& x = s.findings[k];
+      if (k) o += ",";
+      o += "{\"RuleID\":"; json_str(&o, x.rule_id);
+      o += ",\"Category\":"; json_str(&o, x.category);
+      o += ",\"Severity\":"; json_str(&o, x.severity);
+      o += ",\"Title\":"; json_str(&o, x.title);
+      o += ",\"StartLine\":" + std::to_string(x.start_line);
+      o += ",\"EndLine\":" + std::to_string(x.end_line);
+      o += ",\"Code\":{\"Lines\":[";
+      for (size_t l = 0; l < x.code.size(); ++l) {
+        const Line& ln = x.code[l];
+        if (l) o += ",";
+        o += "{\"Number\":" + std::to_string(ln.number);
+        o += ",\"Content\":"; json_str(&o, ln.content);
+        o += std::string(",\"IsCause\":") + (ln.is_cause ? "true" : "false");
+        o += ",\"Annotation\":"; json_str(&o, ln.annotation);
+        o += std::string(",\"Truncated\":") + (ln.truncated ? "true" : "false");
+        o += ",\"Highlighted\":"; json_str(&o, ln.highlighted);
+        o += std::string(",\"FirstCause\":") + (ln.first_cause ? "true" : "false");
+        o += std::string(",\"LastCause\":") + (ln.last_cause ? "true" : "false");
+        o += "}";
+      }
+      o += "]},\"Match\":";
+      json_str(&o, x.match);
+      o += "}";
+    }
+    o += "]";
+    if (s.error) o += ",\"Error\":1";
+    o += "}";
+  }
+  o += "]";
+  char* buf = static_cast<char*>(malloc(o.size() + 1));
+  if (!buf) return fail(TSG_ERR_INTERNAL, "out of memory");
+  memcpy(buf, o.data(), o.size());
+  buf[o.size()] = 0;
+  *json = buf;
+  if (len) *len = o.size();
+  return TSG_OK;
+}
+
+int tsg_result_stats(const tsg_result* r, tsg_stats* out) {
+  if (!r || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  const ScanStats& s = r->stats;
+  out->k1_ms = s.k1_ms; out->k2_ms = s.k2_ms; out->h2d_ms = s.h2d_ms; out->d2h_ms = s.d2h_ms;
+  out->host_ms = s.host_ms; out->total_ms = s.total_ms;
+  out->bytes = s.bytes; out->files = s.files; out->hits = s.hits; out->candidates = s.candidates;
+  out->confirm_files = s.confirm_files; out->findings = s.findings;
+  out->k1_blocks = s.k1_blocks; out->k1_threads = s.k1_threads; out->chunk_bytes = s.chunk_bytes;
+  out->table_in_lds = s.table_in_lds;
+  return TSG_OK;
+}
+
+int tsg_result_candidates(const tsg_result* r, uint32_t f, uint32_t rule, const uint64_t** starts, size_t* n) {
+  if (!r || f >= r->cands.size() || rule >= r->cands[f].size()) { *starts = nullptr; *n = 0; return TSG_OK; }
+  *starts = r->cands[f][rule].data();
+  *n = r->cands[f][rule].size();
+  return TSG_OK;
+}
+
+void tsg_result_free(tsg_result* r) { delete r; }
+void tsg_free(void* p) { free(p); }
+
+static std::string path_of(const char* const* paths, const uint32_t* lens, uint32_t i) {
+  return lens ? std::string(paths[i], lens[i]) : std::string(paths[i]);
+}
+
+int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                            const char* const* paths, const uint32_t* path_lens, const uint8_t* binary, int threads,
+                            tsg_result** out) {
+  if (!rs || !out || !offsets || (nfiles && (!paths || !data))) return fail(TSG_ERR_INVALID, "NULL argument");
+  auto* r = new tsg_result();
+  r->files.resize(nfiles);
+  std::atomic<uint32_t> next{0};
+  auto worker = [&]() {
+    for (;;) {
+      uint32_t f = next.fetch_add(1);
+      if (f >= nfiles) break;
+      r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), data + offsets[f], offsets[f + 1] - offsets[f],
+                              binary ? binary[f] != 0 : false, nullptr);
+    }
+  };
+  int nt = threads > 0 ? threads : 1;
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
+  worker();
+  for (auto& t : pool) t.join();
+  *out = r;
+  return TSG_OK;
+}
+
+int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                         const char* const* paths, const uint32_t* path_lens, const uint8_t* binary,
+                         tsg_result** out) {
+  if (!rs || !out || !offsets || (nfiles && (!paths || !data))) return fail(TSG_ERR_INVALID, "NULL argument");
+  Prefilter pf;
+  std::string err;
+  if (!build_prefilter(*rs->rs, &pf, &err)) return fail(TSG_ERR_INTERNAL, err);
+  auto* r = new tsg_result();
+  r->files.resize(nfiles);
+  r->cands.resize(nfiles);
+  const size_t nr = rs->rs->rules.size();
+  for (uint32_t f = 0; f < nfiles; ++f) {
+    const uint8_t* c = data + offsets[f];
+    const size_t len = offsets[f + 1] - offsets[f];
+    std::vector<uint8_t> gate;
+    const bool special = prefilter_reference_file(pf, c, len, &r->cands[f], &gate);
+    if (special) {
+      r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, nullptr);
+      continue;
+    }
+    FilePlan plan;
+    plan.kind.assign(nr, kPlanNoMatch);
+    for (size_t k = 0; k < nr; ++k) {
+      const RuleGpuInfo& gi = pf.rules[k];
+      if (gi.mode == 1) plan.kind[k] = kPlanFull;
+      else if (gi.mode == 0 && !r->cands[f][k].empty()) {
+        plan.kind[k] = gi.gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
+        plan.cands.push_back({static_cast<uint32_t>(k), r->cands[f][k]});
+      }
+    }
+    r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, &plan);
+  }
+  *out = r;
+  return TSG_OK;
+}
+
+int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
+  if (!rs || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  Prefilter pf;
+  std::string err;
+  if (!build_prefilter(*rs->rs, &pf, &err)) return fail(TSG_ERR_INTERNAL, err);
+  char* buf = static_cast<char*>(malloc(pf.report.size() + 1));
+  memcpy(buf, pf.report.c_str(), pf.report.size() + 1);
+  *out = buf;
+  return TSG_OK;
+}
+
+const char* tsg_builtin_rules_json(void) { return tsg_builtin_json_ptr(); }
+
+}  // extern "C"

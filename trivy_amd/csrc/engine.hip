@@ -1,0 +1,589 @@
+// MI355X (gfx950) secret-scanning engine: two HIP kernels + host driver.
+//
+// K1  tsg_k1_scan    one streaming pass over the packed batch in HBM.  Each
+//                    thread owns a CHUNK of bytes (16-byte vector loads),
+//                    warms its DFA state up over the preceding
+//                    (max_pattern_bytes-1) bytes of the same file, then steps
+//                    the LDS-resident scan DFA (keyword + anchor literals,
+//                    uint16 transitions over byte classes) byte by byte.
+//                    Keyword outputs set per-(file, keyword) bits (exact
+//                    bytes.ToLower gate, scanner.go:174-186); anchor outputs
+//                    append a 64-bit hit (end offset << 24 | anchor id).  It
+//                    also counts '\n' per chunk (newline prefix for line
+//                    numbers).  Memory-bound target: HBM, 1 byte read per
+//                    content byte.
+// K2  tsg_k2_verify  one thread per anchor hit: keyword gate of the hit's
+//                    rule, then the rule's anchored relaxed verify DFA (L2
+//                    resident) from every possible match start in the
+//                    anchor's offset window.  Accepting starts become
+//                    (file, rule, start) candidates for the host confirmer.
+// No MFMA anywhere: this path is byte/integer automaton work.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "engine.h"
+
+namespace tsg {
+
+namespace {
+
+constexpr uint32_t kBlock = 1024;              // one K1 workgroup per CU: 16 waves share the LDS table
+constexpr uint32_t kChunk = 2048;              // bytes per thread-chunk (multiple of 16)
+constexpr uint32_t kLdsTableMax = 140 * 1024;  // scan table bytes kept in LDS (160 KiB per CU)
+
+struct AnchorDev { uint32_t rule, min_len, max_len, dmin, dmax; };
+struct RuleDev { uint32_t mode, gate_on_gpu, always_gate, kw_begin, kw_count, verify_dfa, verify_limit, pad; };
+struct VDfaDev { uint32_t next_off, acc_off, cls_off, nclasses, dead, pad0, pad1, pad2; };
+struct CandDev { uint32_t file, rule; unsigned long long start; };
+
+#define HIP_OK(expr)                                                              \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      if (err) *err = std::string(#expr) + ": " + hipGetErrorString(e_);          \
+      return false;                                                               \
+    }                                                                             \
+  } while (0)
+
+__device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, uint32_t nfiles, uint64_t pos) {
+  // largest f with off[f] <= pos, then skip empty files (off[f+1] == off[f])
+  uint32_t lo = 0, hi = nfiles;   // search in off[0..nfiles]
+  while (lo < hi) {
+    uint32_t m = (lo + hi + 1) >> 1;
+    if (off[m] <= pos) lo = m; else hi = m - 1;
+  }
+  uint32_t f = lo;
+  while (f < nfiles && off[f + 1] <= pos) ++f;
+  return f;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void tsg_k1_scan(
+    const uint8_t* __restrict__ data, unsigned long long total,
+    const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
+    uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
+    const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_ids, uint32_t nkw,
+    uint32_t warmup, unsigned long long nchunks,
+    uint32_t* __restrict__ kwbits, uint32_t kw_words,
+    unsigned long long* __restrict__ hits, unsigned int* __restrict__ counters, uint32_t hit_cap,
+    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint16_t* next = g_next;
+  const uint8_t* cls = g_cls;
+  if (kLds) {
+    uint16_t* s_next = reinterpret_cast<uint16_t*>(smem);
+    const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
+    uint8_t* s_cls = smem + padded;
+    const uint4* src = reinterpret_cast<const uint4*>(g_next);
+    uint4* dst = reinterpret_cast<uint4*>(s_next);
+    for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = g_cls[i];
+    __syncthreads();
+    next = s_next;
+    cls = s_cls;
+  }
+  const unsigned long long stride = static_cast<unsigned long long>(gridDim.x) * blockDim.x;
+  for (unsigned long long c = static_cast<unsigned long long>(blockIdx.x) * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
+    const unsigned long long c0 = c * kChunk;
+    const unsigned long long c1 = min(c0 + kChunk, total);
+    uint32_t f = file_of(offsets, nfiles, c0);
+    unsigned long long fstart = offsets[f], fend = offsets[f + 1];
+    uint32_t s = 0;
+    unsigned long long p = (c0 - fstart > warmup) ? c0 - warmup : fstart;
+    uint32_t p1 = 0, p2 = 0;   // previous two bytes (fold-special detection)
+    for (; p < c0; ++p) {
+      const uint32_t b = data[p];
+      s = next[s * nclasses + cls[b]];
+      p2 = p1;
+      p1 = b;
+    }
+    uint32_t nl = 0;
+    uint32_t last_kw = 0xffffffffu, last_kw_file = 0xffffffffu;
+    for (p = c0; p < c1; p += 16) {
+      const uint4 v = *reinterpret_cast<const uint4*>(data + p);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const unsigned long long q = p + k;
+        if (q >= c1) break;
+        if (q >= fend) {
+          do { ++f; fstart = fend; fend = offsets[f + 1]; } while (q >= fend);
+          s = 0;
+          p1 = p2 = 0;
+        }
+        const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+        nl += (b == 0x0au);
+        if (b & 0x80u) {
+          // U+0130 / U+017F / U+212A fold onto ASCII letters: the ASCII-only
+          // scan DFA cannot see them, so the file goes to the exact host path
+          if ((b == 0xB0u && p1 == 0xC4u) || (b == 0xBFu && p1 == 0xC5u) || (b == 0xAAu && p1 == 0x84u && p2 == 0xE2u))
+            atomicOr(&fflags[f], 1u);
+        }
+        p2 = p1;
+        p1 = b;
+        s = next[s * nclasses + cls[b]];
+        if (s >= first_out) {
+          const uint32_t o = s - first_out;
+          for (uint32_t j = out_off[o]; j < out_off[o + 1]; ++j) {
+            const uint32_t id = out_ids[j];
+            if (id < nkw) {
+              if (id == last_kw && f == last_kw_file) continue;
+              last_kw = id;
+              last_kw_file = f;
+              uint32_t* word = kwbits + static_cast<size_t>(f) * kw_words + (id >> 5);
+              const uint32_t bit = 1u << (id & 31);
+              if (!(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(word, bit);
+            } else {
+              const unsigned int idx = atomicAdd(&counters[0], 1u);
+              if (idx < hit_cap) hits[idx] = (q << 24) | (id - nkw);
+            }
+          }
+        }
+      }
+    }
+    nl_count[c] = nl;
+  }
+}
+
+__global__ __launch_bounds__(256) void tsg_k2_verify(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const unsigned long long* __restrict__ hits, uint32_t nhits,
+    const AnchorDev* __restrict__ anchors, const RuleDev* __restrict__ rules,
+    const uint32_t* __restrict__ rule_kw, const uint32_t* __restrict__ kwbits, uint32_t kw_words,
+    const VDfaDev* __restrict__ vd, const uint16_t* __restrict__ v_next,
+    const uint8_t* __restrict__ v_acc, const uint8_t* __restrict__ v_cls,
+    CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nhits; i += stride) {
+    const unsigned long long h = hits[i];
+    const unsigned long long q = h >> 24;
+    const AnchorDev an = anchors[h & 0xffffffu];
+    const RuleDev r = rules[an.rule];
+    const uint32_t f = file_of(offsets, nfiles, q);
+    if (!r.always_gate && r.gate_on_gpu) {
+      uint32_t g = 0;
+      for (uint32_t k = 0; k < r.kw_count && !g; ++k) {
+        const uint32_t id = rule_kw[r.kw_begin + k];
+        g = (kwbits[static_cast<size_t>(f) * kw_words + (id >> 5)] >> (id & 31)) & 1u;
+      }
+      if (!g) continue;
+    }
+    const long long fstart = static_cast<long long>(offsets[f]);
+    const long long fend = static_cast<long long>(offsets[f + 1]);
+    long long hi = static_cast<long long>(q) + 1 - an.min_len - an.dmin;
+    long long lo = static_cast<long long>(q) + 1 - an.max_len - an.dmax;
+    if (lo < fstart) lo = fstart;
+    const VDfaDev d = vd[r.verify_dfa];
+    const uint16_t* nx = v_next + d.next_off;
+    const uint8_t* acc = v_acc + d.acc_off;
+    const uint8_t* cl = v_cls + d.cls_off;
+    for (long long s = lo; s <= hi; ++s) {
+      uint32_t st = 0;
+      bool ok = acc[0] != 0;
+      long long p = s;
+      const long long lim = min(fend, s + static_cast<long long>(r.verify_limit));
+      for (; !ok && p < lim; ++p) {
+        st = nx[st * d.nclasses + cl[data[p]]];
+        if (acc[st]) ok = true;
+        else if (st == d.dead) break;
+      }
+      if (!ok && st != d.dead && p < fend && p >= lim) ok = true;   // gave up: conservative
+      if (ok) {
+        const unsigned int idx = atomicAdd(&counters[1], 1u);
+        if (idx < cand_cap) {
+          cands[idx].file = f;
+          cands[idx].rule = an.rule;
+          cands[idx].start = static_cast<unsigned long long>(s - fstart);
+        }
+      }
+    }
+  }
+}
+
+template <typename T>
+bool dev_upload(const std::vector<T>& v, T** out, std::string* err) {
+  size_t n = std::max<size_t>(v.size(), 1) * sizeof(T);
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(out), n + 16));
+  HIP_OK(hipMemset(*out, 0, n + 16));
+  if (!v.empty()) HIP_OK(hipMemcpy(*out, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return true;
+}
+
+template <typename T>
+bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
+  if (*cap >= n && *p) return true;
+  if (*p) HIP_OK(hipFree(*p));
+  *p = nullptr;
+  size_t want = std::max<size_t>(n, 1);
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(p), want * sizeof(T) + 64));
+  *cap = want;
+  return true;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+struct Engine::Impl {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  // tables
+  uint16_t* scan_next = nullptr;
+  uint8_t* scan_cls = nullptr;
+  uint32_t* out_off = nullptr;
+  uint32_t* out_ids = nullptr;
+  AnchorDev* anchors = nullptr;
+  RuleDev* rules = nullptr;
+  uint32_t* rule_kw = nullptr;
+  VDfaDev* vdfa = nullptr;
+  uint16_t* v_next = nullptr;
+  uint8_t* v_acc = nullptr;
+  uint8_t* v_cls = nullptr;
+  uint32_t table_words16 = 0;
+  bool table_in_lds = false;
+  uint32_t kw_words = 1;
+  // batch buffers
+  uint8_t* d_data = nullptr; size_t d_data_cap = 0;
+  uint64_t* d_off = nullptr; size_t d_off_cap = 0;
+  uint32_t* d_kw = nullptr; size_t d_kw_cap = 0;
+  unsigned long long* d_hits = nullptr; size_t d_hits_cap = 0;
+  CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
+  uint32_t* d_nl = nullptr; size_t d_nl_cap = 0;
+  uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
+  unsigned int* d_cnt = nullptr;
+  size_t hit_cap = 1 << 20, cand_cap = 1 << 18;
+  // last batch results (host)
+  std::vector<CandDev> h_cands;
+  std::vector<uint32_t> h_nl;
+  std::vector<uint32_t> h_kw;
+  std::vector<uint32_t> h_ff;
+  int sms = 256;
+};
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int device, std::string* err) {
+  int n = device_count();
+  if (n <= 0) { *err = "no HIP device available (the GPU engine has no CPU fallback)"; return nullptr; }
+  if (device < 0 || device >= n) { *err = "HIP device index out of range"; return nullptr; }
+  std::unique_ptr<Engine> e(new Engine());
+  e->rs_ = std::move(rs);
+  e->device_ = device;
+  if (!build_prefilter(*e->rs_, &e->pf_, err)) return nullptr;
+  e->impl_.reset(new Impl());
+  Impl& m = *e->impl_;
+  if (hipSetDevice(device) != hipSuccess) { *err = "hipSetDevice failed"; return nullptr; }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) m.sms = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess) { *err = "hipStreamCreate failed"; return nullptr; }
+  for (auto& ev : m.ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
+  const Prefilter& pf = e->pf_;
+  // scan table (padded to 16 B for vector LDS fill)
+  std::vector<uint16_t> sn = pf.scan.t.next;
+  m.table_words16 = static_cast<uint32_t>(sn.size());
+  sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
+  m.table_in_lds = static_cast<size_t>(m.table_words16) * 2 <= kLdsTableMax;
+  std::vector<uint8_t> cls(pf.scan.t.byte_class, pf.scan.t.byte_class + 256);
+  std::vector<AnchorDev> an;
+  for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
+  std::vector<RuleDev> rd;
+  for (const auto& r : pf.rules) rd.push_back({r.mode, r.gate_on_gpu, r.always_gate, r.kw_begin, r.kw_count, r.verify_dfa, r.verify_limit, 0});
+  std::vector<VDfaDev> vd;
+  std::vector<uint16_t> vn;
+  std::vector<uint8_t> va, vc;
+  for (const auto& t : pf.verify) {
+    VDfaDev d{};
+    d.next_off = static_cast<uint32_t>(vn.size());
+    d.acc_off = static_cast<uint32_t>(va.size());
+    d.cls_off = static_cast<uint32_t>(vc.size());
+    d.nclasses = t.nclasses;
+    d.dead = t.dead;
+    vn.insert(vn.end(), t.next.begin(), t.next.end());
+    va.insert(va.end(), t.accept.begin(), t.accept.end());
+    vc.insert(vc.end(), t.byte_class, t.byte_class + 256);
+    vd.push_back(d);
+  }
+  m.kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
+  if (!dev_upload(sn, &m.scan_next, err) || !dev_upload(cls, &m.scan_cls, err) ||
+      !dev_upload(pf.scan.out_off, &m.out_off, err) || !dev_upload(pf.scan.out_ids, &m.out_ids, err) ||
+      !dev_upload(an, &m.anchors, err) || !dev_upload(rd, &m.rules, err) ||
+      !dev_upload(pf.rule_kw, &m.rule_kw, err) || !dev_upload(vd, &m.vdfa, err) ||
+      !dev_upload(vn, &m.v_next, err) || !dev_upload(va, &m.v_acc, err) || !dev_upload(vc, &m.v_cls, err)) {
+    return nullptr;
+  }
+  if (hipMalloc(&m.d_cnt, 64) != hipSuccess) { *err = "hipMalloc counters failed"; return nullptr; }
+  return e;
+}
+
+Engine::~Engine() {
+  if (!impl_) return;
+  Impl& m = *impl_;
+  hipSetDevice(device_);
+  void* ps[] = {m.scan_next, m.scan_cls, m.out_off, m.out_ids, m.anchors, m.rules, m.rule_kw, m.vdfa,
+                m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw, m.d_hits, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
+  for (void* p : ps) if (p) hipFree(p);
+  for (auto& ev : m.ev) if (ev) hipEventDestroy(ev);
+  if (m.stream) hipStreamDestroy(m.stream);
+}
+
+bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
+  Impl& m = *impl_;
+  HIP_OK(hipSetDevice(device_));
+  const uint64_t total = in.offsets[in.nfiles] - in.offsets[0];
+  if (in.offsets[0] != 0) { *err = "offsets[0] must be 0"; return false; }
+  for (uint32_t i = 0; i < in.nfiles; ++i) {
+    if (in.offsets[i + 1] < in.offsets[i]) { *err = "offsets must be non-decreasing"; return false; }
+  }
+  st->bytes = total;
+  st->files = in.nfiles;
+  st->chunk_bytes = kChunk;
+  const uint8_t* d_data = static_cast<const uint8_t*>(in.d_data);
+  auto t_h2d = std::chrono::steady_clock::now();
+  if (!d_data) {
+    if (!ensure(&m.d_data, &m.d_data_cap, total + 64, err)) return false;
+    if (total) HIP_OK(hipMemcpyAsync(m.d_data, in.h_data, total, hipMemcpyHostToDevice, m.stream));
+    HIP_OK(hipMemsetAsync(m.d_data + total, 0, 64, m.stream));
+    d_data = m.d_data;
+  } else if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) {
+    *err = "device data must be 16-byte aligned";
+    return false;
+  }
+  if (!ensure(&m.d_off, &m.d_off_cap, in.nfiles + 1, err)) return false;
+  HIP_OK(hipMemcpyAsync(m.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, m.stream));
+  const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * m.kw_words;
+  if (!ensure(&m.d_kw, &m.d_kw_cap, kw_n, err)) return false;
+  const unsigned long long nchunks = (total + kChunk - 1) / kChunk;
+  if (!ensure(&m.d_nl, &m.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
+  if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
+  if (!ensure(&m.d_ff, &m.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
+  HIP_OK(hipStreamSynchronize(m.stream));
+  st->h2d_ms = in.d_data ? 0.0 : ms_since(t_h2d);
+
+  const uint32_t sms = static_cast<uint32_t>(m.sms);
+  const Prefilter& pf = pf_;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_OK(hipMemsetAsync(m.d_kw, 0, kw_n * sizeof(uint32_t), m.stream));
+    HIP_OK(hipMemsetAsync(m.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), m.stream));
+    HIP_OK(hipMemsetAsync(m.d_cnt, 0, 64, m.stream));
+    uint64_t want_blocks = (nchunks + kBlock - 1) / kBlock;
+    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * 8ull)));
+    const uint32_t warm = pf.scan.max_pattern_bytes > 0 ? pf.scan.max_pattern_bytes - 1 : 0;
+    const size_t lds = m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 : 0;
+    st->k1_blocks = blocks;
+    st->k1_threads = kBlock;
+    st->table_in_lds = m.table_in_lds;
+    HIP_OK(hipEventRecord(m.ev[0], m.stream));
+    if (nchunks > 0) {
+      if (m.table_in_lds) {
+        hipLaunchKernelGGL(tsg_k1_scan<true>, dim3(blocks), dim3(kBlock), lds, m.stream,
+                           d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
+                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state, m.out_off, m.out_ids,
+                           pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
+                           static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
+      } else {
+        hipLaunchKernelGGL(tsg_k1_scan<false>, dim3(blocks), dim3(kBlock), 0, m.stream,
+                           d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
+                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state, m.out_off, m.out_ids,
+                           pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
+                           static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
+      }
+      HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipEventRecord(m.ev[1], m.stream));
+    unsigned int cnt[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(cnt, m.d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, m.stream));
+    HIP_OK(hipStreamSynchronize(m.stream));
+    float k1 = 0;
+    HIP_OK(hipEventElapsedTime(&k1, m.ev[0], m.ev[1]));
+    st->k1_ms += k1;
+    if (cnt[0] > m.hit_cap) {                          // hit buffer overflow: grow, rerun K1
+      m.hit_cap = static_cast<size_t>(cnt[0]) * 5 / 4 + 1024;
+      if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
+      continue;
+    }
+    st->hits = cnt[0];
+    // K2 (re-run only if the candidate buffer overflows)
+    for (int a2 = 0; a2 < 3; ++a2) {
+      if (!ensure(&m.d_cands, &m.d_cands_cap, m.cand_cap, err)) return false;
+      HIP_OK(hipMemsetAsync(m.d_cnt + 1, 0, 4, m.stream));
+      HIP_OK(hipEventRecord(m.ev[2], m.stream));
+      if (cnt[0] > 0) {
+        uint32_t b2 = static_cast<uint32_t>(std::min<uint64_t>((cnt[0] + 255) / 256, sms * 16ull));
+        hipLaunchKernelGGL(tsg_k2_verify, dim3(b2), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles, m.d_hits,
+                           cnt[0], m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
+                           m.v_cls, m.d_cands, m.d_cnt, static_cast<uint32_t>(m.cand_cap));
+        HIP_OK(hipGetLastError());
+      }
+      HIP_OK(hipEventRecord(m.ev[3], m.stream));
+      unsigned int c2 = 0;
+      HIP_OK(hipMemcpyAsync(&c2, m.d_cnt + 1, 4, hipMemcpyDeviceToHost, m.stream));
+      HIP_OK(hipStreamSynchronize(m.stream));
+      float k2 = 0;
+      HIP_OK(hipEventElapsedTime(&k2, m.ev[2], m.ev[3]));
+      st->k2_ms += k2;
+      if (c2 > m.cand_cap) { m.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
+      auto t_d2h = std::chrono::steady_clock::now();
+      m.h_cands.resize(c2);
+      if (c2) HIP_OK(hipMemcpyAsync(m.h_cands.data(), m.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, m.stream));
+      m.h_ff.resize(in.nfiles);
+      if (in.nfiles) HIP_OK(hipMemcpyAsync(m.h_ff.data(), m.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+      m.h_nl.resize(nchunks);
+      if (nchunks) HIP_OK(hipMemcpyAsync(m.h_nl.data(), m.d_nl, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+      HIP_OK(hipStreamSynchronize(m.stream));
+      st->d2h_ms += ms_since(t_d2h);
+      st->candidates = c2;
+      return true;
+    }
+    *err = "candidate buffer overflow persisted";
+    return false;
+  }
+  *err = "hit buffer overflow persisted";
+  return false;
+}
+
+bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
+                            std::vector<std::vector<std::vector<uint64_t>>>* cands, ScanStats* st,
+                            std::string* err) {
+  ScanStats local;
+  if (!st) st = &local;
+  if (!run_gpu(in, st, err)) return false;
+  Impl& m = *impl_;
+  const size_t nr = pf_.rules.size();
+  if (kw_gate) {
+    m.h_kw.resize(static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * m.kw_words);
+    HIP_OK(hipMemcpy(m.h_kw.data(), m.d_kw, m.h_kw.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    kw_gate->assign(static_cast<size_t>(in.nfiles) * nr, 0);
+    for (uint32_t f = 0; f < in.nfiles; ++f) {
+      for (size_t r = 0; r < nr; ++r) {
+        const RuleGpuInfo& gi = pf_.rules[r];
+        uint8_t g = gi.always_gate;
+        for (uint32_t k = 0; k < gi.kw_count && !g; ++k) {
+          uint32_t id = pf_.rule_kw[gi.kw_begin + k];
+          g = (m.h_kw[static_cast<size_t>(f) * m.kw_words + (id >> 5)] >> (id & 31)) & 1u;
+        }
+        (*kw_gate)[static_cast<size_t>(f) * nr + r] = g;
+      }
+    }
+  }
+  if (cands) {
+    cands->assign(in.nfiles, std::vector<std::vector<uint64_t>>(nr));
+    for (const CandDev& c : m.h_cands) (*cands)[c.file][c.rule].push_back(c.start);
+    for (auto& f : *cands)
+      for (auto& v : f) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); }
+  }
+  return true;
+}
+
+bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* st, std::string* err) {
+  ScanStats local;
+  if (!st) st = &local;
+  auto t0 = std::chrono::steady_clock::now();
+  if (!run_gpu(in, st, err)) return false;
+  auto t_host = std::chrono::steady_clock::now();
+  Impl& m = *impl_;
+  const Ruleset& rs = *rs_;
+  const size_t nr = rs.rules.size();
+  // group candidates per file (counting sort by file, then sort each file's list)
+  std::vector<uint32_t> per_file(in.nfiles + 1, 0);
+  for (const CandDev& c : m.h_cands) per_file[c.file + 1]++;
+  for (uint32_t f = 0; f < in.nfiles; ++f) per_file[f + 1] += per_file[f];
+  std::vector<CandDev> sorted(m.h_cands.size());
+  {
+    std::vector<uint32_t> pos(per_file.begin(), per_file.end() - 1);
+    for (const CandDev& c : m.h_cands) sorted[pos[c.file]++] = c;
+  }
+  bool any_full = false;
+  for (const auto& gi : pf_.rules) if (gi.mode == 1) any_full = true;
+  results->assign(in.nfiles, Secret());
+  std::vector<uint32_t> work;
+  for (uint32_t f = 0; f < in.nfiles; ++f) work.push_back(f);
+  std::atomic<uint32_t> next{0};
+  std::atomic<uint64_t> nfind{0}, nconf{0};
+  auto worker = [&]() {
+    FilePlan plan;
+    for (;;) {
+      uint32_t wi = next.fetch_add(1);
+      if (wi >= work.size()) break;
+      uint32_t f = work[wi];
+      std::string path = in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]);
+      const uint8_t* content = in.h_data + in.offsets[f];
+      const size_t len = in.offsets[f + 1] - in.offsets[f];
+      const bool binary = in.binary ? in.binary[f] != 0 : false;
+      const uint32_t cb = per_file[f], ce = per_file[f + 1];
+      if (m.h_ff[f]) {
+        // fold-special file: exact host evaluation of every rule
+        nconf.fetch_add(1);
+        Secret s = scan_file(rs, path, content, len, binary, nullptr);
+        nfind.fetch_add(s.findings.size());
+        (*results)[f] = std::move(s);
+        continue;
+      }
+      if (cb == ce && !any_full) {
+        // no candidates, no host-evaluated rule: only the global allow-path outcome remains
+        Secret s;
+        for (const auto& a : rs.allow_rules) {
+          if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) { s.file_path = path; break; }
+        }
+        (*results)[f] = std::move(s);
+        continue;
+      }
+      nconf.fetch_add(1);
+      plan.kind.assign(nr, kPlanNoMatch);
+      plan.cands.clear();
+      for (size_t r = 0; r < nr; ++r) {
+        const RuleGpuInfo& gi = pf_.rules[r];
+        if (gi.mode == 1) plan.kind[r] = kPlanFull;
+      }
+      std::sort(sorted.begin() + cb, sorted.begin() + ce, [](const CandDev& a, const CandDev& b) {
+        return a.rule != b.rule ? a.rule < b.rule : a.start < b.start;
+      });
+      for (uint32_t k = cb; k < ce;) {
+        uint32_t r = sorted[k].rule;
+        RuleCandidates rc;
+        rc.rule = r;
+        while (k < ce && sorted[k].rule == r) {
+          if (rc.starts.empty() || rc.starts.back() != sorted[k].start) rc.starts.push_back(sorted[k].start);
+          ++k;
+        }
+        plan.kind[r] = pf_.rules[r].gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
+        plan.cands.push_back(std::move(rc));
+      }
+      Secret s = scan_file(rs, path, content, len, binary, &plan);
+      nfind.fetch_add(s.findings.size());
+      (*results)[f] = std::move(s);
+    }
+  };
+  int nt = threads_ > 0 ? threads_ : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
+  worker();
+  for (auto& t : pool) t.join();
+  st->host_ms = ms_since(t_host);
+  st->confirm_files = nconf.load();
+  st->findings = nfind.load();
+  st->total_ms = ms_since(t0);
+  return true;
+}
+
+}  // namespace tsg
+
+extern "C" int tsg_alloc_pinned(size_t bytes, void** out) {
+  if (!out) return -1;
+  return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? 0 : -4;
+}
+
+extern "C" void tsg_free_pinned(void* p) {
+  if (p) hipHostFree(p);
+}

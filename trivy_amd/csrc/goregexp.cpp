@@ -1,0 +1,1042 @@
+// Go regexp semantics restated in C++ -- see goregexp.h for the contract and
+// the Go sources each part follows (regexp/syntax parse.go, simplify.go,
+// compile.go; regexp/exec.go, regexp.go allMatches).
+#include "goregexp.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+
+namespace tsg {
+namespace re {
+
+namespace {
+#include "unicode_tables.inc"
+
+constexpr uint32_t kMaxRune = 0x10FFFF;
+constexpr int kMaxRepeat = 1000;
+
+bool lookup_pair(const uint32_t (*tab)[2], size_t n, uint32_t r, uint32_t* out) {
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (tab[m][0] == r) { *out = tab[m][1]; return true; }
+    if (tab[m][0] < r) lo = m + 1; else hi = m;
+  }
+  return false;
+}
+
+void add_range(std::vector<Range>* v, uint32_t lo, uint32_t hi) { v->push_back({lo, hi}); }
+
+void normalize(std::vector<Range>* v) {
+  std::sort(v->begin(), v->end(), [](const Range& a, const Range& b) { return a.lo < b.lo; });
+  std::vector<Range> out;
+  for (const Range& r : *v) {
+    if (!out.empty() && r.lo <= out.back().hi + 1) {
+      out.back().hi = std::max(out.back().hi, r.hi);
+    } else {
+      out.push_back(r);
+    }
+  }
+  *v = std::move(out);
+}
+
+void negate(std::vector<Range>* v) {
+  normalize(v);
+  std::vector<Range> out;
+  uint32_t next = 0;
+  for (const Range& r : *v) {
+    if (r.lo > next) out.push_back({next, r.lo - 1});
+    next = r.hi + 1;
+  }
+  if (next <= kMaxRune) out.push_back({next, kMaxRune});
+  *v = std::move(out);
+}
+
+// Add every SimpleFold orbit member of every rune in [lo,hi] (appendFoldedRange).
+void add_folded(std::vector<Range>* v, uint32_t lo, uint32_t hi) {
+  add_range(v, lo, hi);
+  const size_t n = sizeof(kFoldOrbit) / sizeof(kFoldOrbit[0]);
+  // kFoldOrbit is sorted by rune; walk the entries inside [lo,hi]
+  size_t a = 0, b = n;
+  while (a < b) {
+    size_t m = (a + b) / 2;
+    if (kFoldOrbit[m][0] < lo) a = m + 1; else b = m;
+  }
+  for (size_t k = a; k < n && kFoldOrbit[k][0] <= hi; ++k) {
+    uint32_t r = kFoldOrbit[k][0];
+    for (uint32_t f = kFoldOrbit[k][1]; f != r;) {
+      add_range(v, f, f);
+      uint32_t nx;
+      if (!lookup_pair(kFoldOrbit, n, f, &nx)) break;
+      f = nx;
+    }
+  }
+}
+
+bool is_word(int32_t r) {
+  return (r >= '0' && r <= '9') || (r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z') || r == '_';
+}
+
+// syntax.EmptyOpContext(r1, r2)
+uint8_t empty_context(int32_t r1, int32_t r2) {
+  uint8_t op = kEmptyNoWordBoundary;
+  int boundary = 0;
+  if (is_word(r1)) boundary = 1;
+  else if (r1 == '\n') op |= kEmptyBeginLine;
+  else if (r1 < 0) op |= kEmptyBeginText | kEmptyBeginLine;
+  if (is_word(r2)) boundary ^= 1;
+  else if (r2 == '\n') op |= kEmptyEndLine;
+  else if (r2 < 0) op |= kEmptyEndText | kEmptyEndLine;
+  if (boundary) op ^= (kEmptyWordBoundary | kEmptyNoWordBoundary);
+  return op;
+}
+
+// Rune before position pos: only ASCII word chars / '\n' matter for contexts,
+// so a non-ASCII predecessor is reported as U+FFFD (never word, never '\n').
+int32_t rune_before(const uint8_t* s, size_t pos) {
+  if (pos == 0) return -1;
+  uint8_t c = s[pos - 1];
+  return c < 0x80 ? c : 0xFFFD;
+}
+
+// ------------------------------------------------------------------ parser
+struct Flags { bool i = false, m = false, s = false, U = false; };
+
+std::unique_ptr<Node> mk(Op op) { auto n = std::make_unique<Node>(); n->op = op; return n; }
+
+class Parser {
+ public:
+  Parser(const std::string& p) : p_(p) {}
+  std::unique_ptr<Node> parse(std::string* err, std::vector<std::string>* names) {
+    names_.push_back("");
+    Flags f;
+    auto n = alternation(&f);
+    if (err_.empty() && i_ < p_.size()) err_ = "unexpected ): `" + p_ + "`";
+    if (!err_.empty()) { *err = "error parsing regexp: " + err_; return nullptr; }
+    *names = names_;
+    return n;
+  }
+
+ private:
+  const std::string& p_;
+  size_t i_ = 0;
+  std::string err_;
+  int ncap_ = 0;
+  std::vector<std::string> names_;
+
+  bool eof() const { return i_ >= p_.size(); }
+  char peek(size_t k = 0) const { return i_ + k < p_.size() ? p_[i_ + k] : '\0'; }
+  void fail(const std::string& m) { if (err_.empty()) err_ = m; }
+
+  uint32_t next_rune() {
+    int32_t r; int w;
+    decode_rune(reinterpret_cast<const uint8_t*>(p_.data()) + i_, p_.size() - i_, &r, &w);
+    if (r == 0xFFFD && w == 1) fail("invalid UTF-8: `" + p_ + "`");
+    i_ += w;
+    return static_cast<uint32_t>(r);
+  }
+
+  std::unique_ptr<Node> alternation(Flags* f) {
+    std::vector<std::unique_ptr<Node>> alts;
+    alts.push_back(concat(f));
+    while (err_.empty() && peek() == '|') {
+      ++i_;
+      alts.push_back(concat(f));
+    }
+    if (alts.size() == 1) return std::move(alts[0]);
+    auto n = mk(Op::Alternate);
+    n->sub = std::move(alts);
+    return n;
+  }
+
+  std::unique_ptr<Node> concat(Flags* f) {
+    auto n = mk(Op::Concat);
+    while (err_.empty() && !eof() && peek() != '|' && peek() != ')') {
+      auto a = atom(f);
+      if (!err_.empty()) break;
+      if (!a) continue;   // flag group (?i)
+      a = repeat(std::move(a), *f);
+      n->sub.push_back(std::move(a));
+    }
+    if (n->sub.size() == 1) return std::move(n->sub[0]);
+    if (n->sub.empty()) return mk(Op::EmptyMatch);
+    return n;
+  }
+
+  bool try_brace(int* lo, int* hi) {
+    size_t j = i_ + 1, k = j;
+    while (k < p_.size() && isdigit(static_cast<unsigned char>(p_[k]))) ++k;
+    if (k == j) return false;
+    if (k - j > 8) { fail("invalid repeat count"); return false; }
+    *lo = std::stoi(p_.substr(j, k - j));
+    *hi = *lo;
+    if (k < p_.size() && p_[k] == ',') {
+      ++k;
+      size_t m = k;
+      while (m < p_.size() && isdigit(static_cast<unsigned char>(p_[m]))) ++m;
+      if (m - k > 8) { fail("invalid repeat count"); return false; }
+      *hi = m > k ? std::stoi(p_.substr(k, m - k)) : -1;
+      k = m;
+    }
+    if (k >= p_.size() || p_[k] != '}') return false;
+    i_ = k + 1;
+    return true;
+  }
+
+  std::unique_ptr<Node> repeat(std::unique_ptr<Node> a, const Flags& f) {
+    bool seen = false;
+    for (;;) {
+      char c = peek();
+      Op op;
+      int lo = 0, hi = 0;
+      size_t save = i_;
+      if (c == '*') { op = Op::Star; ++i_; }
+      else if (c == '+') { op = Op::Plus; ++i_; }
+      else if (c == '?') { op = Op::Quest; ++i_; }
+      else if (c == '{') {
+        if (!try_brace(&lo, &hi)) { if (err_.empty()) i_ = save; return a; }
+        if (lo > kMaxRepeat || hi > kMaxRepeat || (hi >= 0 && hi < lo)) {
+          fail("invalid repeat count: `" + p_.substr(save, i_ - save) + "`");
+          return a;
+        }
+        op = Op::Repeat;
+      } else {
+        return a;
+      }
+      if (seen) { fail("invalid nested repetition operator: `" + p_.substr(save, i_ - save) + "`"); return a; }
+      seen = true;
+      bool ng = false;
+      if (peek() == '?') { ++i_; ng = true; }
+      if (f.U) ng = !ng;
+      auto n = mk(op);
+      n->nongreedy = ng;
+      n->min = lo;
+      n->max = hi;
+      n->sub.push_back(std::move(a));
+      a = std::move(n);
+    }
+  }
+
+  std::unique_ptr<Node> literal(uint32_t r, const Flags& f) {
+    if (f.i) {
+      std::vector<uint32_t> orb = fold_orbit(r);
+      if (orb.size() > 1) {
+        auto n = mk(Op::CharClass);
+        for (uint32_t x : orb) add_range(&n->ranges, x, x);
+        normalize(&n->ranges);
+        return n;
+      }
+    }
+    auto n = mk(Op::Literal);
+    n->rune = r;
+    return n;
+  }
+
+  std::unique_ptr<Node> atom(Flags* f) {
+    char c = peek();
+    if (c == '(') return group(f);
+    if (c == '[') return char_class(*f);
+    if (c == '*' || c == '+' || c == '?') { fail("missing argument to repetition operator: `" + std::string(1, c) + "`"); return nullptr; }
+    if (c == '{') {
+      size_t save = i_;
+      int lo, hi;
+      if (try_brace(&lo, &hi)) { fail("missing argument to repetition operator"); return nullptr; }
+      i_ = save + 1;
+      return literal('{', *f);
+    }
+    if (c == '.') {
+      ++i_;
+      return mk(f->s ? Op::AnyChar : Op::AnyCharNotNL);
+    }
+    if (c == '^') { ++i_; return mk(f->m ? Op::BeginLine : Op::BeginText); }
+    if (c == '$') { ++i_; return mk(f->m ? Op::EndLine : Op::EndText); }
+    if (c == '\\') return escape(*f);
+    return literal(next_rune(), *f);
+  }
+
+  std::unique_ptr<Node> group(Flags* f) {
+    ++i_;  // '('
+    std::string name;
+    bool named = false;
+    if (peek() == '?') {
+      if (p_.compare(i_, 3, "?P<") == 0 || (p_.compare(i_, 2, "?<") == 0 && peek(2) != '=' && peek(2) != '!')) {
+        size_t start = i_ + (peek(1) == 'P' ? 3 : 2);
+        size_t end = p_.find('>', start);
+        if (end == std::string::npos) { fail("invalid named capture: `" + p_ + "`"); return nullptr; }
+        name = p_.substr(start, end - start);
+        bool ok = !name.empty();
+        for (char ch : name) ok = ok && (isalnum(static_cast<unsigned char>(ch)) || ch == '_');
+        if (!ok) { fail("invalid named capture: `" + p_ + "`"); return nullptr; }
+        named = true;
+        i_ = end + 1;
+      } else {
+        ++i_;
+        Flags nf = *f;
+        bool neg = false, sawflag = false;
+        for (;;) {
+          if (eof()) { fail("missing closing ): `" + p_ + "`"); return nullptr; }
+          char ch = p_[i_++];
+          if (ch == 'i' || ch == 'm' || ch == 's' || ch == 'U') {
+            bool v = !neg;
+            if (ch == 'i') nf.i = v; else if (ch == 'm') nf.m = v; else if (ch == 's') nf.s = v; else nf.U = v;
+            sawflag = true;
+          } else if (ch == '-') {
+            if (neg) { fail("invalid or unsupported Perl syntax: `" + p_ + "`"); return nullptr; }
+            neg = true;
+            sawflag = false;
+          } else if (ch == ')' || ch == ':') {
+            if (neg && !sawflag) { fail("invalid or unsupported Perl syntax: `" + p_ + "`"); return nullptr; }
+            if (ch == ')') { *f = nf; return nullptr; }
+            auto inner = alternation(&nf);
+            if (peek() != ')') { fail("missing closing ): `" + p_ + "`"); return nullptr; }
+            ++i_;
+            return inner;
+          } else {
+            fail("invalid or unsupported Perl syntax: `" + p_ + "`");
+            return nullptr;
+          }
+        }
+      }
+    }
+    int cap = ++ncap_;
+    names_.push_back(named ? name : "");
+    Flags inner_flags = *f;
+    auto inner = alternation(&inner_flags);
+    if (peek() != ')') { fail("missing closing ): `" + p_ + "`"); return nullptr; }
+    ++i_;
+    auto n = mk(Op::Capture);
+    n->cap = cap;
+    n->name = name;
+    n->sub.push_back(std::move(inner));
+    return n;
+  }
+
+  bool escape_rune(uint32_t* out) {
+    if (eof()) { fail("trailing backslash at end of expression"); return false; }
+    char c = p_[i_++];
+    if (c >= '1' && c <= '7') {
+      if (!(peek() >= '0' && peek() <= '7')) { fail("invalid escape sequence: `\\" + std::string(1, c) + "`"); return false; }
+    }
+    if (c >= '0' && c <= '7') {
+      uint32_t v = c - '0';
+      for (int k = 0; k < 2 && peek() >= '0' && peek() <= '7'; ++k) v = v * 8 + (p_[i_++] - '0');
+      *out = v;
+      return true;
+    }
+    if (c == 'x') {
+      if (peek() == '{') {
+        size_t end = p_.find('}', i_);
+        if (end == std::string::npos || end == i_ + 1) { fail("invalid escape sequence"); return false; }
+        uint32_t v = 0;
+        for (size_t k = i_ + 1; k < end; ++k) {
+          char h = p_[k];
+          if (!isxdigit(static_cast<unsigned char>(h))) { fail("invalid escape sequence"); return false; }
+          v = v * 16 + (isdigit(static_cast<unsigned char>(h)) ? h - '0' : (tolower(h) - 'a' + 10));
+          if (v > kMaxRune) { fail("invalid escape sequence"); return false; }
+        }
+        i_ = end + 1;
+        *out = v;
+        return true;
+      }
+      if (i_ + 2 > p_.size() || !isxdigit(static_cast<unsigned char>(p_[i_])) || !isxdigit(static_cast<unsigned char>(p_[i_ + 1]))) {
+        fail("invalid escape sequence");
+        return false;
+      }
+      *out = static_cast<uint32_t>(std::stoul(p_.substr(i_, 2), nullptr, 16));
+      i_ += 2;
+      return true;
+    }
+    switch (c) {
+      case 'a': *out = 7; return true;
+      case 'f': *out = 12; return true;
+      case 'n': *out = 10; return true;
+      case 'r': *out = 13; return true;
+      case 't': *out = 9; return true;
+      case 'v': *out = 11; return true;
+    }
+    if (static_cast<unsigned char>(c) < 0x80 && !isalnum(static_cast<unsigned char>(c))) { *out = static_cast<uint8_t>(c); return true; }
+    fail(std::string("invalid escape sequence: `\\") + c + "`");
+    return false;
+  }
+
+  // Go parser.appendGroup: the group is case folded under (?i) first, then
+  // negated for \D \S \W / [:^name:].
+  static void perl_class(char k, bool fold, std::vector<Range>* v) {
+    std::vector<Range> tmp;
+    switch (tolower(k)) {
+      case 'd': add_range(&tmp, '0', '9'); break;
+      case 's': add_range(&tmp, '\t', '\n'); add_range(&tmp, '\f', '\r'); add_range(&tmp, ' ', ' '); break;
+      case 'w': add_range(&tmp, '0', '9'); add_range(&tmp, 'A', 'Z'); add_range(&tmp, 'a', 'z'); add_range(&tmp, '_', '_'); break;
+    }
+    group_into(tmp, fold, isupper(static_cast<unsigned char>(k)), v);
+  }
+
+  static void group_into(const std::vector<Range>& g, bool fold, bool neg, std::vector<Range>* v) {
+    std::vector<Range> tmp;
+    if (fold) { for (const Range& r : g) add_folded(&tmp, r.lo, r.hi); }
+    else tmp = g;
+    if (neg) negate(&tmp); else normalize(&tmp);
+    v->insert(v->end(), tmp.begin(), tmp.end());
+  }
+
+  bool posix_class(const std::string& name, std::vector<Range>* v) {
+    struct P { const char* n; const char* r; };
+    static const P tab[] = {
+      {"alnum", "09AZaz"}, {"alpha", "AZaz"}, {"ascii", "\x01\x7f"}, {"blank", "\t\t  "},
+      {"cntrl", "\x01\x1f\x7f\x7f"}, {"digit", "09"}, {"graph", "!~"}, {"lower", "az"},
+      {"print", " ~"}, {"punct", "!/:@[`{~"}, {"space", "\t\r  "}, {"upper", "AZ"},
+      {"word", "09AZ__az"}, {"xdigit", "09AFaf"}};
+    for (const P& p : tab) {
+      if (name == p.n) {
+        const char* r = p.r;
+        size_t len = strlen(r);
+        for (size_t k = 0; k + 1 < len; k += 2) add_range(v, static_cast<uint8_t>(r[k]), static_cast<uint8_t>(r[k + 1]));
+        if (name == "ascii" || name == "cntrl") add_range(v, 0, 0);  // \x00 can't live in a C string
+        return true;
+      }
+    }
+    return false;
+  }
+
+  bool unicode_class(char pc, bool fold, std::vector<Range>* v) {
+    std::string name;
+    if (peek() == '{') {
+      size_t end = p_.find('}', i_);
+      if (end == std::string::npos) { fail("invalid character class range"); return false; }
+      name = p_.substr(i_ + 1, end - i_ - 1);
+      i_ = end + 1;
+    } else {
+      if (eof()) { fail("invalid character class range"); return false; }
+      name = std::string(1, p_[i_++]);
+    }
+    bool neg = pc == 'P';
+    if (!name.empty() && name[0] == '^') { neg = !neg; name = name.substr(1); }
+    std::vector<Range> tmp;
+    if (name == "Any") {
+      add_range(&tmp, 0, kMaxRune);
+    } else {
+      bool found = false;
+      for (const CatTable& t : kCats) {
+        if (name == t.name) {
+          for (size_t k = 0; k < t.n; ++k) add_range(&tmp, t.r[k][0], t.r[k][1]);
+          found = true;
+          break;
+        }
+      }
+      if (!found) { fail("invalid character class range: `\\p{" + name + "}` (unsupported)"); return false; }
+    }
+    group_into(tmp, fold, neg, v);
+    return true;
+  }
+
+  std::unique_ptr<Node> escape(const Flags& f) {
+    ++i_;  // '\\'
+    char c = peek();
+    if (c == 'd' || c == 's' || c == 'w' || c == 'D' || c == 'S' || c == 'W') {
+      ++i_;
+      auto n = mk(Op::CharClass);
+      perl_class(c, f.i, &n->ranges);
+      normalize(&n->ranges);
+      return n;
+    }
+    if (c == 'p' || c == 'P') {
+      ++i_;
+      auto n = mk(Op::CharClass);
+      if (!unicode_class(c, f.i, &n->ranges)) return nullptr;
+      normalize(&n->ranges);
+      return n;
+    }
+    if (c == 'A') { ++i_; return mk(Op::BeginText); }
+    if (c == 'z') { ++i_; return mk(Op::EndText); }
+    if (c == 'b') { ++i_; return mk(Op::WordBoundary); }
+    if (c == 'B') { ++i_; return mk(Op::NoWordBoundary); }
+    if (c == 'Q') {
+      ++i_;
+      size_t end = p_.find("\\E", i_);
+      std::string lit = end == std::string::npos ? p_.substr(i_) : p_.substr(i_, end - i_);
+      i_ = end == std::string::npos ? p_.size() : end + 2;
+      auto n = mk(Op::Concat);
+      size_t k = 0;
+      while (k < lit.size()) {
+        int32_t r; int w;
+        decode_rune(reinterpret_cast<const uint8_t*>(lit.data()) + k, lit.size() - k, &r, &w);
+        k += w;
+        n->sub.push_back(literal(static_cast<uint32_t>(r), f));
+      }
+      if (n->sub.size() == 1) return std::move(n->sub[0]);
+      if (n->sub.empty()) return mk(Op::EmptyMatch);
+      return n;
+    }
+    uint32_t r;
+    if (!escape_rune(&r)) return nullptr;
+    return literal(r, f);
+  }
+
+  bool class_rune(uint32_t* r) {
+    if (peek() == '\\') { ++i_; return escape_rune(r); }
+    *r = next_rune();
+    return err_.empty();
+  }
+
+  std::unique_ptr<Node> char_class(const Flags& f) {
+    ++i_;  // '['
+    bool neg = false;
+    if (peek() == '^') { neg = true; ++i_; }
+    std::vector<Range> cls;
+    bool first = true;
+    auto add = [&](uint32_t lo, uint32_t hi) {
+      if (f.i) add_folded(&cls, lo, hi); else add_range(&cls, lo, hi);
+    };
+    while (first || peek() != ']') {
+      if (eof()) { fail("missing closing ]: `" + p_ + "`"); return nullptr; }
+      first = false;
+      if (peek() == '[' && peek(1) == ':') {
+        size_t end = p_.find(":]", i_ + 2);
+        if (end != std::string::npos) {
+          std::string name = p_.substr(i_ + 2, end - i_ - 2);
+          bool pneg = !name.empty() && name[0] == '^';
+          if (pneg) name = name.substr(1);
+          std::vector<Range> tmp;
+          if (!posix_class(name, &tmp)) { fail("invalid character class range: `[:" + name + ":]`"); return nullptr; }
+          group_into(tmp, f.i, pneg, &cls);
+          i_ = end + 2;
+          continue;
+        }
+      }
+      if (peek() == '\\' && strchr("dswDSW", peek(1)) && peek(1) != '\0') {
+        perl_class(peek(1), f.i, &cls);
+        i_ += 2;
+        continue;
+      }
+      if (peek() == '\\' && (peek(1) == 'p' || peek(1) == 'P')) {
+        char pc = peek(1);
+        i_ += 2;
+        if (!unicode_class(pc, f.i, &cls)) return nullptr;
+        continue;
+      }
+      uint32_t lo;
+      if (!class_rune(&lo)) return nullptr;
+      uint32_t hi = lo;
+      if (peek() == '-' && peek(1) != ']' && peek(1) != '\0') {
+        ++i_;
+        if (!class_rune(&hi)) return nullptr;
+        if (hi < lo) { fail("invalid character class range"); return nullptr; }
+      }
+      add(lo, hi);
+    }
+    ++i_;  // ']'
+    if (neg) negate(&cls); else normalize(&cls);
+    auto n = mk(Op::CharClass);
+    n->ranges = std::move(cls);
+    return n;
+  }
+};
+
+// ---------------------------------------------------------------- simplify
+std::unique_ptr<Node> clone(const Node& n) {
+  auto c = std::make_unique<Node>();
+  c->op = n.op; c->nongreedy = n.nongreedy; c->rune = n.rune; c->ranges = n.ranges;
+  c->min = n.min; c->max = n.max; c->cap = n.cap; c->name = n.name;
+  for (const auto& s : n.sub) c->sub.push_back(clone(*s));
+  return c;
+}
+
+std::unique_ptr<Node> simplify1(Op op, bool ng, std::unique_ptr<Node> sub) {
+  if (sub->op == Op::EmptyMatch) return sub;
+  if (sub->op == op && sub->nongreedy == ng) return sub;
+  auto n = mk(op);
+  n->nongreedy = ng;
+  n->sub.push_back(std::move(sub));
+  return n;
+}
+
+std::unique_ptr<Node> simplify(std::unique_ptr<Node> n) {
+  for (auto& s : n->sub) s = simplify(std::move(s));
+  switch (n->op) {
+    case Op::Star: case Op::Plus: case Op::Quest:
+      return simplify1(n->op, n->nongreedy, std::move(n->sub[0]));
+    case Op::Repeat: {
+      const Node& sub = *n->sub[0];
+      int mn = n->min, mx = n->max;
+      bool ng = n->nongreedy;
+      if (mn == 0 && mx == 0) return mk(Op::EmptyMatch);
+      if (mx == -1) {
+        if (mn == 0) return simplify1(Op::Star, ng, clone(sub));
+        if (mn == 1) return simplify1(Op::Plus, ng, clone(sub));
+        auto c = mk(Op::Concat);
+        for (int k = 0; k < mn - 1; ++k) c->sub.push_back(clone(sub));
+        c->sub.push_back(simplify1(Op::Plus, ng, clone(sub)));
+        return c;
+      }
+      if (mn == 1 && mx == 1) return clone(sub);
+      std::unique_ptr<Node> prefix;
+      if (mn > 0) {
+        prefix = mk(Op::Concat);
+        for (int k = 0; k < mn; ++k) prefix->sub.push_back(clone(sub));
+      }
+      if (mx > mn) {
+        auto suffix = simplify1(Op::Quest, ng, clone(sub));
+        for (int k = mn + 1; k < mx; ++k) {
+          auto c = mk(Op::Concat);
+          c->sub.push_back(clone(sub));
+          c->sub.push_back(std::move(suffix));
+          suffix = simplify1(Op::Quest, ng, std::move(c));
+        }
+        if (!prefix) return suffix;
+        prefix->sub.push_back(std::move(suffix));
+      }
+      if (prefix) return prefix;
+      return mk(Op::NoMatch);
+    }
+    default:
+      return n;
+  }
+}
+
+// ----------------------------------------------------------------- compile
+struct Frag {
+  uint32_t i = 0;
+  std::vector<uint32_t> out;   // patch list: (inst << 1) | is_arg
+  bool nullable = false;
+};
+
+class Compiler {
+ public:
+  Prog* p;
+  explicit Compiler(Prog* prog) : p(prog) { inst(IOp::Fail); }
+
+  uint32_t inst(IOp op) {
+    Inst in;
+    in.op = op;
+    p->inst.push_back(in);
+    return static_cast<uint32_t>(p->inst.size() - 1);
+  }
+  void patch(const std::vector<uint32_t>& l, uint32_t to) {
+    for (uint32_t x : l) {
+      if (x & 1) p->inst[x >> 1].arg = to; else p->inst[x >> 1].out = to;
+    }
+  }
+  static std::vector<uint32_t> cat_list(std::vector<uint32_t> a, const std::vector<uint32_t>& b) {
+    a.insert(a.end(), b.begin(), b.end());
+    return a;
+  }
+
+  Frag nop() { Frag f; f.i = inst(IOp::Nop); f.out = {f.i << 1}; f.nullable = true; return f; }
+  Frag fail() { Frag f; return f; }
+  Frag empty(uint8_t flags) {
+    Frag f; f.i = inst(IOp::Empty); p->inst[f.i].arg = flags; f.out = {f.i << 1}; f.nullable = true; return f;
+  }
+  Frag cap(uint32_t slot) {
+    Frag f; f.i = inst(IOp::Capture); p->inst[f.i].arg = slot; f.out = {f.i << 1}; f.nullable = true;
+    if (static_cast<int>(slot) + 1 > p->num_cap * 2 + 2) {}
+    return f;
+  }
+  Frag rune(const std::vector<Range>& rs) {
+    Frag f;
+    if (rs.size() == 1 && rs[0].lo == rs[0].hi) {
+      f.i = inst(IOp::Rune1);
+      p->inst[f.i].arg = rs[0].lo;
+    } else if (rs.size() == 1 && rs[0].lo == 0 && rs[0].hi == kMaxRune) {
+      f.i = inst(IOp::RuneAny);
+    } else if (rs.size() == 2 && rs[0].lo == 0 && rs[0].hi == 9 && rs[1].lo == 11 && rs[1].hi == kMaxRune) {
+      f.i = inst(IOp::RuneAnyNotNL);
+    } else {
+      f.i = inst(IOp::Rune);
+    }
+    Inst& in = p->inst[f.i];
+    in.rbeg = static_cast<uint32_t>(p->ranges.size());
+    in.rcnt = static_cast<uint32_t>(rs.size());
+    for (const Range& r : rs) {
+      p->ranges.push_back(r);
+      for (uint32_t c = r.lo; c <= std::min<uint32_t>(r.hi, 127); ++c) in.ascii[c >> 6] |= 1ull << (c & 63);
+      if (r.hi >= 0x80) in.nonascii = true;
+    }
+    f.out = {f.i << 1};
+    return f;
+  }
+  Frag cat(Frag f1, Frag f2) {
+    if (f1.i == 0 || f2.i == 0) return fail();
+    patch(f1.out, f2.i);
+    Frag f; f.i = f1.i; f.out = std::move(f2.out); f.nullable = f1.nullable && f2.nullable;
+    return f;
+  }
+  Frag alt(Frag f1, Frag f2) {
+    if (f1.i == 0) return f2;
+    if (f2.i == 0) return f1;
+    Frag f; f.i = inst(IOp::Alt);
+    p->inst[f.i].out = f1.i;
+    p->inst[f.i].arg = f2.i;
+    f.out = cat_list(std::move(f1.out), f2.out);
+    f.nullable = f1.nullable || f2.nullable;
+    return f;
+  }
+  Frag quest(Frag f1, bool ng) {
+    Frag f; f.i = inst(IOp::Alt); f.nullable = true;
+    if (ng) { p->inst[f.i].arg = f1.i; f.out = {f.i << 1}; }
+    else { p->inst[f.i].out = f1.i; f.out = {(f.i << 1) | 1}; }
+    f.out = cat_list(std::move(f.out), f1.out);
+    return f;
+  }
+  Frag loop(Frag f1, bool ng) {
+    Frag f; f.i = inst(IOp::Alt);
+    if (ng) { p->inst[f.i].arg = f1.i; f.out = {f.i << 1}; }
+    else { p->inst[f.i].out = f1.i; f.out = {(f.i << 1) | 1}; }
+    patch(f1.out, f.i);
+    f.nullable = f1.nullable;
+    return f;
+  }
+  Frag star(Frag f1, bool ng) {
+    if (f1.nullable) return quest(plus(f1, ng), ng);
+    return loop(f1, ng);
+  }
+  Frag plus(Frag f1, bool ng) {
+    uint32_t start = f1.i;
+    bool nl = f1.nullable;
+    Frag l = loop(std::move(f1), ng);
+    Frag f; f.i = start; f.out = std::move(l.out); f.nullable = nl;
+    return f;
+  }
+
+  Frag compile(const Node& n) {
+    switch (n.op) {
+      case Op::NoMatch: return fail();
+      case Op::EmptyMatch: return nop();
+      case Op::Literal: return rune({{n.rune, n.rune}});
+      case Op::CharClass: return rune(n.ranges);
+      case Op::AnyCharNotNL: return rune({{0, 9}, {11, kMaxRune}});
+      case Op::AnyChar: return rune({{0, kMaxRune}});
+      case Op::BeginLine: return empty(kEmptyBeginLine);
+      case Op::EndLine: return empty(kEmptyEndLine);
+      case Op::BeginText: return empty(kEmptyBeginText);
+      case Op::EndText: return empty(kEmptyEndText);
+      case Op::WordBoundary: return empty(kEmptyWordBoundary);
+      case Op::NoWordBoundary: return empty(kEmptyNoWordBoundary);
+      case Op::Capture: {
+        Frag bra = cap(static_cast<uint32_t>(n.cap << 1));
+        Frag sub = compile(*n.sub[0]);
+        Frag ket = cap(static_cast<uint32_t>((n.cap << 1) | 1));
+        return cat(cat(std::move(bra), std::move(sub)), std::move(ket));
+      }
+      case Op::Star: return star(compile(*n.sub[0]), n.nongreedy);
+      case Op::Plus: return plus(compile(*n.sub[0]), n.nongreedy);
+      case Op::Quest: return quest(compile(*n.sub[0]), n.nongreedy);
+      case Op::Concat: {
+        if (n.sub.empty()) return nop();
+        Frag f;
+        for (size_t k = 0; k < n.sub.size(); ++k) {
+          if (k == 0) f = compile(*n.sub[k]); else f = cat(std::move(f), compile(*n.sub[k]));
+        }
+        return f;
+      }
+      case Op::Alternate: {
+        Frag f;
+        for (const auto& s : n.sub) f = alt(std::move(f), compile(*s));
+        return f;
+      }
+      case Op::Repeat: break;  // removed by simplify
+    }
+    return fail();
+  }
+};
+
+int max_cap(const Node& n) {
+  int m = n.op == Op::Capture ? n.cap : 0;
+  for (const auto& s : n.sub) m = std::max(m, max_cap(*s));
+  return m;
+}
+
+// ----------------------------------------------------------------- Pike VM
+inline bool rune_match(const Prog& p, const Inst& in, int32_t c) {
+  if (c < 0) return false;
+  if (c < 128) return (in.ascii[c >> 6] >> (c & 63)) & 1;
+  if (!in.nonascii) return false;
+  const Range* r = &p.ranges[in.rbeg];
+  uint32_t lo = 0, hi = in.rcnt;
+  uint32_t uc = static_cast<uint32_t>(c);
+  while (lo < hi) {
+    uint32_t m = (lo + hi) / 2;
+    if (uc < r[m].lo) hi = m;
+    else if (uc > r[m].hi) lo = m + 1;
+    else return true;
+  }
+  return false;
+}
+
+class Machine {
+ public:
+  Machine(const Prog& p, int ncap) : p_(p), ncap_(ncap) {
+    size_t n = p.inst.size();
+    for (int q = 0; q < 2; ++q) {
+      sparse_[q].assign(n, 0);
+      dense_pc_[q].assign(n, 0);
+      dense_has_[q].assign(n, 0);
+      caps_[q].assign(n * std::max(ncap, 1), -1);
+      size_[q] = 0;
+    }
+    matchcap_.assign(std::max(ncap, 1), -1);
+    scratch_.assign(std::max(ncap, 1), -1);
+    stack_.reserve(64);
+  }
+
+  bool match(const uint8_t* s, size_t len, size_t pos0, bool anchored, int* caps_out) {
+    matched_ = false;
+    std::fill(matchcap_.begin(), matchcap_.end(), -1);
+    int rq = 0, nq = 1;
+    size_[0] = size_[1] = 0;
+    size_t pos = pos0;
+    int32_t r, r1 = -1;
+    int w, w1 = 0;
+    decode_rune(s + pos, len - pos, &r, &w);
+    if (r >= 0) decode_rune(s + pos + w, len - pos - w, &r1, &w1);
+    uint8_t flag = pos == 0 ? empty_context(-1, r) : empty_context(rune_before(s, pos), r);
+    for (;;) {
+      if (size_[rq] == 0) {
+        if (anchored && pos != pos0) break;
+        if (matched_) break;
+      }
+      if (!matched_ && (!anchored || pos == pos0)) {
+        if (ncap_ > 0) {
+          std::fill(scratch_.begin(), scratch_.end(), -1);
+          scratch_[0] = static_cast<int>(pos);
+        }
+        add(rq, p_.start, pos, scratch_.data(), flag);
+      }
+      uint8_t nflag = empty_context(r, r1);
+      step(rq, nq, pos, pos + w, r, nflag);
+      if (w == 0) break;
+      if (ncap_ == 0 && matched_) break;
+      pos += w;
+      r = r1; w = w1;
+      if (r >= 0) decode_rune(s + pos + w, len - pos - w, &r1, &w1);
+      else { r1 = -1; w1 = 0; }
+      flag = nflag;
+      std::swap(rq, nq);
+    }
+    size_[nq] = 0;
+    if (matched_ && caps_out) std::copy(matchcap_.begin(), matchcap_.begin() + ncap_, caps_out);
+    return matched_;
+  }
+
+ private:
+  const Prog& p_;
+  int ncap_;
+  std::vector<uint32_t> sparse_[2], dense_pc_[2];
+  std::vector<uint8_t> dense_has_[2];
+  std::vector<int> caps_[2];
+  uint32_t size_[2];
+  std::vector<int> matchcap_, scratch_;
+  bool matched_ = false;
+  struct Frame { uint32_t pc; int slot; int old; };
+  std::vector<Frame> stack_;
+
+  bool contains(int q, uint32_t pc) const {
+    uint32_t j = sparse_[q][pc];
+    return j < size_[q] && dense_pc_[q][j] == pc;
+  }
+
+  // Go machine.add: DFS in priority order; capture slots restored on unwind.
+  void add(int q, uint32_t pc0, size_t pos, int* cap, uint8_t cond) {
+    // explicit stack: entries are either (pc) to visit or a capture-restore
+    stack_.clear();
+    stack_.push_back({pc0, -1, 0});
+    while (!stack_.empty()) {
+      Frame fr = stack_.back();
+      stack_.pop_back();
+      if (fr.slot >= 0) { cap[fr.slot] = fr.old; continue; }
+      uint32_t pc = fr.pc;
+      if (pc == 0) continue;
+      if (contains(q, pc)) continue;
+      uint32_t j = size_[q]++;
+      sparse_[q][pc] = j;
+      dense_pc_[q][j] = pc;
+      dense_has_[q][j] = 0;
+      const Inst& in = p_.inst[pc];
+      switch (in.op) {
+        case IOp::Fail: break;
+        case IOp::Alt: case IOp::AltMatch:
+          stack_.push_back({in.arg, -1, 0});
+          stack_.push_back({in.out, -1, 0});
+          break;
+        case IOp::Empty:
+          if ((in.arg & ~cond) == 0) stack_.push_back({in.out, -1, 0});
+          break;
+        case IOp::Nop:
+          stack_.push_back({in.out, -1, 0});
+          break;
+        case IOp::Capture:
+          if (static_cast<int>(in.arg) < ncap_) {
+            stack_.push_back({0, static_cast<int>(in.arg), cap[in.arg]});   // restore after subtree
+            cap[in.arg] = static_cast<int>(pos);
+            stack_.push_back({in.out, -1, 0});
+          } else {
+            stack_.push_back({in.out, -1, 0});
+          }
+          break;
+        default:  // Match / Rune*: a thread lives here
+          dense_has_[q][j] = 1;
+          if (ncap_ > 0) std::copy(cap, cap + ncap_, &caps_[q][static_cast<size_t>(j) * ncap_]);
+          break;
+      }
+    }
+  }
+
+  void step(int rq, int nq, size_t pos, size_t npos, int32_t c, uint8_t ncond) {
+    for (uint32_t j = 0; j < size_[rq]; ++j) {
+      if (!dense_has_[rq][j]) continue;
+      const Inst& in = p_.inst[dense_pc_[rq][j]];
+      int* tcap = ncap_ > 0 ? &caps_[rq][static_cast<size_t>(j) * ncap_] : nullptr;
+      bool addit = false;
+      switch (in.op) {
+        case IOp::Match:
+          if (ncap_ > 0) {
+            tcap[1] = static_cast<int>(pos);
+            std::copy(tcap, tcap + ncap_, matchcap_.begin());
+          }
+          matched_ = true;
+          size_[rq] = j + 1;   // cut off lower-priority threads
+          break;
+        case IOp::Rune: addit = rune_match(p_, in, c); break;
+        case IOp::Rune1: addit = c == static_cast<int32_t>(in.arg); break;
+        case IOp::RuneAny: addit = c >= 0; break;
+        case IOp::RuneAnyNotNL: addit = c >= 0 && c != '\n'; break;
+        default: break;
+      }
+      if (addit) {
+        if (ncap_ > 0) {
+          std::copy(tcap, tcap + ncap_, scratch_.begin());
+          add(nq, in.out, npos, scratch_.data(), ncond);
+        } else {
+          add(nq, in.out, npos, scratch_.data(), ncond);
+        }
+      }
+    }
+    size_[rq] = 0;
+  }
+};
+
+}  // namespace
+
+std::vector<uint32_t> fold_orbit(uint32_t r) {
+  std::vector<uint32_t> out{r};
+  const size_t n = sizeof(kFoldOrbit) / sizeof(kFoldOrbit[0]);
+  uint32_t f;
+  if (!lookup_pair(kFoldOrbit, n, r, &f)) return out;
+  while (f != r) {
+    out.push_back(f);
+    if (!lookup_pair(kFoldOrbit, n, f, &f)) break;
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+bool is_print(uint32_t r) {
+  if (r == 0x20) return true;
+  static const char* cats[] = {"L", "M", "N", "P", "S"};
+  for (const char* c : cats) {
+    for (const CatTable& t : kCats) {
+      if (t.name[0] == c[0] && t.name[1] == 0) {
+        size_t lo = 0, hi = t.n;
+        while (lo < hi) {
+          size_t m = (lo + hi) / 2;
+          if (r < t.r[m][0]) hi = m; else if (r > t.r[m][1]) lo = m + 1; else return true;
+        }
+      }
+    }
+  }
+  return false;
+}
+
+uint32_t to_lower(uint32_t r) {
+  if (r < 0x80) return (r >= 'A' && r <= 'Z') ? r + 32 : r;
+  uint32_t l;
+  if (lookup_pair(kLower, sizeof(kLower) / sizeof(kLower[0]), r, &l)) return l;
+  return r;
+}
+
+void append_utf8(std::string* out, uint32_t r) {
+  if (r < 0x80) { out->push_back(static_cast<char>(r)); return; }
+  if (r < 0x800) { out->push_back(static_cast<char>(0xC0 | (r >> 6))); out->push_back(static_cast<char>(0x80 | (r & 0x3F))); return; }
+  if (r < 0x10000) {
+    out->push_back(static_cast<char>(0xE0 | (r >> 12)));
+    out->push_back(static_cast<char>(0x80 | ((r >> 6) & 0x3F)));
+    out->push_back(static_cast<char>(0x80 | (r & 0x3F)));
+    return;
+  }
+  out->push_back(static_cast<char>(0xF0 | (r >> 18)));
+  out->push_back(static_cast<char>(0x80 | ((r >> 12) & 0x3F)));
+  out->push_back(static_cast<char>(0x80 | ((r >> 6) & 0x3F)));
+  out->push_back(static_cast<char>(0x80 | (r & 0x3F)));
+}
+
+std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string* err) {
+  static std::atomic<uint64_t> next_id{1};
+  auto re = std::unique_ptr<Regexp>(new Regexp());
+  re->id_ = next_id.fetch_add(1);
+  re->pattern_ = pattern;
+  Parser ps(pattern);
+  re->ast_ = ps.parse(err, &re->names_);
+  if (!re->ast_) return nullptr;
+  re->prog_.num_cap = max_cap(*re->ast_);
+  auto simp = simplify(clone(*re->ast_));
+  Compiler c(&re->prog_);
+  Frag f = c.compile(*simp);
+  uint32_t m = c.inst(IOp::Match);
+  c.patch(f.out, m);
+  re->prog_.start = f.i;
+  re->nullable_ = f.nullable;
+  return re;
+}
+
+bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored, int ncap_wanted,
+                      int* caps) const {
+  if (prog_.start == 0) return false;
+  // one Machine per (thread, Regexp): keyed by the Regexp's unique id
+  thread_local std::vector<std::pair<uint64_t, std::unique_ptr<Machine>>> cache;
+  Machine* m = nullptr;
+  for (auto& e : cache) {
+    if (e.first == id_) { m = e.second.get(); break; }
+  }
+  (void)ncap_wanted;
+  const int ncap = 2 * (prog_.num_cap + 1);
+  std::unique_ptr<Machine> own;
+  if (!m) {
+    own.reset(new Machine(prog_, ncap));
+    m = own.get();
+    if (cache.size() > 4096) cache.clear();
+    cache.emplace_back(id_, std::move(own));
+  }
+  return m->match(text, len, pos, anchored, caps);
+}
+
+bool Regexp::match_string(const uint8_t* text, size_t len) const {
+  std::vector<int> caps(2 * (prog_.num_cap + 1));
+  return match_at(text, len, 0, false, 0, caps.data());
+}
+
+void Regexp::find_all(const uint8_t* text, size_t len, bool submatch, std::vector<int>* out) const {
+  const int ncap = 2 * (prog_.num_cap + 1);
+  std::vector<int> caps(ncap);
+  size_t pos = 0;
+  long prev_end = -1;
+  while (pos <= len) {
+    if (!match_at(text, len, pos, false, ncap, caps.data())) break;
+    bool accept = true;
+    if (static_cast<size_t>(caps[1]) == pos) {
+      if (caps[0] == prev_end) accept = false;
+      int32_t r; int w;
+      decode_rune(text + pos, len - pos, &r, &w);
+      pos = w > 0 ? pos + w : len + 1;
+    } else {
+      pos = static_cast<size_t>(caps[1]);
+    }
+    prev_end = caps[1];
+    if (accept) {
+      if (submatch) out->insert(out->end(), caps.begin(), caps.end());
+      else { out->push_back(caps[0]); out->push_back(caps[1]); }
+    }
+  }
+}
+
+}  // namespace re
+}  // namespace tsg

@@ -1,0 +1,136 @@
+// Go `regexp` semantics (RE2 syntax, leftmost-first, UTF-8 runes) for the host
+// side of the secret scanner.  The reference compiles every rule with Go's
+// regexp.Compile (pkg/fanal/secret/scanner.go:66-87) and calls FindAllIndex /
+// FindAllSubmatchIndex / MatchString (scanner.go:112,130,171,207,216,264).
+// Go is not available to link against, so this engine restates the semantics:
+//   * parser: Perl flags (i m s U), (?P<n>..)/(?<n>..), classes, \pX, POSIX
+//     classes, repeats <= 1000, ClassNL/OneLine (syntax.Perl defaults)
+//   * simplify: x{n,m} -> n copies + nested quests, x** -> x* (syntax.Simplify)
+//   * program: Go-shaped instruction list (Alt/Capture/EmptyWidth/Rune...),
+//     star of a nullable body compiled as (x+)?  (syntax/compile.go)
+//   * Pike VM: priority-ordered threads, first thread to reach a pc wins,
+//     first match cuts lower-priority threads (regexp/exec.go)
+//   * allMatches: empty match right after a previous match is skipped.
+// Invalid UTF-8 bytes decode as U+FFFD with width 1 (utf8.DecodeRune).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace tsg {
+namespace re {
+
+enum class Op : uint8_t {
+  NoMatch, EmptyMatch, Literal, CharClass, AnyCharNotNL, AnyChar,
+  BeginLine, EndLine, BeginText, EndText, WordBoundary, NoWordBoundary,
+  Capture, Star, Plus, Quest, Repeat, Concat, Alternate
+};
+
+struct Range { uint32_t lo, hi; };
+
+struct Node {
+  Op op = Op::EmptyMatch;
+  bool nongreedy = false;
+  uint32_t rune = 0;              // Literal (one rune; case folding already expanded to CharClass)
+  std::vector<Range> ranges;      // CharClass: sorted, non-overlapping, merged
+  int min = 0, max = 0;           // Repeat (max == -1: unbounded)
+  int cap = 0;                    // Capture index (1-based)
+  std::string name;               // Capture name
+  std::vector<std::unique_ptr<Node>> sub;
+};
+
+// Empty-width assertion bits (syntax.EmptyOp)
+enum : uint8_t {
+  kEmptyBeginLine = 1, kEmptyEndLine = 2, kEmptyBeginText = 4, kEmptyEndText = 8,
+  kEmptyWordBoundary = 16, kEmptyNoWordBoundary = 32
+};
+
+enum class IOp : uint8_t { Alt, AltMatch, Capture, Empty, Match, Fail, Nop, Rune, Rune1, RuneAny, RuneAnyNotNL };
+
+struct Inst {
+  IOp op;
+  uint32_t out = 0, arg = 0;      // Alt: out (preferred) / arg; Capture: arg = slot; Empty: arg = flags; Rune1: arg = rune
+  uint32_t rbeg = 0, rcnt = 0;    // Rune: ranges in Prog::ranges
+  uint64_t ascii[2] = {0, 0};     // Rune/Rune1: ASCII membership bitmap
+  bool nonascii = false;          // Rune: has any range >= 0x80
+};
+
+struct Prog {
+  std::vector<Inst> inst;
+  std::vector<Range> ranges;
+  uint32_t start = 0;
+  int num_cap = 0;                // capture groups, excluding group 0
+};
+
+// Go utf8.DecodeRune: rune + width; invalid -> 0xFFFD width 1; at end width 0.
+inline void decode_rune(const uint8_t* s, size_t n, int32_t* r, int* w) {
+  if (n == 0) { *r = -1; *w = 0; return; }
+  uint8_t c = s[0];
+  if (c < 0x80) { *r = c; *w = 1; return; }
+  auto cont = [](uint8_t b) { return (b & 0xC0) == 0x80; };
+  if (c >= 0xC2 && c <= 0xDF) {
+    if (n >= 2 && cont(s[1])) { *r = ((c & 0x1F) << 6) | (s[1] & 0x3F); *w = 2; return; }
+  } else if (c >= 0xE0 && c <= 0xEF) {
+    uint8_t lo = 0x80, hi = 0xBF;
+    if (c == 0xE0) lo = 0xA0;
+    if (c == 0xED) hi = 0x9F;
+    if (n >= 3 && s[1] >= lo && s[1] <= hi && cont(s[2])) {
+      *r = ((c & 0x0F) << 12) | ((s[1] & 0x3F) << 6) | (s[2] & 0x3F); *w = 3; return;
+    }
+  } else if (c >= 0xF0 && c <= 0xF4) {
+    uint8_t lo = 0x80, hi = 0xBF;
+    if (c == 0xF0) lo = 0x90;
+    if (c == 0xF4) hi = 0x8F;
+    if (n >= 4 && s[1] >= lo && s[1] <= hi && cont(s[2]) && cont(s[3])) {
+      *r = ((c & 0x07) << 18) | ((s[1] & 0x3F) << 12) | ((s[2] & 0x3F) << 6) | (s[3] & 0x3F); *w = 4; return;
+    }
+  }
+  *r = 0xFFFD; *w = 1;
+}
+
+// Go unicode.SimpleFold orbit of r (including r), sorted.
+std::vector<uint32_t> fold_orbit(uint32_t r);
+// Go unicode.ToLower (simple mapping).
+uint32_t to_lower(uint32_t r);
+// Go unicode.IsPrint: categories L, M, N, P, S and U+0020.
+bool is_print(uint32_t r);
+// Append UTF-8 encoding of rune r.
+void append_utf8(std::string* out, uint32_t r);
+
+class Regexp {
+ public:
+  // Returns nullptr and sets *err on a syntax error (Go: "error parsing regexp: ...").
+  static std::unique_ptr<Regexp> compile(const std::string& pattern, std::string* err);
+
+  const std::string& pattern() const { return pattern_; }
+  const Node* ast() const { return ast_.get(); }
+  const Prog& prog() const { return prog_; }
+  int num_subexp() const { return prog_.num_cap; }
+  // SubexpNames(): index 0 is "" (the whole match).
+  const std::vector<std::string>& subexp_names() const { return names_; }
+
+  // Leftmost-first match search starting at `pos` (context from the whole text).
+  // If `anchored`, only a match starting exactly at `pos` is considered.
+  // caps receives 2*(num_subexp+1) offsets (-1 for non-participating groups).
+  bool match_at(const uint8_t* text, size_t len, size_t pos, bool anchored, int ncap_wanted,
+                int* caps) const;
+  // Regexp.MatchString
+  bool match_string(const uint8_t* text, size_t len) const;
+  // Regexp.FindAll(Submatch)Index(text, -1): flattened vectors of 2 (or 2*(ncap+1)) ints.
+  void find_all(const uint8_t* text, size_t len, bool submatch, std::vector<int>* out) const;
+  // Minimal byte length of a match (used by the prefilter to reject nullable rules).
+  bool nullable() const { return nullable_; }
+
+ private:
+  std::string pattern_;
+  std::unique_ptr<Node> ast_;     // parsed + simplified
+  Prog prog_;
+  std::vector<std::string> names_;
+  bool nullable_ = false;
+  uint64_t id_ = 0;
+};
+
+}  // namespace re
+}  // namespace tsg

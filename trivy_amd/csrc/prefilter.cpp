@@ -1,0 +1,791 @@
+// Rule -> GPU table compiler.  See prefilter.h for what is produced and
+// DESIGN.md ("Why candidates are a superset") for the correctness argument.
+#include "prefilter.h"
+
+#include <algorithm>
+#include <bitset>
+#include <cstring>
+#include <map>
+#include <set>
+#include <unordered_map>
+
+namespace tsg {
+
+using re::Node;
+using re::Op;
+
+namespace {
+
+constexpr uint32_t kInf = 0x3fffffff;
+constexpr int kMaxSetSize = 64;          // literal-set cap
+constexpr int kMaxUnits = 6;             // literal length cap (units): longer adds DFA states, little selectivity
+constexpr uint32_t kMaxPrefixBytes = 96; // dmax cap for a usable anchor
+constexpr uint32_t kVerifyStateCap = 3000;
+constexpr uint32_t kScanStateCap = 60000;
+constexpr uint32_t kVerifyLimitCap = 8192;
+
+using Bits = std::bitset<256>;
+
+// ------------------------------------------------------------------ NFA
+struct NState {
+  std::vector<int> eps;
+  std::vector<std::pair<int, int>> edges;   // (set index, target)
+  int out = -1;                             // scan: output id; verify: 0 = accept
+};
+
+struct Nfa {
+  std::vector<NState> st;
+  std::vector<Bits> sets;
+  std::map<std::string, int> set_index;
+  int add() { st.emplace_back(); return static_cast<int>(st.size()) - 1; }
+  void eps(int a, int b) { st[a].eps.push_back(b); }
+  int set_id(const Bits& b) {
+    std::string k = b.to_string();
+    auto it = set_index.find(k);
+    if (it != set_index.end()) return it->second;
+    sets.push_back(b);
+    int id = static_cast<int>(sets.size()) - 1;
+    set_index.emplace(std::move(k), id);
+    return id;
+  }
+  void edge(int a, const Bits& b, int to) { st[a].edges.push_back({set_id(b), to}); }
+  void byte_chain(int from, const std::string& bytes, int to) {
+    int cur = from;
+    for (size_t i = 0; i < bytes.size(); ++i) {
+      int nx = (i + 1 == bytes.size()) ? to : add();
+      Bits b;
+      b.set(static_cast<uint8_t>(bytes[i]));
+      edge(cur, b, nx);
+      cur = nx;
+    }
+    if (bytes.empty()) eps(from, to);
+  }
+  // [\x80-\xFF]{1,4}: any non-ASCII rune (valid 2-4 byte sequence or an invalid byte)
+  void high_unit(int from, int to) {
+    Bits hi;
+    for (int c = 0x80; c < 256; ++c) hi.set(c);
+    int cur = from;
+    for (int k = 0; k < 4; ++k) {
+      int nx = add();
+      edge(cur, hi, nx);
+      eps(nx, to);
+      cur = nx;
+    }
+  }
+};
+
+std::string utf8(uint32_t r) { std::string s; re::append_utf8(&s, r); return s; }
+
+uint64_t class_size(const Node& n) {
+  uint64_t c = 0;
+  for (const auto& r : n.ranges) c += static_cast<uint64_t>(r.hi) - r.lo + 1;
+  return c;
+}
+
+// Relaxed rune class -> NFA fragment from `from` to `to`.
+void class_frag(Nfa* nfa, const std::vector<re::Range>& ranges, int from, int to) {
+  Bits ascii;
+  uint64_t nonascii = 0;
+  bool has_fffd = false;
+  std::vector<uint32_t> small;
+  for (const auto& r : ranges) {
+    for (uint32_t c = r.lo; c <= std::min<uint32_t>(r.hi, 0x7f); ++c) ascii.set(c);
+    if (r.hi >= 0x80) {
+      uint32_t lo = std::max<uint32_t>(r.lo, 0x80);
+      nonascii += r.hi - lo + 1;
+      if (lo <= 0xFFFD && 0xFFFD <= r.hi) has_fffd = true;
+      if (nonascii <= 16) for (uint32_t c = lo; c <= r.hi; ++c) small.push_back(c);
+    }
+  }
+  if (ascii.any()) nfa->edge(from, ascii, to);
+  if (nonascii == 0) return;
+  if (nonascii <= 16 && !has_fffd) {
+    for (uint32_t c : small) nfa->byte_chain(from, utf8(c), to);
+  } else {
+    nfa->high_unit(from, to);
+  }
+}
+
+// Relaxed (superset) NFA of an AST node.
+int build(Nfa* nfa, const Node& n, int from);
+
+int build_repeat(Nfa* nfa, const Node& sub, int mn, int mx, int from) {
+  // relaxation: X{m,n} with m > 64 or n-m > 8 becomes X{min(m,64)}X*
+  int m = std::min(mn, 64);
+  bool loose = mx < 0 || mn > 64 || (mx - mn) > 8;
+  int cur = from;
+  for (int k = 0; k < m; ++k) cur = build(nfa, sub, cur);
+  if (loose) {
+    int loop = nfa->add();
+    nfa->eps(cur, loop);
+    int body_end = build(nfa, sub, loop);
+    nfa->eps(body_end, loop);
+    return loop;
+  }
+  int end = nfa->add();
+  nfa->eps(cur, end);
+  for (int k = m; k < mx; ++k) {
+    cur = build(nfa, sub, cur);
+    nfa->eps(cur, end);
+  }
+  return end;
+}
+
+int build(Nfa* nfa, const Node& n, int from) {
+  switch (n.op) {
+    case Op::NoMatch: {
+      return nfa->add();   // unreachable end
+    }
+    case Op::EmptyMatch: case Op::BeginLine: case Op::EndLine: case Op::BeginText:
+    case Op::EndText: case Op::WordBoundary: case Op::NoWordBoundary:
+      return from;
+    case Op::Literal: {
+      int to = nfa->add();
+      if (n.rune < 0x80) { Bits b; b.set(n.rune); nfa->edge(from, b, to); }
+      else nfa->byte_chain(from, utf8(n.rune), to);
+      return to;
+    }
+    case Op::CharClass: {
+      int to = nfa->add();
+      class_frag(nfa, n.ranges, from, to);
+      return to;
+    }
+    case Op::AnyCharNotNL: {
+      int to = nfa->add();
+      class_frag(nfa, {{0, 9}, {11, 0x10FFFF}}, from, to);
+      return to;
+    }
+    case Op::AnyChar: {
+      int to = nfa->add();
+      class_frag(nfa, {{0, 0x10FFFF}}, from, to);
+      return to;
+    }
+    case Op::Capture:
+      return build(nfa, *n.sub[0], from);
+    case Op::Concat: {
+      int cur = from;
+      for (const auto& s : n.sub) cur = build(nfa, *s, cur);
+      return cur;
+    }
+    case Op::Alternate: {
+      int end = nfa->add();
+      for (const auto& s : n.sub) {
+        int st = nfa->add();
+        nfa->eps(from, st);
+        nfa->eps(build(nfa, *s, st), end);
+      }
+      return end;
+    }
+    case Op::Star: return build_repeat(nfa, *n.sub[0], 0, -1, from);
+    case Op::Plus: return build_repeat(nfa, *n.sub[0], 1, -1, from);
+    case Op::Quest: return build_repeat(nfa, *n.sub[0], 0, 1, from);
+    case Op::Repeat: return build_repeat(nfa, *n.sub[0], n.min, n.max, from);
+  }
+  return from;
+}
+
+// Byte-length bounds of a match of n (relaxed; runes >= 0x80 may be 1..4 bytes).
+void len_bounds(const Node& n, uint32_t* lo, uint32_t* hi) {
+  auto add = [](uint32_t a, uint32_t b) { return (a >= kInf || b >= kInf) ? kInf : std::min(a + b, kInf); };
+  auto mul = [](uint32_t a, uint32_t k) { return a >= kInf ? kInf : static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(a) * k, kInf)); };
+  switch (n.op) {
+    case Op::NoMatch: *lo = kInf; *hi = 0; return;
+    case Op::EmptyMatch: case Op::BeginLine: case Op::EndLine: case Op::BeginText:
+    case Op::EndText: case Op::WordBoundary: case Op::NoWordBoundary:
+      *lo = *hi = 0; return;
+    case Op::Literal: *lo = *hi = static_cast<uint32_t>(utf8(n.rune).size()); return;
+    case Op::CharClass: {
+      bool ascii = false, non = false;
+      for (const auto& r : n.ranges) { if (r.lo < 0x80) ascii = true; if (r.hi >= 0x80) non = true; }
+      *lo = ascii ? 1 : (non ? 1 : kInf);
+      *hi = non ? 4 : 1;
+      return;
+    }
+    case Op::AnyCharNotNL: case Op::AnyChar: *lo = 1; *hi = 4; return;
+    case Op::Capture: len_bounds(*n.sub[0], lo, hi); return;
+    case Op::Concat: {
+      uint32_t a = 0, b = 0;
+      for (const auto& s : n.sub) { uint32_t x, y; len_bounds(*s, &x, &y); a = add(a, x); b = add(b, y); }
+      *lo = a; *hi = b; return;
+    }
+    case Op::Alternate: {
+      uint32_t a = kInf, b = 0;
+      for (const auto& s : n.sub) { uint32_t x, y; len_bounds(*s, &x, &y); a = std::min(a, x); b = std::max(b, y); }
+      *lo = a; *hi = b; return;
+    }
+    case Op::Star: { uint32_t x, y; len_bounds(*n.sub[0], &x, &y); *lo = 0; *hi = y == 0 ? 0 : kInf; return; }
+    case Op::Plus: { uint32_t x, y; len_bounds(*n.sub[0], &x, &y); *lo = x; *hi = y == 0 ? 0 : kInf; return; }
+    case Op::Quest: { uint32_t x, y; len_bounds(*n.sub[0], &x, &y); *lo = 0; *hi = y; return; }
+    case Op::Repeat: {
+      uint32_t x, y; len_bounds(*n.sub[0], &x, &y);
+      *lo = mul(x, n.min);
+      *hi = n.max < 0 ? (y == 0 ? 0 : kInf) : mul(y, n.max);
+      return;
+    }
+  }
+  *lo = 0; *hi = kInf;
+}
+
+// --------------------------------------------------------- literal sets
+using Unit = std::vector<std::string>;     // sorted alternative byte strings
+using Seq = std::vector<Unit>;
+using SeqSet = std::set<Seq>;
+
+bool small_class(const Node& n, Unit* u) {
+  if (class_size(n) > 4) return false;
+  for (const auto& r : n.ranges)
+    for (uint32_t c = r.lo; c <= r.hi; ++c) {
+      if (c == 0xFFFD) return false;       // would also stand for every invalid byte
+      u->push_back(utf8(c));
+    }
+  std::sort(u->begin(), u->end());
+  return true;
+}
+
+bool cross(const SeqSet& a, const SeqSet& b, SeqSet* out) {
+  out->clear();
+  for (const auto& x : a) {
+    for (const auto& y : b) {
+      Seq s = x;
+      for (const auto& u : y) { if (static_cast<int>(s.size()) >= kMaxUnits) break; s.push_back(u); }
+      out->insert(std::move(s));
+      if (static_cast<int>(out->size()) > kMaxSetSize) return false;
+    }
+  }
+  return true;
+}
+
+// Exact finite set of literal sequences matched by n, if small.
+bool finite_set(const Node& n, SeqSet* out) {
+  out->clear();
+  switch (n.op) {
+    case Op::EmptyMatch: case Op::BeginLine: case Op::EndLine: case Op::BeginText:
+    case Op::EndText: case Op::WordBoundary: case Op::NoWordBoundary:
+      out->insert(Seq{});
+      return true;
+    case Op::Literal: out->insert(Seq{Unit{utf8(n.rune)}}); return true;
+    case Op::CharClass: {
+      Unit u;
+      if (!small_class(n, &u)) return false;
+      out->insert(Seq{u});
+      return true;
+    }
+    case Op::Capture: return finite_set(*n.sub[0], out);
+    case Op::Concat: {
+      SeqSet acc{Seq{}};
+      for (const auto& s : n.sub) {
+        SeqSet f, t;
+        if (!finite_set(*s, &f)) return false;
+        if (!cross(acc, f, &t)) return false;
+        acc.swap(t);
+      }
+      *out = std::move(acc);
+      return true;
+    }
+    case Op::Alternate: {
+      for (const auto& s : n.sub) {
+        SeqSet f;
+        if (!finite_set(*s, &f)) return false;
+        out->insert(f.begin(), f.end());
+        if (static_cast<int>(out->size()) > kMaxSetSize) return false;
+      }
+      return true;
+    }
+    case Op::Quest: {
+      SeqSet f;
+      if (!finite_set(*n.sub[0], &f)) return false;
+      *out = std::move(f);
+      out->insert(Seq{});
+      return static_cast<int>(out->size()) <= kMaxSetSize;
+    }
+    case Op::Repeat: {
+      if (n.max < 0 || n.max > 4) return false;
+      SeqSet f;
+      if (!finite_set(*n.sub[0], &f)) return false;
+      SeqSet acc{Seq{}}, all;
+      for (int k = 0; k <= n.max; ++k) {
+        if (k >= n.min) all.insert(acc.begin(), acc.end());
+        SeqSet t;
+        if (!cross(acc, f, &t)) return false;
+        acc.swap(t);
+      }
+      *out = std::move(all);
+      return static_cast<int>(out->size()) <= kMaxSetSize;
+    }
+    default:
+      return false;
+  }
+}
+
+// Set of sequences one of which begins every match of items[k..] (Seq{} = no info).
+SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k);
+
+SeqSet prefix_set(const Node& n) {
+  SeqSet f;
+  if (finite_set(n, &f)) return f;
+  switch (n.op) {
+    case Op::Capture: return prefix_set(*n.sub[0]);
+    case Op::Concat: {
+      std::vector<const Node*> items;
+      for (const auto& s : n.sub) items.push_back(s.get());
+      return prefix_of_items(items, 0);
+    }
+    case Op::Alternate: {
+      SeqSet out;
+      for (const auto& s : n.sub) {
+        SeqSet p = prefix_set(*s);
+        out.insert(p.begin(), p.end());
+        if (static_cast<int>(out.size()) > kMaxSetSize) return SeqSet{Seq{}};
+      }
+      return out;
+    }
+    case Op::Plus: return prefix_set(*n.sub[0]);
+    case Op::Repeat: if (n.min >= 1) return prefix_set(*n.sub[0]); return SeqSet{Seq{}};
+    default: return SeqSet{Seq{}};
+  }
+}
+
+SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k) {
+  SeqSet acc{Seq{}};
+  for (size_t i = k; i < items.size(); ++i) {
+    SeqSet f, t;
+    if (finite_set(*items[i], &f)) {
+      if (!cross(acc, f, &t)) return acc;   // keep what we have (still a valid prefix set)
+      acc.swap(t);
+      continue;
+    }
+    SeqSet p = prefix_set(*items[i]);
+    if (!cross(acc, p, &t)) return acc;
+    acc.swap(t);
+    break;
+  }
+  return acc;
+}
+
+void flatten(const Node& n, std::vector<const Node*>* items) {
+  if (n.op == Op::Concat) { for (const auto& s : n.sub) flatten(*s, items); return; }
+  if (n.op == Op::Capture) { flatten(*n.sub[0], items); return; }
+  items->push_back(&n);
+}
+
+uint32_t seq_min_len(const Seq& s) {
+  uint32_t l = 0;
+  for (const auto& u : s) { size_t m = 1000; for (const auto& a : u) m = std::min(m, a.size()); l += static_cast<uint32_t>(m); }
+  return l;
+}
+uint32_t seq_max_len(const Seq& s) {
+  uint32_t l = 0;
+  for (const auto& u : s) { size_t m = 0; for (const auto& a : u) m = std::max(m, a.size()); l += static_cast<uint32_t>(m); }
+  return l;
+}
+
+// Selectivity score of a literal unit sequence: longer and case-sensitive is better.
+double seq_score(const Seq& s) {
+  double sc = 0;
+  for (const auto& u : s) {
+    const char c = static_cast<char>(tolower(static_cast<unsigned char>(u[0][0])));
+    bool common = u[0].size() == 1 && strchr(" etaoinsr\"'=:_-.,", c) != nullptr;
+    sc += common ? 0.7 : 1.0;
+  }
+  return sc;
+}
+
+// --------------------------------------------------------- DFA building
+struct ClassMap { uint8_t cls[256]; uint32_t n; };
+
+ClassMap byte_classes(const Nfa& nfa) {
+  std::map<std::vector<bool>, uint8_t> sig;
+  ClassMap cm;
+  for (int b = 0; b < 256; ++b) {
+    std::vector<bool> s(nfa.sets.size());
+    for (size_t i = 0; i < nfa.sets.size(); ++i) s[i] = nfa.sets[i].test(b);
+    auto it = sig.find(s);
+    if (it == sig.end()) it = sig.emplace(s, static_cast<uint8_t>(sig.size())).first;
+    cm.cls[b] = it->second;
+  }
+  cm.n = static_cast<uint32_t>(sig.size());
+  return cm;
+}
+
+void closure(const Nfa& nfa, std::vector<int>* set) {
+  std::vector<int> stack(set->begin(), set->end());
+  std::vector<char> in(nfa.st.size(), 0);
+  for (int s : *set) in[s] = 1;
+  while (!stack.empty()) {
+    int s = stack.back();
+    stack.pop_back();
+    for (int t : nfa.st[s].eps) if (!in[t]) { in[t] = 1; set->push_back(t); stack.push_back(t); }
+  }
+  std::sort(set->begin(), set->end());
+}
+
+struct RawDfa {
+  std::vector<std::vector<int>> subsets;
+  std::vector<std::vector<uint32_t>> next;   // per state, per class
+  ClassMap cm;
+};
+
+// Subset construction.  `loop_start`: scan DFA (the start closure is re-added
+// after every byte).  `absorb_accept`: verify DFA (accepting subsets stop).
+bool determinize(const Nfa& nfa, int start, bool loop_start, int accept_state, uint32_t cap, RawDfa* out) {
+  out->cm = byte_classes(nfa);
+  const uint32_t C = out->cm.n;
+  std::vector<int> s0{start};
+  closure(nfa, &s0);
+  std::map<std::vector<int>, uint32_t> ids;
+  out->subsets.push_back(s0);
+  ids[s0] = 0;
+  // representative byte of each class
+  std::vector<int> rep(C, -1);
+  for (int b = 0; b < 256; ++b) if (rep[out->cm.cls[b]] < 0) rep[out->cm.cls[b]] = b;
+  for (size_t i = 0; i < out->subsets.size(); ++i) {
+    if (out->subsets.size() > cap) return false;
+    std::vector<uint32_t> row(C, 0);
+    const std::vector<int> cur = out->subsets[i];
+    bool acc = accept_state >= 0 && std::binary_search(cur.begin(), cur.end(), accept_state);
+    for (uint32_t c = 0; c < C; ++c) {
+      std::vector<int> nx;
+      if (acc) { row[c] = static_cast<uint32_t>(i); continue; }
+      std::vector<char> seen(0);
+      for (int s : cur) {
+        for (const auto& e : nfa.st[s].edges) {
+          if (nfa.sets[e.first].test(rep[c])) nx.push_back(e.second);
+        }
+      }
+      if (loop_start) nx.push_back(start);
+      std::sort(nx.begin(), nx.end());
+      nx.erase(std::unique(nx.begin(), nx.end()), nx.end());
+      closure(nfa, &nx);
+      auto it = ids.find(nx);
+      uint32_t id;
+      if (it == ids.end()) {
+        id = static_cast<uint32_t>(out->subsets.size());
+        ids.emplace(nx, id);
+        out->subsets.push_back(std::move(nx));
+      } else {
+        id = it->second;
+      }
+      row[c] = id;
+    }
+    out->next.push_back(std::move(row));
+  }
+  return true;
+}
+
+// Add a literal unit sequence as a chain into the scan NFA; returns max bytes.
+uint32_t add_seq(Nfa* nfa, int start, const Seq& s, int out_id) {
+  int cur = start;
+  uint32_t maxb = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    int nx = nfa->add();
+    size_t m = 0;
+    for (const auto& alt : s[i]) { nfa->byte_chain(cur, alt, nx); m = std::max(m, alt.size()); }
+    maxb += static_cast<uint32_t>(m);
+    cur = nx;
+  }
+  nfa->st[cur].out = out_id;
+  return maxb;
+}
+
+// Scan-DFA unit for one ASCII byte: the byte and, for letters, its other case.
+Unit folded_unit(unsigned char c) {
+  Unit u;
+  u.push_back(std::string(1, static_cast<char>(c)));
+  if (c >= 'a' && c <= 'z') u.push_back(std::string(1, static_cast<char>(c - 32)));
+  if (c >= 'A' && c <= 'Z') u.push_back(std::string(1, static_cast<char>(c + 32)));
+  std::sort(u.begin(), u.end());
+  return u;
+}
+
+// Keyword (already strings.ToLower'ed, ASCII) under bytes.ToLower semantics.
+// The two non-ASCII runes that lower to ASCII (U+0130 -> 'i', U+212A -> 'k')
+// are not in the DFA: K1 flags files containing them and the host evaluates
+// such files exactly.
+Seq keyword_seq(const std::string& kw) {
+  Seq s;
+  for (char ch : kw) s.push_back(folded_unit(static_cast<unsigned char>(ch)));
+  return s;
+}
+
+// Scan-DFA form of an anchor literal: every unit case-folded over ASCII (a
+// superset; the verify DFA re-checks case).  Non-ASCII alternatives that are
+// the fold images of ASCII letters (U+212A, U+017F) are dropped -- files that
+// contain them are flagged by K1 and scanned exactly on the host.  The literal
+// is cut before any unit with another non-ASCII alternative.
+Seq scan_form(const Seq& lit) {
+  Seq out;
+  for (const Unit& u : lit) {
+    Unit f;
+    bool ok = true;
+    for (const auto& alt : u) {
+      if (alt == "\xE2\x84\xAA" || alt == "\xC5\xBF") continue;
+      if (alt.size() != 1 || static_cast<unsigned char>(alt[0]) >= 0x80) { ok = false; break; }
+      for (const auto& x : folded_unit(static_cast<unsigned char>(alt[0]))) f.push_back(x);
+    }
+    if (!ok || f.empty()) break;
+    std::sort(f.begin(), f.end());
+    f.erase(std::unique(f.begin(), f.end()), f.end());
+    out.push_back(f);
+  }
+  return out;
+}
+
+bool is_ascii(const std::string& s) {
+  for (unsigned char c : s) if (c >= 0x80) return false;
+  return true;
+}
+
+struct AnchorChoice {
+  bool ok = false;
+  size_t k = 0;
+  SeqSet lits;
+  uint32_t dmin = 0, dmax = 0;
+};
+
+AnchorChoice choose_anchor(const std::vector<const Node*>& items) {
+  AnchorChoice best;
+  double best_score = -1;
+  uint32_t plo = 0, phi = 0;
+  for (size_t k = 0; k < items.size(); ++k) {
+    if (phi <= kMaxPrefixBytes) {
+      SeqSet raw = prefix_of_items(items, k);
+      SeqSet lits;
+      for (const auto& s : raw) lits.insert(scan_form(s));
+      double score = 1e9;
+      bool usable = !lits.empty();
+      for (const auto& s : lits) {
+        if (s.empty()) { usable = false; break; }
+        score = std::min(score, seq_score(s));
+      }
+      if (usable) {
+        // every extra literal costs scan-DFA states: prefer small sets
+        score -= 0.05 * static_cast<double>(lits.size() - 1);
+        if (score > best_score) {
+          best_score = score;
+          best.ok = true;
+          best.k = k;
+          best.lits = lits;
+          best.dmin = plo;
+          best.dmax = phi;
+        }
+      }
+    }
+    uint32_t lo, hi;
+    len_bounds(*items[k], &lo, &hi);
+    plo = std::min(plo + lo, kInf);
+    phi = (phi >= kInf || hi >= kInf) ? kInf : std::min(phi + hi, kInf);
+  }
+  if (best.ok && best_score < 1.5) best.ok = false;   // a 1-unit anchor is useless
+  return best;
+}
+
+DfaTable to_table(const RawDfa& raw, const std::vector<uint32_t>& order, int accept_state) {
+  DfaTable t;
+  t.nstates = static_cast<uint32_t>(raw.subsets.size());
+  t.nclasses = raw.cm.n;
+  std::copy(raw.cm.cls, raw.cm.cls + 256, t.byte_class);
+  std::vector<uint32_t> inv(order.size());
+  for (size_t i = 0; i < order.size(); ++i) inv[order[i]] = static_cast<uint32_t>(i);
+  t.next.resize(static_cast<size_t>(t.nstates) * t.nclasses);
+  t.accept.assign(t.nstates, 0);
+  for (uint32_t i = 0; i < t.nstates; ++i) {
+    uint32_t old = order[i];
+    for (uint32_t c = 0; c < t.nclasses; ++c) t.next[static_cast<size_t>(i) * t.nclasses + c] = static_cast<uint16_t>(inv[raw.next[old][c]]);
+    if (accept_state >= 0 && std::binary_search(raw.subsets[old].begin(), raw.subsets[old].end(), accept_state)) t.accept[i] = 1;
+    if (raw.subsets[old].empty()) t.dead = i;
+  }
+  return t;
+}
+
+bool build_verify(const std::vector<const Node*>& items, size_t min_items, DfaTable* out, uint32_t* limit,
+                  std::string* note) {
+  for (size_t j = items.size(); j >= min_items && j > 0; --j) {
+    Nfa nfa;
+    int start = nfa.add();
+    int cur = start;
+    uint32_t lo = 0, hi = 0;
+    for (size_t i = 0; i < j; ++i) {
+      cur = build(&nfa, *items[i], cur);
+      uint32_t a, b;
+      len_bounds(*items[i], &a, &b);
+      hi = (hi >= kInf || b >= kInf) ? kInf : std::min(hi + b, kInf);
+    }
+    int acc = nfa.add();
+    nfa.eps(cur, acc);
+    nfa.st[acc].out = 0;
+    RawDfa raw;
+    if (!determinize(nfa, start, false, acc, kVerifyStateCap, &raw)) continue;
+    // make sure a dead (empty) state exists
+    bool has_dead = false;
+    for (const auto& s : raw.subsets) if (s.empty()) has_dead = true;
+    if (!has_dead) {
+      raw.subsets.push_back({});
+      raw.next.push_back(std::vector<uint32_t>(raw.cm.n, static_cast<uint32_t>(raw.subsets.size() - 1)));
+    }
+    std::vector<uint32_t> order(raw.subsets.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
+    *out = to_table(raw, order, acc);
+    *limit = std::min(hi, kVerifyLimitCap);
+    if (j < items.size()) *note += " verify-truncated:" + std::to_string(j) + "/" + std::to_string(items.size());
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
+  *pf = Prefilter();
+  // --- keywords: distinct ASCII lowered keywords get a GPU pattern id
+  std::map<std::string, uint32_t> kw_ids;
+  pf->rules.resize(rs.rules.size());
+  for (size_t r = 0; r < rs.rules.size(); ++r) {
+    const Rule& rule = rs.rules[r];
+    RuleGpuInfo& gi = pf->rules[r];
+    gi.kw_begin = static_cast<uint32_t>(pf->rule_kw.size());
+    gi.always_gate = rule.keywords.empty();
+    gi.gate_on_gpu = 1;
+    for (const auto& kw : rule.keywords_lower) {
+      if (kw.empty()) { gi.always_gate = 1; continue; }
+      if (!is_ascii(kw)) { gi.gate_on_gpu = 0; continue; }
+      auto it = kw_ids.find(kw);
+      if (it == kw_ids.end()) {
+        it = kw_ids.emplace(kw, static_cast<uint32_t>(pf->kw_text.size())).first;
+        pf->kw_text.push_back(kw);
+      }
+      pf->rule_kw.push_back(it->second);
+    }
+    gi.kw_count = static_cast<uint32_t>(pf->rule_kw.size()) - gi.kw_begin;
+    if (gi.always_gate) gi.gate_on_gpu = 1;
+  }
+  pf->nkw = static_cast<uint32_t>(pf->kw_text.size());
+
+  // --- scan NFA
+  Nfa scan;
+  int s0 = scan.add();
+  uint32_t maxb = 1;
+  for (uint32_t k = 0; k < pf->nkw; ++k) {
+    maxb = std::max(maxb, add_seq(&scan, s0, keyword_seq(pf->kw_text[k]), static_cast<int>(k)));
+  }
+  std::string rep;
+  for (size_t r = 0; r < rs.rules.size(); ++r) {
+    const Rule& rule = rs.rules[r];
+    RuleGpuInfo& gi = pf->rules[r];
+    gi.mode = 1;
+    if (!rule.regex) { gi.mode = 2; continue; }      // no regex: never any location
+    std::vector<const Node*> items;
+    flatten(*rule.regex->ast(), &items);
+    AnchorChoice ch = rule.regex->nullable() ? AnchorChoice() : choose_anchor(items);
+    if (!ch.ok) { rep += rule.id + ": FULL (no bounded anchor)\n"; continue; }
+    std::string note;
+    DfaTable vt;
+    uint32_t limit = 0;
+    if (!build_verify(items, ch.k + 1, &vt, &limit, &note)) { rep += rule.id + ": FULL (verify DFA too large)\n"; continue; }
+    gi.mode = 0;
+    gi.verify_dfa = static_cast<uint32_t>(pf->verify.size());
+    gi.verify_limit = std::max<uint32_t>(limit, 1);
+    pf->verify.push_back(std::move(vt));
+    for (const auto& s : ch.lits) {
+      AnchorInfo a;
+      a.rule = static_cast<uint32_t>(r);
+      a.min_len = seq_min_len(s);
+      a.max_len = seq_max_len(s);
+      a.dmin = ch.dmin;
+      a.dmax = ch.dmax;
+      uint32_t id = pf->nkw + static_cast<uint32_t>(pf->anchors.size());
+      pf->anchors.push_back(a);
+      maxb = std::max(maxb, add_seq(&scan, s0, s, static_cast<int>(id)));
+    }
+    rep += rule.id + ": anchored item " + std::to_string(ch.k) + ", " + std::to_string(ch.lits.size()) +
+           " literal(s), offset [" + std::to_string(ch.dmin) + "," + std::to_string(ch.dmax) + "], verify " +
+           std::to_string(pf->verify.back().nstates) + " states x " + std::to_string(pf->verify.back().nclasses) +
+           " classes, limit " + std::to_string(gi.verify_limit) + note + "\n";
+  }
+  RawDfa raw;
+  if (!determinize(scan, s0, true, -1, kScanStateCap, &raw)) { *err = "scan DFA exceeds state cap"; return false; }
+  // outputs per subset; renumber: states without outputs first (start stays 0)
+  std::vector<std::vector<uint32_t>> outs(raw.subsets.size());
+  for (size_t i = 0; i < raw.subsets.size(); ++i) {
+    for (int s : raw.subsets[i]) if (scan.st[s].out >= 0) outs[i].push_back(static_cast<uint32_t>(scan.st[s].out));
+    std::sort(outs[i].begin(), outs[i].end());
+    outs[i].erase(std::unique(outs[i].begin(), outs[i].end()), outs[i].end());
+  }
+  if (!outs[0].empty()) { *err = "scan DFA start state has outputs"; return false; }
+  std::vector<uint32_t> order;
+  for (size_t i = 0; i < raw.subsets.size(); ++i) if (outs[i].empty()) order.push_back(static_cast<uint32_t>(i));
+  pf->scan.first_out_state = static_cast<uint32_t>(order.size());
+  for (size_t i = 0; i < raw.subsets.size(); ++i) if (!outs[i].empty()) order.push_back(static_cast<uint32_t>(i));
+  if (order.size() > 65535) { *err = "scan DFA too large for 16-bit states"; return false; }
+  pf->scan.t = to_table(raw, order, -1);
+  pf->scan.out_off.push_back(0);
+  for (size_t i = pf->scan.first_out_state; i < order.size(); ++i) {
+    const auto& o = outs[order[i]];
+    pf->scan.out_ids.insert(pf->scan.out_ids.end(), o.begin(), o.end());
+    pf->scan.out_off.push_back(static_cast<uint32_t>(pf->scan.out_ids.size()));
+  }
+  pf->scan.max_pattern_bytes = maxb;
+  pf->report = "scan DFA: " + std::to_string(pf->scan.t.nstates) + " states x " + std::to_string(pf->scan.t.nclasses) +
+               " classes (" + std::to_string(pf->scan.first_out_state) + " silent), " + std::to_string(pf->nkw) +
+               " keywords, " + std::to_string(pf->anchors.size()) + " anchor literals, max pattern " +
+               std::to_string(maxb) + " B\n" + rep;
+  return true;
+}
+
+bool prefilter_reference_file(const Prefilter& pf, const uint8_t* data, size_t len,
+                              std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
+  const DfaTable& t = pf.scan.t;
+  bool special = false;
+  for (size_t p = 1; p < len; ++p) {
+    if (fold_special_at(p >= 2 ? data[p - 2] : 0, data[p - 1], data[p])) { special = true; break; }
+  }
+  std::vector<uint8_t> kwbit(pf.nkw, 0);
+  struct Hit { uint64_t end; uint32_t anchor; };
+  std::vector<Hit> hits;
+  uint32_t s = 0;
+  for (size_t p = 0; p < len; ++p) {
+    s = t.next[static_cast<size_t>(s) * t.nclasses + t.byte_class[data[p]]];
+    if (s >= pf.scan.first_out_state) {
+      uint32_t o = s - pf.scan.first_out_state;
+      for (uint32_t k = pf.scan.out_off[o]; k < pf.scan.out_off[o + 1]; ++k) {
+        uint32_t id = pf.scan.out_ids[k];
+        if (id < pf.nkw) kwbit[id] = 1; else hits.push_back({p, id - pf.nkw});
+      }
+    }
+  }
+  gate->assign(pf.rules.size(), 0);
+  for (size_t r = 0; r < pf.rules.size(); ++r) {
+    const RuleGpuInfo& gi = pf.rules[r];
+    uint8_t g = gi.always_gate;
+    for (uint32_t k = 0; k < gi.kw_count; ++k) g |= kwbit[pf.rule_kw[gi.kw_begin + k]];
+    (*gate)[r] = g;
+  }
+  cand->assign(pf.rules.size(), {});
+  for (const Hit& h : hits) {
+    const AnchorInfo& a = pf.anchors[h.anchor];
+    if (!(*gate)[a.rule]) continue;
+    const RuleGpuInfo& gi = pf.rules[a.rule];
+    const DfaTable& v = pf.verify[gi.verify_dfa];
+    long hi = static_cast<long>(h.end) + 1 - a.min_len - a.dmin;
+    long lo = static_cast<long>(h.end) + 1 - a.max_len - a.dmax;
+    if (lo < 0) lo = 0;
+    for (long st = lo; st <= hi; ++st) {
+      uint32_t q = 0;
+      bool emit = v.accept[0];
+      size_t p = st;
+      for (; !emit && p < len && p - st < gi.verify_limit; ++p) {
+        q = v.next[static_cast<size_t>(q) * v.nclasses + v.byte_class[data[p]]];
+        if (v.accept[q]) emit = true;
+        else if (q == v.dead) break;
+      }
+      if (!emit && q != v.dead && p < len && p - st >= gi.verify_limit) emit = true;   // gave up: conservative
+      if (emit) (*cand)[a.rule].push_back(static_cast<uint64_t>(st));
+    }
+  }
+  for (auto& c : *cand) {
+    std::sort(c.begin(), c.end());
+    c.erase(std::unique(c.begin(), c.end()), c.end());
+  }
+  return special;
+}
+
+}  // namespace tsg

@@ -1,0 +1,89 @@
+// Rule compiler for the GPU prefilter (host side, run once per ruleset, the
+// equivalent of where the reference compiles its regexes: ParseConfig /
+// NewScanner, pkg/fanal/secret/scanner.go:75-87,320-364).
+//
+// Produces, from the Go regexp ASTs and keywords of every rule:
+//  * one SCAN DFA over bytes (`.*(p1|p2|...)`) whose patterns are
+//      - every distinct ASCII keyword under bytes.ToLower semantics
+//        (A-Z folded; U+0130 -> 'i', U+212A -> 'k' as in unicode.ToLower),
+//        exact, giving the per-(file, rule) keyword gate of
+//        Rule.MatchKeywords (scanner.go:174-186);
+//      - ANCHOR literals: for each rule a set of literal unit sequences such
+//        that every match of the rule's regex contains one of them at a
+//        byte offset d in [dmin, dmax] from the match start;
+//  * one anchored VERIFY DFA per rule: a relaxed superset of the regex
+//    (assertions -> empty, non-ASCII runes -> 1-4 high bytes, long repeats
+//    loosened, tail truncated to fit a state budget), accepting as soon as a
+//    prefix of the text from a candidate start is in the relaxed language.
+// A rule with no usable anchor (nullable regex, unbounded prefix) is marked
+// FULL: the host evaluates it exactly over the whole file.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "scanner.h"
+
+namespace tsg {
+
+struct DfaTable {
+  uint32_t nstates = 0;     // state 0 = start; state `dead` = no match possible
+  uint32_t nclasses = 0;
+  uint32_t dead = 0;
+  uint8_t byte_class[256] = {0};
+  std::vector<uint16_t> next;          // nstates * nclasses
+  std::vector<uint8_t> accept;         // verify DFA: absorbing accept flag per state
+};
+
+struct ScanDfa {
+  DfaTable t;
+  uint32_t first_out_state = 0;        // states >= this have outputs (renumbered)
+  std::vector<uint32_t> out_off;       // (nstates - first_out_state + 1) offsets into out_ids
+  std::vector<uint32_t> out_ids;       // output ids: [0, nkw) keywords, [nkw, nkw+nanchor) anchors
+  uint32_t max_pattern_bytes = 1;      // warm-up window = max_pattern_bytes - 1
+};
+
+struct AnchorInfo {                    // one literal of one rule
+  uint32_t rule;
+  uint32_t min_len, max_len;           // byte length range of the literal
+  uint32_t dmin, dmax;                 // byte offset of the literal from the match start
+};
+
+struct RuleGpuInfo {
+  uint8_t mode;                        // 0 = anchored (GPU candidates), 1 = FULL (host)
+  uint8_t gate_on_gpu;                 // keyword gate exact on GPU (ASCII keywords)
+  uint8_t always_gate;                 // no keywords (or an empty keyword): gate always true
+  uint32_t kw_begin, kw_count;         // keyword ids in Prefilter::rule_kw
+  uint32_t verify_dfa;                 // index into verify
+  uint32_t verify_limit;               // bytes scanned before giving up (emit conservatively)
+};
+
+struct Prefilter {
+  uint32_t nkw = 0;                    // distinct keyword patterns
+  ScanDfa scan;
+  std::vector<AnchorInfo> anchors;
+  std::vector<RuleGpuInfo> rules;
+  std::vector<uint32_t> rule_kw;       // flattened keyword ids per rule
+  std::vector<DfaTable> verify;
+  std::vector<std::string> kw_text;    // for diagnostics
+  std::string report;                  // human-readable compile summary
+};
+
+bool build_prefilter(const Ruleset& rs, Prefilter* out, std::string* err);
+
+// CPU model of the two GPU passes (used by unit tests to check the compiled
+// tables without a GPU, never by the product path): returns per-rule sorted
+// candidate starts and keyword-gate bits for one file.
+// Returns true when the file contains U+0130 (C4 B0), U+212A (E2 84 AA) or
+// U+017F (C5 BF): the scan DFA is ASCII-only, so such files are evaluated
+// exactly on the host (FilePlan == nullptr).
+bool prefilter_reference_file(const Prefilter& pf, const uint8_t* data, size_t len,
+                              std::vector<std::vector<uint64_t>>* cand_per_rule,
+                              std::vector<uint8_t>* gate_per_rule);
+
+// True when bytes[i-2..i] end one of the fold-special sequences above.
+inline bool fold_special_at(uint8_t p2, uint8_t p1, uint8_t b) {
+  return (b == 0xB0 && p1 == 0xC4) || (b == 0xBF && p1 == 0xC5) || (b == 0xAA && p1 == 0x84 && p2 == 0xE2);
+}
+
+}  // namespace tsg

@@ -1,0 +1,697 @@
+// Exact restatement of pkg/fanal/secret/scanner.go on the host (see scanner.h).
+#include "scanner.h"
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <mutex>
+
+namespace tsg {
+
+#include "builtin_rules.inc"   // kBuiltinRulesJson: trivy_amd/data/builtin_rules.json
+
+namespace {
+
+RegexpPtr compile_or_err(const JValue* v, std::string* err) {
+  if (!v || v->is_null()) return nullptr;
+  std::string e;
+  auto re = re::Regexp::compile(v->as_string(), &e);
+  if (!re) {
+    // scanner.go:80-83: xerrors.Errorf("regexp compile error: %w", err)
+    if (err->empty()) *err = "regexp compile error: " + e;
+    return nullptr;
+  }
+  return RegexpPtr(re.release());
+}
+
+std::vector<std::string> str_list(const JValue* v) {
+  std::vector<std::string> out;
+  if (!v) return out;
+  if (v->kind == JValue::Arr) {
+    for (const auto& x : v->arr) out.push_back(x.as_string());
+  }
+  return out;
+}
+
+std::string field(const JValue* o, const char* k) {
+  const JValue* v = o ? o->get(k) : nullptr;
+  return v ? v->as_string() : "";
+}
+
+bool allow_rules_from(const JValue* v, std::vector<AllowRule>* out, std::string* err) {
+  if (!v || v->kind != JValue::Arr) return true;
+  for (const auto& a : v->arr) {
+    AllowRule r;
+    r.id = field(&a, "id");
+    r.description = field(&a, "description");
+    r.regex = compile_or_err(a.get("regex"), err);
+    r.path = compile_or_err(a.get("path"), err);
+    if (!err->empty()) return false;
+    out->push_back(std::move(r));
+  }
+  return true;
+}
+
+bool exclude_from(const JValue* v, std::vector<RegexpPtr>* out, std::string* err) {
+  if (!v || v->kind != JValue::Obj) return true;
+  const JValue* rx = v->get("regexes");
+  if (!rx || rx->kind != JValue::Arr) return true;
+  for (const auto& r : rx->arr) {
+    RegexpPtr p = compile_or_err(&r, err);
+    if (!err->empty()) return false;
+    out->push_back(p);
+  }
+  return true;
+}
+
+// scanner.go:309-318
+std::string convert_severity(const std::string& s) {
+  std::string lo, up;
+  for (char c : s) { lo.push_back(static_cast<char>(tolower(static_cast<unsigned char>(c)))); }
+  if (lo == "low" || lo == "medium" || lo == "high" || lo == "critical" || lo == "unknown") {
+    for (char c : s) up.push_back(static_cast<char>(toupper(static_cast<unsigned char>(c))));
+    return up;
+  }
+  return "UNKNOWN";
+}
+
+void finish_rule(Rule* r) {
+  for (const auto& k : r->keywords) r->keywords_lower.push_back(go_str_to_lower(k));
+  r->secret_groups.clear();
+  if (r->regex && !r->secret_group_name.empty()) {
+    const auto& names = r->regex->subexp_names();
+    for (size_t i = 0; i < names.size(); ++i) {
+      if (names[i] == r->secret_group_name) r->secret_groups.push_back(static_cast<int>(i));
+    }
+  }
+}
+
+bool load_builtins(std::vector<Rule>* rules, std::vector<AllowRule>* allows, std::string* err) {
+  static std::once_flag once;
+  static std::vector<Rule> b_rules;
+  static std::vector<AllowRule> b_allow;
+  static std::string b_err;
+  std::call_once(once, [] {
+    JValue doc;
+    if (!json_parse(kBuiltinRulesJson, &doc, &b_err)) return;
+    for (const auto& j : doc.get("rules")->arr) {
+      Rule r;
+      r.id = field(&j, "id");
+      r.category = field(&j, "category");
+      r.title = field(&j, "title");
+      r.severity = field(&j, "severity");
+      r.regex = compile_or_err(j.get("regex"), &b_err);
+      r.keywords = str_list(j.get("keywords"));
+      r.secret_group_name = field(&j, "secret_group_name");
+      finish_rule(&r);
+      b_rules.push_back(std::move(r));
+    }
+    allow_rules_from(doc.get("allow_rules"), &b_allow, &b_err);
+  });
+  if (!b_err.empty()) { *err = "builtin rules: " + b_err; return false; }
+  *rules = b_rules;
+  *allows = b_allow;
+  return true;
+}
+
+bool contains(const std::vector<std::string>& v, const std::string& s) {
+  return std::find(v.begin(), v.end(), s) != v.end();
+}
+
+}  // namespace
+
+bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
+  std::vector<Rule> b_rules;
+  std::vector<AllowRule> b_allow;
+  if (!load_builtins(&b_rules, &b_allow, err)) return false;
+  if (!cfg || cfg->is_null()) {                       // scanner.go:324-332
+    out->rules = std::move(b_rules);
+    out->allow_rules = std::move(b_allow);
+    out->exclude_block.clear();
+    return true;
+  }
+  std::vector<std::string> enable = str_list(cfg->get("enable-builtin-rules"));
+  std::vector<std::string> disable = str_list(cfg->get("disable-rules"));
+  std::vector<std::string> disable_allow = str_list(cfg->get("disable-allow-rules"));
+  std::vector<Rule> custom;
+  if (const JValue* rl = cfg->get("rules")) {
+    if (rl->kind == JValue::Arr) {
+      for (const auto& j : rl->arr) {
+        Rule r;
+        r.id = field(&j, "id");
+        r.category = field(&j, "category");
+        r.title = field(&j, "title");
+        r.severity = convert_severity(field(&j, "severity"));   // scanner.go:301-304
+        r.regex = compile_or_err(j.get("regex"), err);
+        r.keywords = str_list(j.get("keywords"));
+        r.path = compile_or_err(j.get("path"), err);
+        if (!allow_rules_from(j.get("allow-rules"), &r.allow_rules, err)) return false;
+        if (!exclude_from(j.get("exclude-block"), &r.exclude_block, err)) return false;
+        r.secret_group_name = field(&j, "secret-group-name");
+        if (!err->empty()) return false;
+        finish_rule(&r);
+        custom.push_back(std::move(r));
+      }
+    }
+  }
+  std::vector<AllowRule> custom_allow;
+  if (!allow_rules_from(cfg->get("allow-rules"), &custom_allow, err)) return false;
+  std::vector<RegexpPtr> excl;
+  if (!exclude_from(cfg->get("exclude-block"), &excl, err)) return false;
+
+  std::vector<Rule> enabled;                          // scanner.go:334-348
+  for (auto& r : b_rules) {
+    if (enable.empty() || contains(enable, r.id)) enabled.push_back(r);
+  }
+  for (auto& r : custom) enabled.push_back(std::move(r));
+  out->rules.clear();
+  for (auto& r : enabled) {
+    if (!contains(disable, r.id)) out->rules.push_back(std::move(r));
+  }
+  out->allow_rules.clear();                           // scanner.go:350-354
+  for (auto& a : b_allow) if (!contains(disable_allow, a.id)) out->allow_rules.push_back(a);
+  for (auto& a : custom_allow) if (!contains(disable_allow, a.id)) out->allow_rules.push_back(a);
+  out->exclude_block = std::move(excl);
+  return true;
+}
+
+// ---------------------------------------------------------------- helpers
+std::string go_bytes_to_lower(const uint8_t* s, size_t n) {
+  bool ascii = true;
+  for (size_t i = 0; i < n; ++i) if (s[i] >= 0x80) { ascii = false; break; }
+  std::string out;
+  out.resize(n);
+  if (ascii) {
+    for (size_t i = 0; i < n; ++i) {
+      uint8_t c = s[i];
+      out[i] = static_cast<char>((c >= 'A' && c <= 'Z') ? c + 32 : c);
+    }
+    return out;
+  }
+  out.clear();
+  out.reserve(n + 16);
+  size_t i = 0;
+  while (i < n) {
+    int32_t r; int w;
+    re::decode_rune(s + i, n - i, &r, &w);
+    re::append_utf8(&out, re::to_lower(static_cast<uint32_t>(r)));   // invalid byte: r == U+FFFD
+    i += w;
+  }
+  return out;
+}
+
+std::string go_str_to_lower(const std::string& s) {
+  return go_bytes_to_lower(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+}
+
+std::string go_quote(const std::string& s) {
+  std::string out = "\"";
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(s.data());
+  size_t i = 0, n = s.size();
+  char buf[16];
+  while (i < n) {
+    int32_t r; int w;
+    re::decode_rune(p + i, n - i, &r, &w);
+    if (r == 0xFFFD && w == 1) { snprintf(buf, sizeof buf, "\\x%02x", p[i]); out += buf; i += 1; continue; }
+    if (r == '"' || r == '\\') { out.push_back('\\'); out.push_back(static_cast<char>(r)); }
+    else if (r < 0x80 && r >= 0x20 && r != 0x7f) out.push_back(static_cast<char>(r));
+    else if (r >= 0x80 && re::is_print(static_cast<uint32_t>(r))) out.append(s, i, w);
+    else {
+      switch (r) {
+        case '\a': out += "\\a"; break;
+        case '\b': out += "\\b"; break;
+        case '\f': out += "\\f"; break;
+        case '\n': out += "\\n"; break;
+        case '\r': out += "\\r"; break;
+        case '\t': out += "\\t"; break;
+        case '\v': out += "\\v"; break;
+        default:
+          if (r < 0x80) snprintf(buf, sizeof buf, "\\x%02x", r);
+          else if (r < 0x10000) snprintf(buf, sizeof buf, "\\u%04x", r);
+          else snprintf(buf, sizeof buf, "\\U%08x", r);
+          out += buf;
+      }
+    }
+    i += w;
+  }
+  out += "\"";
+  return out;
+}
+
+bool go_is_binary(const uint8_t* head, size_t n) {          // utils.go:68-86
+  n = std::min<size_t>(n, 300);
+  for (size_t i = 0; i < n; ++i) {
+    uint8_t b = head[i];
+    if (b < 7 || b == 11 || (13 < b && b < 27) || (27 < b && b < 0x20) || b == 0x7f) return true;
+  }
+  return false;
+}
+
+std::string go_extract_printable(const uint8_t* s, size_t n) {   // utils.go:111-143
+  std::string out, cur;
+  for (size_t i = 0; i < n; ++i) {
+    if (re::is_print(s[i])) { cur.push_back(static_cast<char>(s[i])); continue; }
+    if (cur.size() > 4) { cur.push_back('\n'); out += cur; }
+    cur.clear();
+  }
+  if (cur.size() > 4) { cur.push_back('\n'); out += cur; }
+  return out;
+}
+
+// ------------------------------------------------------ candidate find-all
+namespace {
+
+// Is `s` a rune boundary of the decoding chain that starts at boundary `pos`?
+bool chain_boundary(const uint8_t* t, size_t len, size_t pos, size_t s) {
+  if (s == pos || s >= len) return s <= len;
+  if ((t[s] & 0xC0) != 0x80) return true;            // not a continuation byte
+  size_t q = s;
+  while (q > pos && (t[q] & 0xC0) == 0x80 && s - q < 4) --q;
+  if ((t[q] & 0xC0) == 0x80 && q != pos) return true;  // >=4 continuation bytes: all invalid, width 1
+  // decode forward from q (a chain boundary) until reaching >= s
+  size_t x = q;
+  while (x < s) {
+    int32_t r; int w;
+    re::decode_rune(t + x, len - x, &r, &w);
+    x += w;
+  }
+  return x == s;
+}
+
+}  // namespace
+
+void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t len,
+                              const std::vector<uint64_t>& starts, bool submatch,
+                              std::vector<int>* out) {
+  const int ncap = 2 * (re.num_subexp() + 1);
+  std::vector<int> caps(ncap);
+  size_t pos = 0;
+  long prev_end = -1;
+  size_t idx = 0;
+  while (pos <= len) {
+    // leftmost match with start >= pos: first candidate with an anchored match
+    bool found = false;
+    while (idx < starts.size()) {
+      size_t s = starts[idx];
+      if (s < pos) { ++idx; continue; }
+      if (s > len) { idx = starts.size(); break; }
+      if (chain_boundary(text, len, pos, s) && re.match_at(text, len, s, true, ncap, caps.data())) {
+        found = true;
+        break;
+      }
+      ++idx;
+    }
+    if (!found) break;
+    bool accept = true;
+    if (static_cast<size_t>(caps[1]) == pos) {
+      if (caps[0] == prev_end) accept = false;
+      int32_t r; int w;
+      re::decode_rune(text + pos, len - pos, &r, &w);
+      pos = w > 0 ? pos + w : len + 1;
+    } else {
+      pos = static_cast<size_t>(caps[1]);
+    }
+    prev_end = caps[1];
+    if (accept) {
+      if (submatch) out->insert(out->end(), caps.begin(), caps.end());
+      else { out->push_back(caps[0]); out->push_back(caps[1]); }
+    }
+  }
+}
+
+// ------------------------------------------------------------------- Scan
+namespace {
+
+bool allow_path(const std::vector<AllowRule>& rules, const std::string& path) {
+  for (const auto& r : rules) {
+    if (r.path && r.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) return true;
+  }
+  return false;
+}
+
+bool allow_match(const std::vector<AllowRule>& rules, const uint8_t* m, size_t n) {
+  for (const auto& r : rules) {
+    if (r.regex && r.regex->match_string(m, n)) return true;
+  }
+  return false;
+}
+
+struct Loc { long start, end; };
+
+class Blocks {                                        // scanner.go:237-275
+ public:
+  Blocks(const uint8_t* c, size_t n, const std::vector<RegexpPtr>& rx) : c_(c), n_(n), rx_(rx) {}
+  bool match(const Loc& l) {
+    if (!done_) {
+      done_ = true;
+      std::vector<int> m;
+      for (const auto& r : rx_) {
+        if (!r) continue;
+        m.clear();
+        r->find_all(c_, n_, false, &m);
+        for (size_t k = 0; k + 1 < m.size(); k += 2) locs_.push_back({m[k], m[k + 1]});
+      }
+    }
+    for (const auto& b : locs_) if (b.start <= l.start && l.end <= b.end) return true;
+    return false;
+  }
+
+ private:
+  const uint8_t* c_;
+  size_t n_;
+  const std::vector<RegexpPtr>& rx_;
+  bool done_ = false;
+  std::vector<Loc> locs_;
+};
+
+// scanner.go:102-148
+void find_locations(const Ruleset& rs, const Rule& rule, const uint8_t* c, size_t n,
+                    const std::vector<uint64_t>* starts, std::vector<Loc>* locs, int* error) {
+  if (!rule.regex) return;
+  const bool sub = !rule.secret_group_name.empty();
+  std::vector<int> m;
+  if (starts) find_all_from_candidates(*rule.regex, c, n, *starts, sub, &m);
+  else rule.regex->find_all(c, n, sub, &m);
+  const size_t stride = sub ? 2 * (rule.regex->num_subexp() + 1) : 2;
+  for (size_t k = 0; k + stride <= m.size(); k += stride) {
+    const int s = m[k], e = m[k + 1];
+    // AllowLocation (scanner.go:150-153): global then rule allow regexes on the whole match
+    if (allow_match(rs.allow_rules, c + s, e - s) || allow_match(rule.allow_rules, c + s, e - s)) continue;
+    if (!sub) { locs->push_back({s, e}); continue; }
+    for (int gi : rule.secret_groups) {                // scanner.go:155-168
+      Loc l{m[k + 2 * gi], m[k + 2 * gi + 1]};
+      if (l.start < 0) *error = 1;                     // reference: censorLocation panics on {-1,-1}
+      locs->push_back(l);
+    }
+  }
+}
+
+// sort.Slice (go1.23 sort/zsortfunc.go pdqsort_func), restated.
+class GoSort {
+ public:
+  using Less = std::function<bool(size_t, size_t)>;
+  GoSort(std::vector<Finding>* v, Less less) : v_(v), less_(std::move(less)) {}
+  void run() {
+    size_t n = v_->size();
+    int limit = 0;
+    for (size_t x = n; x; x >>= 1) ++limit;
+    pdq(0, static_cast<long>(n), limit);
+  }
+
+ private:
+  std::vector<Finding>* v_;
+  Less less_;
+  bool lt(long i, long j) { return less_(i, j); }
+  void sw(long i, long j) { std::swap((*v_)[i], (*v_)[j]); }
+
+  void ins(long a, long b) {
+    for (long i = a + 1; i < b; ++i)
+      for (long j = i; j > a && lt(j, j - 1); --j) sw(j, j - 1);
+  }
+  void sift(long lo, long hi, long first) {
+    long root = lo;
+    for (;;) {
+      long child = 2 * root + 1;
+      if (child >= hi) return;
+      if (child + 1 < hi && lt(first + child, first + child + 1)) ++child;
+      if (!lt(first + root, first + child)) return;
+      sw(first + root, first + child);
+      root = child;
+    }
+  }
+  void heap(long a, long b) {
+    long first = a, lo = 0, hi = b - a;
+    for (long i = (hi - 1) / 2; i >= 0; --i) sift(i, hi, first);
+    for (long i = hi - 1; i >= 0; --i) { sw(first, first + i); sift(lo, i, first); }
+  }
+  enum Hint { kUnknown, kIncreasing, kDecreasing };
+  void pdq(long a, long b, int limit) {
+    bool was_balanced = true, was_partitioned = true;
+    for (;;) {
+      long length = b - a;
+      if (length <= 12) { ins(a, b); return; }
+      if (limit == 0) { heap(a, b); return; }
+      if (!was_balanced) { break_patterns(a, b); --limit; }
+      Hint hint;
+      long pivot = choose_pivot(a, b, &hint);
+      if (hint == kDecreasing) {
+        reverse(a, b);
+        pivot = (b - 1) - (pivot - a);
+        hint = kIncreasing;
+      }
+      if (was_balanced && was_partitioned && hint == kIncreasing) {
+        if (partial_ins(a, b)) return;
+      }
+      if (a > 0 && !lt(a - 1, pivot)) {
+        a = partition_equal(a, b, pivot);
+        continue;
+      }
+      bool already;
+      long mid = partition(a, b, pivot, &already);
+      was_partitioned = already;
+      long left = mid - a, right = b - mid;
+      long thr = length / 8;
+      if (left < right) {
+        was_balanced = left >= thr;
+        pdq(a, mid, limit);
+        a = mid + 1;
+      } else {
+        was_balanced = right >= thr;
+        pdq(mid + 1, b, limit);
+        b = mid;
+      }
+    }
+  }
+  long partition(long a, long b, long pivot, bool* already) {
+    sw(a, pivot);
+    long i = a + 1, j = b - 1;
+    while (i <= j && lt(i, a)) ++i;
+    while (i <= j && !lt(j, a)) --j;
+    if (i > j) { sw(j, a); *already = true; return j; }
+    sw(i, j); ++i; --j;
+    for (;;) {
+      while (i <= j && lt(i, a)) ++i;
+      while (i <= j && !lt(j, a)) --j;
+      if (i > j) break;
+      sw(i, j); ++i; --j;
+    }
+    sw(j, a);
+    *already = false;
+    return j;
+  }
+  long partition_equal(long a, long b, long pivot) {
+    sw(a, pivot);
+    long i = a + 1, j = b - 1;
+    for (;;) {
+      while (i <= j && !lt(a, i)) ++i;
+      while (i <= j && lt(a, j)) --j;
+      if (i > j) break;
+      sw(i, j); ++i; --j;
+    }
+    return i;
+  }
+  bool partial_ins(long a, long b) {
+    long i = a + 1;
+    for (int step = 0; step < 5; ++step) {
+      while (i < b && !lt(i, i - 1)) ++i;
+      if (i == b) return true;
+      if (b - a < 50) return false;
+      sw(i, i - 1);
+      if (i - a >= 2) {
+        for (long j = i - 1; j >= 1; --j) { if (!lt(j, j - 1)) break; sw(j, j - 1); }
+      }
+      if (b - i >= 2) {
+        for (long j = i + 1; j < b; ++j) { if (!lt(j, j - 1)) break; sw(j, j - 1); }
+      }
+    }
+    return false;
+  }
+  void break_patterns(long a, long b) {
+    long length = b - a;
+    if (length >= 8) {
+      uint64_t r = static_cast<uint64_t>(length);
+      int bits = 0;
+      for (uint64_t x = static_cast<uint64_t>(length); x; x >>= 1) ++bits;
+      uint64_t modulus = 1ull << bits;
+      long idx = a + (length / 4) * 2 - 1;
+      for (int i = 0; i < 3; ++i) {
+        r ^= r << 13; r ^= r >> 7; r ^= r << 17;
+        long other = static_cast<long>(r & (modulus - 1));
+        if (other >= length) other -= length;
+        sw(idx - 1 + i, a + other);
+      }
+    }
+  }
+  long median(long x, long y, long z, int* swaps) {
+    auto order2 = [&](long& p, long& q) { if (lt(q, p)) { ++*swaps; std::swap(p, q); } };
+    order2(x, y);
+    order2(y, z);
+    order2(x, y);
+    return y;
+  }
+  long choose_pivot(long a, long b, Hint* hint) {
+    long l = b - a;
+    int swaps = 0;
+    long i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    if (l >= 8) {
+      if (l >= 50) {
+        i = median(i - 1, i, i + 1, &swaps);
+        j = median(j - 1, j, j + 1, &swaps);
+        k = median(k - 1, k, k + 1, &swaps);
+      }
+      j = median(i, j, k, &swaps);
+    }
+    *hint = swaps == 0 ? kIncreasing : swaps == 12 ? kDecreasing : kUnknown;
+    return j;
+  }
+  void reverse(long a, long b) {
+    for (long i = a, j = b - 1; i < j; ++i, --j) sw(i, j);
+  }
+};
+
+// scanner.go:495-558 on the censored buffer, with a newline index built once.
+struct LineIndex {
+  const uint8_t* c;
+  size_t n;
+  std::vector<size_t> nl;    // positions of '\n'
+  LineIndex(const uint8_t* cc, size_t nn) : c(cc), n(nn) {
+    const uint8_t* p = c;
+    const uint8_t* end = c + n;
+    while (p < end) {
+      const void* q = memchr(p, '\n', end - p);
+      if (!q) break;
+      nl.push_back(static_cast<const uint8_t*>(q) - c);
+      p = static_cast<const uint8_t*>(q) + 1;
+    }
+  }
+  size_t count_before(size_t pos) const { return std::lower_bound(nl.begin(), nl.end(), pos) - nl.begin(); }
+  // bytes of line k (0-based) of bytes.Split(content, "\n")
+  void line(size_t k, size_t* b, size_t* e) const {
+    *b = k == 0 ? 0 : nl[k - 1] + 1;
+    *e = k < nl.size() ? nl[k] : n;
+  }
+};
+
+Finding to_finding(const Rule& rule, Loc loc, const uint8_t* c, size_t n, const LineIndex& li) {
+  Finding f;                                          // scanner.go:475-488
+  f.rule_id = rule.id;
+  f.category = rule.category;
+  f.severity = rule.severity.empty() ? "UNKNOWN" : rule.severity;
+  f.title = rule.title;
+  const size_t start = static_cast<size_t>(loc.start), end = static_cast<size_t>(loc.end);
+  const size_t start_line = li.count_before(start);
+  size_t line_start, line_end;
+  li.line(start_line, &line_start, &line_end);        // LastIndex / Index of '\n' around start
+  if (line_end - line_start > 100) {
+    line_start = (static_cast<long>(start) - static_cast<long>(line_start) - 30 < 0) ? line_start : start - 30;
+    line_end = (end + 20 > line_end) ? line_end : end + 20;
+  }
+  std::string match_line(reinterpret_cast<const char*>(c) + line_start, line_end - line_start);
+  const size_t end_line = start_line + (li.count_before(end) - li.count_before(start));
+  const size_t nlines = li.nl.size() + 1;
+  const size_t code_start = start_line >= 2 ? start_line - 2 : 0;
+  const size_t code_end = std::min(end_line + 2, nlines);
+  bool found_first = false;
+  for (size_t k = code_start; k < code_end; ++k) {
+    size_t b, e;
+    li.line(k, &b, &e);
+    const bool in_cause = k >= start_line && k <= end_line;
+    std::string s;
+    if (e - b > 100) s = in_cause ? match_line : std::string(reinterpret_cast<const char*>(c) + b, 100);
+    else s.assign(reinterpret_cast<const char*>(c) + b, e - b);
+    Line ln;
+    ln.number = static_cast<int>(k + 1);
+    ln.content = s;
+    ln.is_cause = in_cause;
+    ln.highlighted = s;
+    ln.first_cause = !found_first && in_cause;
+    found_first = found_first || in_cause;
+    f.code.push_back(std::move(ln));
+  }
+  for (size_t k = f.code.size(); k-- > 0;) {
+    if (f.code[k].is_cause) { f.code[k].last_cause = true; break; }
+  }
+  f.start_line = static_cast<int>(start_line + 1);
+  f.end_line = static_cast<int>(end_line + 1);
+  f.match = std::move(match_line);
+  return f;
+}
+
+bool keywords_match(const Rule& r, const std::string& lower) {   // scanner.go:174-186
+  if (r.keywords.empty()) return true;
+  for (const auto& kw : r.keywords_lower) {
+    if (kw.empty()) return true;
+    if (lower.find(kw) != std::string::npos) return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
+                 bool binary, const FilePlan* plan) {
+  Secret out;
+  if (allow_path(rs.allow_rules, path)) { out.file_path = path; return out; }   // scanner.go:381-386
+  std::string lower;
+  bool have_lower = false;
+  auto lowered = [&]() -> const std::string& {
+    if (!have_lower) { lower = go_bytes_to_lower(content, len); have_lower = true; }
+    return lower;
+  };
+  Blocks gblocks(content, len, rs.exclude_block);
+  struct M { const Rule* rule; Loc loc; };
+  std::vector<M> matched;
+  std::vector<uint8_t> censored;
+  size_t cand_i = 0;
+  std::vector<Loc> locs;
+  for (size_t ri = 0; ri < rs.rules.size(); ++ri) {
+    const Rule& rule = rs.rules[ri];
+    const uint8_t kind = plan ? plan->kind[ri] : static_cast<uint8_t>(kPlanFull);
+    const std::vector<uint64_t>* starts = nullptr;
+    if (plan) {
+      while (cand_i < plan->cands.size() && plan->cands[cand_i].rule < ri) ++cand_i;
+      if (cand_i < plan->cands.size() && plan->cands[cand_i].rule == ri) starts = &plan->cands[cand_i].starts;
+    }
+    if (rule.path && !rule.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) continue;
+    if (allow_path(rule.allow_rules, path)) continue;
+    if (kind == kPlanSkip) continue;
+    if ((kind == kPlanFull || kind == kPlanCandHostGate) && !keywords_match(rule, lowered())) continue;
+    if (kind == kPlanNoMatch) continue;
+    locs.clear();
+    static const std::vector<uint64_t> kEmpty;
+    const std::vector<uint64_t>* use = nullptr;
+    if (kind == kPlanCandidates || kind == kPlanCandHostGate) use = starts ? starts : &kEmpty;
+    find_locations(rs, rule, content, len, use, &locs, &out.error);
+    if (locs.empty()) continue;
+    Blocks lblocks(content, len, rule.exclude_block);
+    for (const Loc& l : locs) {
+      if (l.start < 0) continue;                      // reference panics here (error flagged)
+      if (gblocks.match(l) || lblocks.match(l)) continue;
+      matched.push_back({&rule, l});
+      if (censored.empty() && len > 0) censored.assign(content, content + len);
+      if (censored.size() < len) censored.resize(len);
+      for (long k = l.start; k < l.end; ++k) censored[k] = '*';
+    }
+  }
+  if (matched.empty()) return out;                    // types.Secret{}
+  LineIndex li(censored.data(), len);
+  for (const auto& m : matched) {
+    Finding f = to_finding(*m.rule, m.loc, censored.data(), len, li);
+    if (binary) {
+      f.match = "Binary file " + go_quote(path) + " matches a rule " + go_quote(m.rule->title);
+      f.code.clear();
+    }
+    out.findings.push_back(std::move(f));
+  }
+  auto& fs = out.findings;
+  GoSort(&fs, [&fs](size_t i, size_t j) {
+    if (fs[i].rule_id != fs[j].rule_id) return fs[i].rule_id < fs[j].rule_id;
+    return fs[i].match < fs[j].match;
+  }).run();
+  out.file_path = path;
+  return out;
+}
+
+}  // namespace tsg
+
+extern "C" const char* tsg_builtin_json_ptr() { return tsg::kBuiltinRulesJson; }

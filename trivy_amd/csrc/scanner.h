@@ -1,0 +1,109 @@
+// Host side of the secret scanner: rule model and the exact `Scan` semantics of
+// pkg/fanal/secret/scanner.go, restricted by a per-(file, rule) plan that the
+// GPU prefilter produces.  With no plan this is the reference algorithm
+// (every rule's keyword gate and full find-all evaluated on the host).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "goregexp.h"
+#include "json.h"
+
+namespace tsg {
+
+using RegexpPtr = std::shared_ptr<re::Regexp>;
+
+struct AllowRule {                       // scanner.go:196-201
+  std::string id, description;
+  RegexpPtr regex, path;
+};
+
+struct Rule {                            // scanner.go:89-100
+  std::string id, category, title, severity;
+  RegexpPtr regex;                       // may be null (scanner.go:103-105)
+  std::vector<std::string> keywords;
+  std::vector<std::string> keywords_lower;   // strings.ToLower(kw)
+  RegexpPtr path;
+  std::vector<AllowRule> allow_rules;
+  std::vector<RegexpPtr> exclude_block;
+  std::string secret_group_name;
+  std::vector<int> secret_groups;        // i with SubexpNames()[i] == SecretGroupName
+};
+
+struct Ruleset {                         // scanner.go:45-49 (Global)
+  std::vector<Rule> rules;
+  std::vector<AllowRule> allow_rules;
+  std::vector<RegexpPtr> exclude_block;
+};
+
+// ParseConfig (already decoded from YAML to JSON) + NewScanner: builtin rules
+// and allow rules, enable/disable filters, custom rules appended
+// (scanner.go:277-364).  cfg == nullptr -> builtins only.
+bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err);
+
+struct Line {                            // types.Line (misconf.go:51-60)
+  int number = 0;
+  std::string content;
+  bool is_cause = false;
+  std::string annotation;
+  bool truncated = false;
+  std::string highlighted;
+  bool first_cause = false, last_cause = false;
+};
+
+struct Finding {                         // types.SecretFinding (secret.go:10-20)
+  std::string rule_id, category, severity, title;
+  int start_line = 0, end_line = 0;
+  std::vector<Line> code;
+  std::string match;
+};
+
+struct Secret {                          // types.Secret
+  std::string file_path;
+  std::vector<Finding> findings;
+  int error = 0;                         // nonzero: the reference would panic on this file
+};
+
+// Per-(file, rule) plan from the GPU prefilter.
+enum PlanKind : uint8_t {
+  kPlanSkip = 0,        // keyword gate false (MatchKeywords == false)
+  kPlanNoMatch = 1,     // gate true; no regex match can exist in the file
+  kPlanCandidates = 2,  // gate true; every match start lies in `starts`
+  kPlanFull = 3,        // host evaluates the gate and a full find-all
+  kPlanCandHostGate = 4 // host evaluates the gate exactly; matches only from `starts`
+};
+
+struct RuleCandidates {
+  uint32_t rule;
+  std::vector<uint64_t> starts;          // sorted, unique byte offsets (superset of match starts)
+};
+
+struct FilePlan {
+  std::vector<uint8_t> kind;             // one PlanKind per rule
+  std::vector<RuleCandidates> cands;     // sorted by rule
+};
+
+// bytes.ToLower (ASCII fast path; Map(unicode.ToLower) with invalid bytes -> U+FFFD)
+std::string go_bytes_to_lower(const uint8_t* s, size_t n);
+std::string go_str_to_lower(const std::string& s);
+// fmt "%q"
+std::string go_quote(const std::string& s);
+
+// Scanner.Scan (scanner.go:377-463).  plan == nullptr: reference algorithm.
+Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
+                 bool binary, const FilePlan* plan);
+
+// Exact Go FindAll(Submatch)Index restricted to candidate start offsets.
+// `starts` must be a sorted superset of every position where an anchored
+// match can start; the result equals re.find_all(text).
+void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t len,
+                              const std::vector<uint64_t>& starts, bool submatch,
+                              std::vector<int>* out);
+
+// SecretAnalyzer helpers (pkg/fanal/analyzer/secret/secret.go:103-190, utils.go:68-143)
+bool go_is_binary(const uint8_t* head, size_t n);
+std::string go_extract_printable(const uint8_t* s, size_t n);
+
+}  // namespace tsg

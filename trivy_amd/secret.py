@@ -1,0 +1,213 @@
+"""Host-side mirror of github.com/aquasecurity/trivy/pkg/fanal/secret.
+
+Same names, argument meaning and error behaviour as the reference package
+(pkg/fanal/secret/scanner.go), backed by the MI355X engine behind the C-ABI in
+include/trivy_secret.h:
+
+  ParseConfig(config_path) -> Config | None     scanner.go:277-307
+  NewScanner(config)       -> Scanner           scanner.go:320-364
+  Scanner.Scan(ScanArgs)   -> types.Secret      scanner.go:377-463
+  Scanner.ScanBatch([ScanArgs]) -> [types.Secret]   (batched entry)
+  GetBuiltinRules()                             builtin-rules.go:87-89
+
+types.Secret is returned as a dict with the Go field names
+({"FilePath", "Findings": [{"RuleID", ..., "Code": {"Lines": [...]}, "Match"}]});
+Go byte strings are decoded with 'surrogateescape'.  Scan runs on the GPU; a
+machine without a HIP device raises instead of silently scanning on the CPU.
+"""
+import ctypes
+import json
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import yaml
+
+from . import _lib
+
+
+class ConfigError(Exception):
+    """ParseConfig failure (file open, YAML decode, regexp compile)."""
+
+
+class _GoStringLoader(yaml.SafeLoader):
+    """yaml.SafeLoader that keeps every plain scalar a string (yaml.v3 decoding
+    into the string fields of secret.Config), except null."""
+
+
+_GoStringLoader.yaml_implicit_resolvers = {
+    k: [(tag, rx) for tag, rx in v if tag == "tag:yaml.org,2002:null"]
+    for k, v in yaml.SafeLoader.yaml_implicit_resolvers.items()
+}
+
+
+def load_yaml(path):
+    with open(path, "rb") as f:
+        return yaml.load(f, Loader=_GoStringLoader)  # noqa: S506 (SafeLoader subclass)
+
+
+@dataclass
+class ScanArgs:                       # scanner.go:366-370
+    FilePath: str
+    Content: bytes
+    Binary: bool = False
+
+
+def ParseConfig(config_path):
+    """nil for an empty path or a missing file (builtin rules only)."""
+    if not config_path:
+        return None
+    if not os.path.exists(config_path):
+        return None
+    try:
+        doc = load_yaml(config_path)
+    except yaml.YAMLError as e:
+        raise ConfigError("secrets config decode error: %s" % e)
+    if doc is None:
+        doc = {}
+    if not isinstance(doc, dict):
+        raise ConfigError("secrets config decode error: not a mapping")
+    return doc
+
+
+def GetBuiltinRules():
+    return json.loads(_lib.lib().tsg_builtin_rules_json().decode("utf-8"))["rules"]
+
+
+def _device_default():
+    v = os.environ.get("TSG_DEVICE") or os.environ.get("LOCAL_RANK") or "0"
+    return int(v)
+
+
+class Scanner:
+    """NewScanner(config) + Scan.  The ruleset is compiled once; the GPU
+    engine is created on first use on `device` (default LOCAL_RANK or 0)."""
+
+    def __init__(self, config=None, device=None, threads=0):
+        L = _lib.lib()
+        rs = ctypes.c_void_p()
+        if config is None:
+            _lib.check(L.tsg_ruleset_compile(None, 0, ctypes.byref(rs)))
+        else:
+            js = json.dumps(config, ensure_ascii=True).encode("utf-8")
+            rc = L.tsg_ruleset_compile(js, len(js), ctypes.byref(rs))
+            if rc != 0:
+                raise ConfigError(L.tsg_last_error().decode("utf-8", "replace"))
+        self._rs = rs
+        self._engine = None
+        self._device = _device_default() if device is None else device
+        self._threads = threads
+
+    def __del__(self):
+        try:
+            L = _lib.lib()
+            if self._engine:
+                L.tsg_engine_destroy(self._engine)
+            if self._rs:
+                L.tsg_ruleset_free(self._rs)
+        except Exception:
+            pass
+
+    @property
+    def rule_ids(self):
+        L = _lib.lib()
+        return [L.tsg_ruleset_rule_id(self._rs, i).decode("utf-8", "surrogateescape")
+                for i in range(L.tsg_ruleset_num_rules(self._rs))]
+
+    def AllowPath(self, path):          # scanner.go:56-59
+        b = path.encode("utf-8", "surrogateescape")
+        return _lib.lib().tsg_ruleset_allow_path(self._rs, b, len(b)) == 1
+
+    def engine(self):
+        if self._engine is None:
+            L = _lib.lib()
+            e = ctypes.c_void_p()
+            _lib.check(L.tsg_engine_create(self._rs, self._device, ctypes.byref(e)))
+            if self._threads:
+                L.tsg_engine_set_threads(e, self._threads)
+            self._engine = e
+        return self._engine
+
+    def report(self):
+        return _lib.lib().tsg_engine_report(self.engine()).decode("utf-8", "replace")
+
+    def Scan(self, args):
+        return self.ScanBatch([args])[0]
+
+    def ScanBatch(self, args_list, with_stats=False):
+        data, offsets = pack(args_list)
+        paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
+        binary = np.array([1 if a.Binary else 0 for a in args_list] or [0], dtype=np.uint8)
+        res = ctypes.c_void_p()
+        _lib.check(_lib.lib().tsg_scan_batch(self.engine(), data.ctypes.data, offsets.ctypes.data,
+                                             len(args_list), paths, lens, binary.ctypes.data,
+                                             ctypes.byref(res)))
+        try:
+            out = _lib.result_json(res)
+            stats = _lib.result_stats(res)
+        finally:
+            _lib.lib().tsg_result_free(res)
+        for s in out:
+            s.pop("Error", None)
+        return (out, stats) if with_stats else out
+
+
+NewScanner = Scanner
+
+
+def pack(args_list):
+    """Pack contents back to back: (uint8 data padded by 64 B, uint64 offsets)."""
+    lens = np.fromiter((len(a.Content) for a in args_list), dtype=np.uint64, count=len(args_list))
+    offsets = np.zeros(len(args_list) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.zeros(int(offsets[-1]) + 64, dtype=np.uint8)
+    for a, o in zip(args_list, offsets[:-1]):
+        if len(a.Content):
+            data[int(o):int(o) + len(a.Content)] = np.frombuffer(a.Content, dtype=np.uint8)
+    return data, offsets
+
+
+# ---------------------------------------------------------------- test hooks
+def scan_host_reference(scanner, args_list, threads=1):
+    """The C++ confirmer on every (file, rule) pair, no prefilter (tests only)."""
+    data, offsets = pack(args_list)
+    paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
+    binary = np.array([1 if a.Binary else 0 for a in args_list] or [0], dtype=np.uint8)
+    res = ctypes.c_void_p()
+    _lib.check(_lib.lib().tsg_scan_host_reference(scanner._rs, data.ctypes.data, offsets.ctypes.data,
+                                                  len(args_list), paths, lens, binary.ctypes.data, threads,
+                                                  ctypes.byref(res)))
+    try:
+        out = _lib.result_json(res)
+    finally:
+        _lib.lib().tsg_result_free(res)
+    for s in out:
+        s.pop("Error", None)
+    return out
+
+
+def scan_table_model(scanner, args_list):
+    """CPU model of the compiled GPU tables feeding the confirmer (tests only)."""
+    data, offsets = pack(args_list)
+    paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
+    binary = np.array([1 if a.Binary else 0 for a in args_list] or [0], dtype=np.uint8)
+    res = ctypes.c_void_p()
+    _lib.check(_lib.lib().tsg_scan_table_model(scanner._rs, data.ctypes.data, offsets.ctypes.data,
+                                               len(args_list), paths, lens, binary.ctypes.data,
+                                               ctypes.byref(res)))
+    try:
+        out = _lib.result_json(res)
+    finally:
+        _lib.lib().tsg_result_free(res)
+    for s in out:
+        s.pop("Error", None)
+    return out
+
+
+def prefilter_report(scanner):
+    buf = ctypes.c_void_p()
+    _lib.check(_lib.lib().tsg_prefilter_report(scanner._rs, ctypes.byref(buf)))
+    try:
+        return ctypes.string_at(buf).decode("utf-8", "replace")
+    finally:
+        _lib.lib().tsg_free(buf)
