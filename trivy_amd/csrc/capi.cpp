@@ -343,20 +343,10 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
     const size_t len = offsets[f + 1] - offsets[f];
     std::vector<uint8_t> gate;
     const bool special = prefilter_reference_file(pf, c, len, &r->cands[f], &gate);
-    if (special) {
-      r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, nullptr);
-      continue;
-    }
+    if (special) prefilter_variant_file(pf, c, len, &r->cands[f], &gate);
+    std::vector<std::vector<uint64_t>> tmp = r->cands[f];
     FilePlan plan;
-    plan.kind.assign(nr, kPlanNoMatch);
-    for (size_t k = 0; k < nr; ++k) {
-      const RuleGpuInfo& gi = pf.rules[k];
-      if (gi.mode == 1) plan.kind[k] = kPlanFull;
-      else if (gi.mode == 0 && !r->cands[f][k].empty()) {
-        plan.kind[k] = gi.gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
-        plan.cands.push_back({static_cast<uint32_t>(k), r->cands[f][k]});
-      }
-    }
+    plan_from_candidates(pf, &tmp, &plan);
     r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, &plan);
   }
   *out = r;

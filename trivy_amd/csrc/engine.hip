@@ -523,9 +523,14 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       const bool binary = in.binary ? in.binary[f] != 0 : false;
       const uint32_t cb = per_file[f], ce = per_file[f + 1];
       if (m.h_ff[f]) {
-        // fold-special file: exact host evaluation of every rule
+        // fold-special file (U+0130/U+212A/U+017F present): the two passes run
+        // on the host with the variant scan DFA, then the exact confirmer
         nconf.fetch_add(1);
-        Secret s = scan_file(rs, path, content, len, binary, nullptr);
+        std::vector<std::vector<uint64_t>> vc;
+        std::vector<uint8_t> vg;
+        prefilter_variant_file(pf_, content, len, &vc, &vg);
+        plan_from_candidates(pf_, &vc, &plan);
+        Secret s = scan_file(rs, path, content, len, binary, &plan);
         nfind.fetch_add(s.findings.size());
         (*results)[f] = std::move(s);
         continue;

@@ -766,6 +766,9 @@ inline bool rune_match(const Prog& p, const Inst& in, int32_t c) {
 class Machine {
  public:
   Machine(const Prog& p, int ncap) : p_(p), ncap_(ncap) {
+    if (p.has_first) {
+      for (int b = 0; b < 256; ++b) first_[b] = (p.first[b >> 6] >> (b & 63)) & 1;
+    }
     size_t n = p.inst.size();
     for (int q = 0; q < 2; ++q) {
       sparse_[q].assign(n, 0);
@@ -794,6 +797,16 @@ class Machine {
       if (size_[rq] == 0) {
         if (anchored && pos != pos0) break;
         if (matched_) break;
+        if (!anchored && p_.has_first && pos < len && !first_[s[pos]]) {
+          // no live thread and no match can start here: skip ahead
+          size_t np = pos + 1;
+          while (np < len && !first_[s[np]]) ++np;
+          if (np >= len) break;          // every match consumes a byte
+          pos = np;
+          decode_rune(s + pos, len - pos, &r, &w);
+          if (r >= 0) decode_rune(s + pos + w, len - pos - w, &r1, &w1); else { r1 = -1; w1 = 0; }
+          flag = empty_context(rune_before(s, pos), r);
+        }
       }
       if (!matched_ && (!anchored || pos == pos0)) {
         if (ncap_ > 0) {
@@ -827,6 +840,7 @@ class Machine {
   uint32_t size_[2];
   std::vector<int> matchcap_, scratch_;
   bool matched_ = false;
+  uint8_t first_[256] = {0};
   struct Frame { uint32_t pc; int slot; int old; };
   std::vector<Frame> stack_;
 
@@ -915,6 +929,36 @@ class Machine {
   }
 };
 
+// First-byte set of a program: follow non-consuming instructions from start
+// (assertions treated as passable); a reachable Match means no filter.
+void compute_first(Prog* p) {
+  p->has_first = false;
+  if (p->start == 0) return;
+  std::vector<char> seen(p->inst.size(), 0);
+  std::vector<uint32_t> st{p->start};
+  uint64_t f[4] = {0, 0, 0, 0};
+  auto set = [&](uint32_t b) { f[b >> 6] |= 1ull << (b & 63); };
+  while (!st.empty()) {
+    uint32_t pc = st.back();
+    st.pop_back();
+    if (pc == 0 || seen[pc]) continue;
+    seen[pc] = 1;
+    const Inst& in = p->inst[pc];
+    switch (in.op) {
+      case IOp::Alt: case IOp::AltMatch: st.push_back(in.out); st.push_back(in.arg); break;
+      case IOp::Capture: case IOp::Empty: case IOp::Nop: st.push_back(in.out); break;
+      case IOp::Fail: break;
+      case IOp::Match: case IOp::RuneAny: case IOp::RuneAnyNotNL: return;
+      case IOp::Rune1: case IOp::Rune:
+        for (uint32_t b = 0; b < 128; ++b) if ((in.ascii[b >> 6] >> (b & 63)) & 1) set(b);
+        if (in.nonascii || (in.op == IOp::Rune1 && in.arg >= 0x80)) for (uint32_t b = 0x80; b < 256; ++b) set(b);
+        break;
+    }
+  }
+  std::copy(f, f + 4, p->first);
+  p->has_first = true;
+}
+
 }  // namespace
 
 std::vector<uint32_t> fold_orbit(uint32_t r) {
@@ -985,6 +1029,7 @@ std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string*
   c.patch(f.out, m);
   re->prog_.start = f.i;
   re->nullable_ = f.nullable;
+  compute_first(&re->prog_);
   return re;
 }
 

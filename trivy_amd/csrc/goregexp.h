@@ -62,6 +62,11 @@ struct Prog {
   std::vector<Range> ranges;
   uint32_t start = 0;
   int num_cap = 0;                // capture groups, excluding group 0
+  // Bytes that can begin a match (first byte of the first rune); used to skip
+  // positions in an unanchored search while no thread is alive.  Performance
+  // only: has_first == false when a match may be empty or start anywhere.
+  bool has_first = false;
+  uint64_t first[4] = {0, 0, 0, 0};
 };
 
 // Go utf8.DecodeRune: rune + width; invalid -> 0xFFFD width 1; at end width 0.

@@ -499,11 +499,16 @@ Unit folded_unit(unsigned char c) {
 
 // Keyword (already strings.ToLower'ed, ASCII) under bytes.ToLower semantics.
 // The two non-ASCII runes that lower to ASCII (U+0130 -> 'i', U+212A -> 'k')
-// are not in the DFA: K1 flags files containing them and the host evaluates
-// such files exactly.
-Seq keyword_seq(const std::string& kw) {
+// are only in the host variant DFA: K1 flags files containing them.
+Seq keyword_seq(const std::string& kw, bool variants) {
   Seq s;
-  for (char ch : kw) s.push_back(folded_unit(static_cast<unsigned char>(ch)));
+  for (char ch : kw) {
+    Unit u = folded_unit(static_cast<unsigned char>(ch));
+    if (variants && ch == 'i') u.push_back("\xC4\xB0");
+    if (variants && ch == 'k') u.push_back("\xE2\x84\xAA");
+    std::sort(u.begin(), u.end());
+    s.push_back(u);
+  }
   return s;
 }
 
@@ -512,13 +517,13 @@ Seq keyword_seq(const std::string& kw) {
 // the fold images of ASCII letters (U+212A, U+017F) are dropped -- files that
 // contain them are flagged by K1 and scanned exactly on the host.  The literal
 // is cut before any unit with another non-ASCII alternative.
-Seq scan_form(const Seq& lit) {
+Seq scan_form(const Seq& lit, bool keep_special = false) {
   Seq out;
   for (const Unit& u : lit) {
     Unit f;
     bool ok = true;
     for (const auto& alt : u) {
-      if (alt == "\xE2\x84\xAA" || alt == "\xC5\xBF") continue;
+      if (alt == "\xE2\x84\xAA" || alt == "\xC5\xBF") { if (keep_special) f.push_back(alt); continue; }
       if (alt.size() != 1 || static_cast<unsigned char>(alt[0]) >= 0x80) { ok = false; break; }
       for (const auto& x : folded_unit(static_cast<unsigned char>(alt[0]))) f.push_back(x);
     }
@@ -539,6 +544,7 @@ struct AnchorChoice {
   bool ok = false;
   size_t k = 0;
   SeqSet lits;
+  SeqSet raw;
   uint32_t dmin = 0, dmax = 0;
 };
 
@@ -565,6 +571,7 @@ AnchorChoice choose_anchor(const std::vector<const Node*>& items) {
           best.ok = true;
           best.k = k;
           best.lits = lits;
+          best.raw = raw;
           best.dmin = plo;
           best.dmax = phi;
         }
@@ -632,6 +639,87 @@ bool build_verify(const std::vector<const Node*>& items, size_t min_items, DfaTa
   return false;
 }
 
+bool make_scan_dfa(const Nfa& nfa, int s0, uint32_t maxb, ScanDfa* out, std::string* err) {
+  RawDfa raw;
+  if (!determinize(nfa, s0, true, -1, kScanStateCap, &raw)) { *err = "scan DFA exceeds state cap"; return false; }
+  // outputs per subset; renumber: states without outputs first (start stays 0)
+  std::vector<std::vector<uint32_t>> outs(raw.subsets.size());
+  for (size_t i = 0; i < raw.subsets.size(); ++i) {
+    for (int s : raw.subsets[i]) if (nfa.st[s].out >= 0) outs[i].push_back(static_cast<uint32_t>(nfa.st[s].out));
+    std::sort(outs[i].begin(), outs[i].end());
+    outs[i].erase(std::unique(outs[i].begin(), outs[i].end()), outs[i].end());
+  }
+  if (!outs[0].empty()) { *err = "scan DFA start state has outputs"; return false; }
+  std::vector<uint32_t> order;
+  for (size_t i = 0; i < raw.subsets.size(); ++i) if (outs[i].empty()) order.push_back(static_cast<uint32_t>(i));
+  out->first_out_state = static_cast<uint32_t>(order.size());
+  for (size_t i = 0; i < raw.subsets.size(); ++i) if (!outs[i].empty()) order.push_back(static_cast<uint32_t>(i));
+  if (order.size() > 65535) { *err = "scan DFA too large for 16-bit states"; return false; }
+  out->t = to_table(raw, order, -1);
+  out->out_off.assign(1, 0);
+  out->out_ids.clear();
+  for (size_t i = out->first_out_state; i < order.size(); ++i) {
+    const auto& o = outs[order[i]];
+    out->out_ids.insert(out->out_ids.end(), o.begin(), o.end());
+    out->out_off.push_back(static_cast<uint32_t>(out->out_ids.size()));
+  }
+  out->max_pattern_bytes = maxb;
+  return true;
+}
+
+// The two passes on the host over one file with a given scan DFA.
+void two_pass(const Prefilter& pf, const ScanDfa& sd, const std::vector<AnchorInfo>& anchors,
+              const uint8_t* data, size_t len, std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
+  const DfaTable& t = sd.t;
+  std::vector<uint8_t> kwbit(pf.nkw, 0);
+  struct Hit { uint64_t end; uint32_t anchor; };
+  std::vector<Hit> hits;
+  uint32_t s = 0;
+  for (size_t p = 0; p < len; ++p) {
+    s = t.next[static_cast<size_t>(s) * t.nclasses + t.byte_class[data[p]]];
+    if (s >= sd.first_out_state) {
+      uint32_t o = s - sd.first_out_state;
+      for (uint32_t k = sd.out_off[o]; k < sd.out_off[o + 1]; ++k) {
+        uint32_t id = sd.out_ids[k];
+        if (id < pf.nkw) kwbit[id] = 1; else hits.push_back({p, id - pf.nkw});
+      }
+    }
+  }
+  gate->assign(pf.rules.size(), 0);
+  for (size_t r = 0; r < pf.rules.size(); ++r) {
+    const RuleGpuInfo& gi = pf.rules[r];
+    uint8_t g = gi.always_gate;
+    for (uint32_t k = 0; k < gi.kw_count; ++k) g |= kwbit[pf.rule_kw[gi.kw_begin + k]];
+    (*gate)[r] = g;
+  }
+  cand->assign(pf.rules.size(), {});
+  for (const Hit& h : hits) {
+    const AnchorInfo& a = anchors[h.anchor];
+    if (!(*gate)[a.rule] && pf.rules[a.rule].gate_on_gpu) continue;
+    const RuleGpuInfo& gi = pf.rules[a.rule];
+    const DfaTable& v = pf.verify[gi.verify_dfa];
+    long hi = static_cast<long>(h.end) + 1 - a.min_len - a.dmin;
+    long lo = static_cast<long>(h.end) + 1 - a.max_len - a.dmax;
+    if (lo < 0) lo = 0;
+    for (long st = lo; st <= hi; ++st) {
+      uint32_t q = 0;
+      bool emit = v.accept[0];
+      size_t p = st;
+      for (; !emit && p < len && p - st < gi.verify_limit; ++p) {
+        q = v.next[static_cast<size_t>(q) * v.nclasses + v.byte_class[data[p]]];
+        if (v.accept[q]) emit = true;
+        else if (q == v.dead) break;
+      }
+      if (!emit && q != v.dead && p < len && p - st >= gi.verify_limit) emit = true;   // gave up: conservative
+      if (emit) (*cand)[a.rule].push_back(static_cast<uint64_t>(st));
+    }
+  }
+  for (auto& c : *cand) {
+    std::sort(c.begin(), c.end());
+    c.erase(std::unique(c.begin(), c.end()), c.end());
+  }
+}
+
 }  // namespace
 
 bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
@@ -660,12 +748,14 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
   }
   pf->nkw = static_cast<uint32_t>(pf->kw_text.size());
 
-  // --- scan NFA
-  Nfa scan;
+  // --- scan NFAs (GPU form and host variant form)
+  Nfa scan, host;
   int s0 = scan.add();
-  uint32_t maxb = 1;
+  int h0 = host.add();
+  uint32_t maxb = 1, hmaxb = 1;
   for (uint32_t k = 0; k < pf->nkw; ++k) {
-    maxb = std::max(maxb, add_seq(&scan, s0, keyword_seq(pf->kw_text[k]), static_cast<int>(k)));
+    maxb = std::max(maxb, add_seq(&scan, s0, keyword_seq(pf->kw_text[k], false), static_cast<int>(k)));
+    hmaxb = std::max(hmaxb, add_seq(&host, h0, keyword_seq(pf->kw_text[k], true), static_cast<int>(k)));
   }
   std::string rep;
   for (size_t r = 0; r < rs.rules.size(); ++r) {
@@ -695,36 +785,29 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
       uint32_t id = pf->nkw + static_cast<uint32_t>(pf->anchors.size());
       pf->anchors.push_back(a);
       maxb = std::max(maxb, add_seq(&scan, s0, s, static_cast<int>(id)));
+      // host variant forms of every raw literal with this scan form
+      AnchorInfo ha = a;
+      ha.min_len = 0xffffffffu;
+      ha.max_len = 0;
+      SeqSet vforms;
+      for (const auto& rawlit : ch.raw) if (scan_form(rawlit) == s) vforms.insert(scan_form(rawlit, true));
+      for (const auto& v : vforms) {
+        ha.min_len = std::min(ha.min_len, seq_min_len(v));
+        ha.max_len = std::max(ha.max_len, seq_max_len(v));
+        hmaxb = std::max(hmaxb, add_seq(&host, h0, v, static_cast<int>(id)));
+      }
+      pf->host_anchors.push_back(ha);
     }
     rep += rule.id + ": anchored item " + std::to_string(ch.k) + ", " + std::to_string(ch.lits.size()) +
            " literal(s), offset [" + std::to_string(ch.dmin) + "," + std::to_string(ch.dmax) + "], verify " +
            std::to_string(pf->verify.back().nstates) + " states x " + std::to_string(pf->verify.back().nclasses) +
            " classes, limit " + std::to_string(gi.verify_limit) + note + "\n";
   }
-  RawDfa raw;
-  if (!determinize(scan, s0, true, -1, kScanStateCap, &raw)) { *err = "scan DFA exceeds state cap"; return false; }
-  // outputs per subset; renumber: states without outputs first (start stays 0)
-  std::vector<std::vector<uint32_t>> outs(raw.subsets.size());
-  for (size_t i = 0; i < raw.subsets.size(); ++i) {
-    for (int s : raw.subsets[i]) if (scan.st[s].out >= 0) outs[i].push_back(static_cast<uint32_t>(scan.st[s].out));
-    std::sort(outs[i].begin(), outs[i].end());
-    outs[i].erase(std::unique(outs[i].begin(), outs[i].end()), outs[i].end());
-  }
-  if (!outs[0].empty()) { *err = "scan DFA start state has outputs"; return false; }
-  std::vector<uint32_t> order;
-  for (size_t i = 0; i < raw.subsets.size(); ++i) if (outs[i].empty()) order.push_back(static_cast<uint32_t>(i));
-  pf->scan.first_out_state = static_cast<uint32_t>(order.size());
-  for (size_t i = 0; i < raw.subsets.size(); ++i) if (!outs[i].empty()) order.push_back(static_cast<uint32_t>(i));
-  if (order.size() > 65535) { *err = "scan DFA too large for 16-bit states"; return false; }
-  pf->scan.t = to_table(raw, order, -1);
-  pf->scan.out_off.push_back(0);
-  for (size_t i = pf->scan.first_out_state; i < order.size(); ++i) {
-    const auto& o = outs[order[i]];
-    pf->scan.out_ids.insert(pf->scan.out_ids.end(), o.begin(), o.end());
-    pf->scan.out_off.push_back(static_cast<uint32_t>(pf->scan.out_ids.size()));
-  }
-  pf->scan.max_pattern_bytes = maxb;
-  pf->report = "scan DFA: " + std::to_string(pf->scan.t.nstates) + " states x " + std::to_string(pf->scan.t.nclasses) +
+  if (!make_scan_dfa(scan, s0, maxb, &pf->scan, err)) return false;
+  if (!make_scan_dfa(host, h0, hmaxb, &pf->host_scan, err)) return false;
+  pf->report = "host variant DFA: " + std::to_string(pf->host_scan.t.nstates) + " states x " +
+               std::to_string(pf->host_scan.t.nclasses) + " classes\n" +
+               "scan DFA: " + std::to_string(pf->scan.t.nstates) + " states x " + std::to_string(pf->scan.t.nclasses) +
                " classes (" + std::to_string(pf->scan.first_out_state) + " silent), " + std::to_string(pf->nkw) +
                " keywords, " + std::to_string(pf->anchors.size()) + " anchor literals, max pattern " +
                std::to_string(maxb) + " B\n" + rep;
@@ -733,59 +816,31 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
 
 bool prefilter_reference_file(const Prefilter& pf, const uint8_t* data, size_t len,
                               std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
-  const DfaTable& t = pf.scan.t;
   bool special = false;
   for (size_t p = 1; p < len; ++p) {
     if (fold_special_at(p >= 2 ? data[p - 2] : 0, data[p - 1], data[p])) { special = true; break; }
   }
-  std::vector<uint8_t> kwbit(pf.nkw, 0);
-  struct Hit { uint64_t end; uint32_t anchor; };
-  std::vector<Hit> hits;
-  uint32_t s = 0;
-  for (size_t p = 0; p < len; ++p) {
-    s = t.next[static_cast<size_t>(s) * t.nclasses + t.byte_class[data[p]]];
-    if (s >= pf.scan.first_out_state) {
-      uint32_t o = s - pf.scan.first_out_state;
-      for (uint32_t k = pf.scan.out_off[o]; k < pf.scan.out_off[o + 1]; ++k) {
-        uint32_t id = pf.scan.out_ids[k];
-        if (id < pf.nkw) kwbit[id] = 1; else hits.push_back({p, id - pf.nkw});
-      }
-    }
-  }
-  gate->assign(pf.rules.size(), 0);
-  for (size_t r = 0; r < pf.rules.size(); ++r) {
-    const RuleGpuInfo& gi = pf.rules[r];
-    uint8_t g = gi.always_gate;
-    for (uint32_t k = 0; k < gi.kw_count; ++k) g |= kwbit[pf.rule_kw[gi.kw_begin + k]];
-    (*gate)[r] = g;
-  }
-  cand->assign(pf.rules.size(), {});
-  for (const Hit& h : hits) {
-    const AnchorInfo& a = pf.anchors[h.anchor];
-    if (!(*gate)[a.rule]) continue;
-    const RuleGpuInfo& gi = pf.rules[a.rule];
-    const DfaTable& v = pf.verify[gi.verify_dfa];
-    long hi = static_cast<long>(h.end) + 1 - a.min_len - a.dmin;
-    long lo = static_cast<long>(h.end) + 1 - a.max_len - a.dmax;
-    if (lo < 0) lo = 0;
-    for (long st = lo; st <= hi; ++st) {
-      uint32_t q = 0;
-      bool emit = v.accept[0];
-      size_t p = st;
-      for (; !emit && p < len && p - st < gi.verify_limit; ++p) {
-        q = v.next[static_cast<size_t>(q) * v.nclasses + v.byte_class[data[p]]];
-        if (v.accept[q]) emit = true;
-        else if (q == v.dead) break;
-      }
-      if (!emit && q != v.dead && p < len && p - st >= gi.verify_limit) emit = true;   // gave up: conservative
-      if (emit) (*cand)[a.rule].push_back(static_cast<uint64_t>(st));
-    }
-  }
-  for (auto& c : *cand) {
-    std::sort(c.begin(), c.end());
-    c.erase(std::unique(c.begin(), c.end()), c.end());
-  }
+  two_pass(pf, pf.scan, pf.anchors, data, len, cand, gate);
   return special;
+}
+
+void plan_from_candidates(const Prefilter& pf, std::vector<std::vector<uint64_t>>* cands, FilePlan* plan) {
+  const size_t nr = pf.rules.size();
+  plan->kind.assign(nr, kPlanNoMatch);
+  plan->cands.clear();
+  for (size_t k = 0; k < nr; ++k) {
+    const RuleGpuInfo& gi = pf.rules[k];
+    if (gi.mode == 1) plan->kind[k] = kPlanFull;
+    else if (gi.mode == 0 && !(*cands)[k].empty()) {
+      plan->kind[k] = gi.gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
+      plan->cands.push_back({static_cast<uint32_t>(k), std::move((*cands)[k])});
+    }
+  }
+}
+
+void prefilter_variant_file(const Prefilter& pf, const uint8_t* data, size_t len,
+                            std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
+  two_pass(pf, pf.host_scan, pf.host_anchors, data, len, cand, gate);
 }
 
 }  // namespace tsg

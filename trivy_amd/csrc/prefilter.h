@@ -60,8 +60,10 @@ struct RuleGpuInfo {
 
 struct Prefilter {
   uint32_t nkw = 0;                    // distinct keyword patterns
-  ScanDfa scan;
+  ScanDfa scan;                        // GPU: ASCII-only, case-folded units
+  ScanDfa host_scan;                   // host: + U+0130/U+212A/U+017F alternatives (fold-special files)
   std::vector<AnchorInfo> anchors;
+  std::vector<AnchorInfo> host_anchors;   // same ids; byte lengths of the variant forms
   std::vector<RuleGpuInfo> rules;
   std::vector<uint32_t> rule_kw;       // flattened keyword ids per rule
   std::vector<DfaTable> verify;
@@ -80,6 +82,15 @@ bool build_prefilter(const Ruleset& rs, Prefilter* out, std::string* err);
 bool prefilter_reference_file(const Prefilter& pf, const uint8_t* data, size_t len,
                               std::vector<std::vector<uint64_t>>* cand_per_rule,
                               std::vector<uint8_t>* gate_per_rule);
+
+// Host path for fold-special files: the same two passes with the variant scan
+// DFA (exact for those runes).  Product code (used by Engine::scan).
+void prefilter_variant_file(const Prefilter& pf, const uint8_t* data, size_t len,
+                            std::vector<std::vector<uint64_t>>* cand_per_rule,
+                            std::vector<uint8_t>* gate_per_rule);
+
+// FilePlan from per-rule candidate lists (moves the lists into the plan).
+void plan_from_candidates(const Prefilter& pf, std::vector<std::vector<uint64_t>>* cands, FilePlan* plan);
 
 // True when bytes[i-2..i] end one of the fold-special sequences above.
 inline bool fold_special_at(uint8_t p2, uint8_t p1, uint8_t b) {
