@@ -62,6 +62,56 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
   return f;
 }
 
+constexpr uint32_t kHitBuf = 4096;             // per-block LDS hit buffer (8-byte hits)
+
+// One DFA step + outputs.  Keyword ids < 128 accumulate in two per-thread
+// 64-bit masks (flushed with atomicOr at file changes / chunk end); anchor
+// hits go to the block's LDS buffer.
+#define TSG_STEP(BYTE, Q)                                                                   \
+  do {                                                                                      \
+    s = next[s * nclasses + cls[(BYTE)]];                                                   \
+    if (s >= first_out) {                                                                   \
+      const uint32_t o_ = s - first_out;                                                    \
+      for (uint32_t j_ = out_off[o_]; j_ < out_off[o_ + 1]; ++j_) {                          \
+        const uint32_t id_ = out_ids[j_];                                                   \
+        if (id_ < nkw) {                                                                    \
+          if (id_ < 64) kw0 |= 1ull << id_;                                                 \
+          else if (id_ < 128) kw1 |= 1ull << (id_ - 64);                                    \
+          else atomicOr(kwbits + static_cast<size_t>(f) * kw_words + (id_ >> 5), 1u << (id_ & 31)); \
+        } else {                                                                            \
+          const unsigned long long h_ = ((Q) << 24) | (id_ - nkw);                          \
+          const uint32_t li_ = atomicAdd(s_hitcnt, 1u);                                     \
+          if (li_ < kHitBuf) s_hits[li_] = h_;                                              \
+          else {                                                                            \
+            const unsigned int gi_ = atomicAdd(&counters[0], 1u);                           \
+            if (gi_ < hit_cap) hits[gi_] = h_;                                              \
+          }                                                                                 \
+        }                                                                                   \
+      }                                                                                     \
+    }                                                                                       \
+  } while (0)
+
+__device__ __forceinline__ void flush_kw(uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t f,
+                                         unsigned long long& kw0, unsigned long long& kw1) {
+  uint32_t* w = kwbits + static_cast<size_t>(f) * kw_words;
+  if (kw0) {
+    if (static_cast<uint32_t>(kw0)) atomicOr(w + 0, static_cast<uint32_t>(kw0));
+    if (static_cast<uint32_t>(kw0 >> 32)) atomicOr(w + 1, static_cast<uint32_t>(kw0 >> 32));
+  }
+  if (kw1) {
+    if (static_cast<uint32_t>(kw1)) atomicOr(w + 2, static_cast<uint32_t>(kw1));
+    if (static_cast<uint32_t>(kw1 >> 32)) atomicOr(w + 3, static_cast<uint32_t>(kw1 >> 32));
+  }
+  kw0 = kw1 = 0;
+}
+
+// exact count of 0x0a bytes in a 32-bit word
+__device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
+  const uint32_t x = w ^ 0x0a0a0a0au;
+  const uint32_t y = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+  return __popc(y);
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     const uint8_t* __restrict__ data, unsigned long long total,
@@ -74,82 +124,112 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     unsigned long long* __restrict__ hits, unsigned int* __restrict__ counters, uint32_t hit_cap,
     uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // LDS layout: [hit buffer | hit count | base | (scan table | class map)]
+  unsigned long long* s_hits = reinterpret_cast<unsigned long long*>(smem);
+  uint32_t* s_hitcnt = reinterpret_cast<uint32_t*>(smem + kHitBuf * 8);
+  uint32_t* s_base = s_hitcnt + 1;
+  uint8_t* s_tab = smem + kHitBuf * 8 + 16;
   const uint16_t* next = g_next;
   const uint8_t* cls = g_cls;
   if (kLds) {
-    uint16_t* s_next = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* s_next = reinterpret_cast<uint16_t*>(s_tab);
     const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
-    uint8_t* s_cls = smem + padded;
+    uint8_t* s_cls = s_tab + padded;
     const uint4* src = reinterpret_cast<const uint4*>(g_next);
     uint4* dst = reinterpret_cast<uint4*>(s_next);
     for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = g_cls[i];
-    __syncthreads();
     next = s_next;
     cls = s_cls;
   }
-  const unsigned long long stride = static_cast<unsigned long long>(gridDim.x) * blockDim.x;
-  for (unsigned long long c = static_cast<unsigned long long>(blockIdx.x) * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
-    const unsigned long long c0 = c * kChunk;
-    const unsigned long long c1 = min(c0 + kChunk, total);
-    uint32_t f = file_of(offsets, nfiles, c0);
-    unsigned long long fstart = offsets[f], fend = offsets[f + 1];
-    uint32_t s = 0;
-    unsigned long long p = (c0 - fstart > warmup) ? c0 - warmup : fstart;
-    uint32_t p1 = 0, p2 = 0;   // previous two bytes (fold-special detection)
-    for (; p < c0; ++p) {
-      const uint32_t b = data[p];
-      s = next[s * nclasses + cls[b]];
-      p2 = p1;
-      p1 = b;
-    }
-    uint32_t nl = 0;
-    uint32_t last_kw = 0xffffffffu, last_kw_file = 0xffffffffu;
-    for (p = c0; p < c1; p += 16) {
-      const uint4 v = *reinterpret_cast<const uint4*>(data + p);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const unsigned long long q = p + k;
-        if (q >= c1) break;
-        if (q >= fend) {
-          do { ++f; fstart = fend; fend = offsets[f + 1]; } while (q >= fend);
-          s = 0;
-          p1 = p2 = 0;
-        }
-        const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-        nl += (b == 0x0au);
-        if (b & 0x80u) {
-          // U+0130 / U+017F / U+212A fold onto ASCII letters: the ASCII-only
-          // scan DFA cannot see them, so the file goes to the exact host path
-          if ((b == 0xB0u && p1 == 0xC4u) || (b == 0xBFu && p1 == 0xC5u) || (b == 0xAAu && p1 == 0x84u && p2 == 0xE2u))
-            atomicOr(&fflags[f], 1u);
-        }
+  const unsigned long long per_iter = static_cast<unsigned long long>(gridDim.x) * blockDim.x;
+  for (unsigned long long base = static_cast<unsigned long long>(blockIdx.x) * blockDim.x; base < nchunks;
+       base += per_iter) {   // block-uniform trip count
+    if (threadIdx.x == 0) *s_hitcnt = 0;
+    __syncthreads();
+    const unsigned long long c = base + threadIdx.x;
+    if (c < nchunks) {
+      const unsigned long long c0 = c * kChunk;
+      const unsigned long long c1 = min(c0 + kChunk, total);
+      uint32_t f = file_of(offsets, nfiles, c0);
+      unsigned long long fstart = offsets[f], fend = offsets[f + 1];
+      uint32_t s = 0;
+      unsigned long long kw0 = 0, kw1 = 0;
+      unsigned long long p = (c0 - fstart > warmup) ? c0 - warmup : fstart;
+      uint32_t p1 = 0, p2 = 0;   // previous two bytes (fold-special detection)
+      for (; p < c0; ++p) {
+        const uint32_t b = data[p];
+        s = next[s * nclasses + cls[b]];
         p2 = p1;
         p1 = b;
-        s = next[s * nclasses + cls[b]];
-        if (s >= first_out) {
-          const uint32_t o = s - first_out;
-          for (uint32_t j = out_off[o]; j < out_off[o + 1]; ++j) {
-            const uint32_t id = out_ids[j];
-            if (id < nkw) {
-              if (id == last_kw && f == last_kw_file) continue;
-              last_kw = id;
-              last_kw_file = f;
-              uint32_t* word = kwbits + static_cast<size_t>(f) * kw_words + (id >> 5);
-              const uint32_t bit = 1u << (id & 31);
-              if (!(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(word, bit);
-            } else {
-              const unsigned int idx = atomicAdd(&counters[0], 1u);
-              if (idx < hit_cap) hits[idx] = (q << 24) | (id - nkw);
+      }
+      // warm-up outputs are not ours: drop them
+      uint32_t nl = 0;
+      for (p = c0; p < c1; p += 16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(data + p);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        if ((v.x | v.y | v.z | v.w) & 0x80808080u) {
+          // a non-ASCII byte: check for U+0130 / U+017F / U+212A (fold onto ASCII letters)
+          unsigned long long q0 = p;
+          uint32_t a = p1, bb = p2;
+          bool hit = false;
+          for (int k = 0; k < 16 && q0 + k < c1; ++k) {
+            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+            if (q0 + k == fend) { a = bb = 0; }
+            if ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)) hit = true;
+            bb = a;
+            a = b;
+          }
+          if (hit) {
+            // attribute to every file overlapping this word (conservative)
+            for (unsigned long long q = p; q < min(p + 16, c1); ++q) atomicOr(&fflags[file_of(offsets, nfiles, q)], 1u);
+          }
+        }
+        if (p + 16 <= fend && p + 16 <= c1) {
+          nl += nl_in_word(w[0]) + nl_in_word(w[1]) + nl_in_word(w[2]) + nl_in_word(w[3]);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+            TSG_STEP(b, p + k);
+          }
+          p2 = (w[3] >> 16) & 0xffu;
+          p1 = w[3] >> 24;
+        } else {
+          for (int k = 0; k < 16; ++k) {
+            const unsigned long long q = p + k;
+            if (q >= c1) break;
+            if (q >= fend) {
+              flush_kw(kwbits, kw_words, f, kw0, kw1);
+              do { ++f; fstart = fend; fend = offsets[f + 1]; } while (q >= fend);
+              s = 0;
+              p1 = p2 = 0;
             }
+            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+            nl += (b == 0x0au);
+            TSG_STEP(b, q);
+            p2 = p1;
+            p1 = b;
           }
         }
       }
+      flush_kw(kwbits, kw_words, f, kw0, kw1);
+      nl_count[c] = nl;
     }
-    nl_count[c] = nl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t n = min(*s_hitcnt, kHitBuf);
+      *s_base = n ? atomicAdd(&counters[0], n) : 0u;
+    }
+    __syncthreads();
+    const uint32_t n = min(*s_hitcnt, kHitBuf);
+    const uint32_t b0 = *s_base;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      if (b0 + i < hit_cap) hits[b0 + i] = s_hits[i];
+    }
+    __syncthreads();
   }
 }
+#undef TSG_STEP
 
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
@@ -294,7 +374,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   std::vector<uint16_t> sn = pf.scan.t.next;
   m.table_words16 = static_cast<uint32_t>(sn.size());
   sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
-  m.table_in_lds = static_cast<size_t>(m.table_words16) * 2 <= kLdsTableMax;
+  m.table_in_lds = static_cast<size_t>(m.table_words16) * 2 + kHitBuf * 8 + 512 <= kLdsTableMax;
   std::vector<uint8_t> cls(pf.scan.t.byte_class, pf.scan.t.byte_class + 256);
   std::vector<AnchorDev> an;
   for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
@@ -378,9 +458,16 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
     HIP_OK(hipMemsetAsync(m.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), m.stream));
     HIP_OK(hipMemsetAsync(m.d_cnt, 0, 64, m.stream));
     uint64_t want_blocks = (nchunks + kBlock - 1) / kBlock;
-    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * 8ull)));
+    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * 2ull)));
     const uint32_t warm = pf.scan.max_pattern_bytes > 0 ? pf.scan.max_pattern_bytes - 1 : 0;
-    const size_t lds = m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 : 0;
+    const size_t lds = kHitBuf * 8 + 16 + (m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 : 0);
+    if (m.table_in_lds) {
+      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tsg_k1_scan<true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    } else {
+      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tsg_k1_scan<false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    }
     st->k1_blocks = blocks;
     st->k1_threads = kBlock;
     st->table_in_lds = m.table_in_lds;
@@ -393,7 +480,7 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
                            pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
                            static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
       } else {
-        hipLaunchKernelGGL(tsg_k1_scan<false>, dim3(blocks), dim3(kBlock), 0, m.stream,
+        hipLaunchKernelGGL(tsg_k1_scan<false>, dim3(blocks), dim3(kBlock), lds, m.stream,
                            d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
                            pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state, m.out_off, m.out_ids,
                            pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
@@ -504,6 +591,9 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     std::vector<uint32_t> pos(per_file.begin(), per_file.end() - 1);
     for (const CandDev& c : m.h_cands) sorted[pos[c.file]++] = c;
   }
+  // global newline prefix over K1's per-chunk counts (findLocation line numbers)
+  std::vector<uint64_t> nl_prefix(m.h_nl.size() + 1, 0);
+  for (size_t c = 0; c < m.h_nl.size(); ++c) nl_prefix[c + 1] = nl_prefix[c] + m.h_nl[c];
   bool any_full = false;
   for (const auto& gi : pf_.rules) if (gi.mode == 1) any_full = true;
   results->assign(in.nfiles, Secret());
@@ -565,7 +655,12 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         plan.kind[r] = pf_.rules[r].gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
         plan.cands.push_back(std::move(rc));
       }
-      Secret s = scan_file(rs, path, content, len, binary, &plan);
+      NlSource nls;
+      nls.prefix = nl_prefix.data();
+      nls.data = in.h_data;
+      nls.file_off = in.offsets[f];
+      nls.chunk = kChunk;
+      Secret s = scan_file(rs, path, content, len, binary, &plan, &nls);
       nfind.fetch_add(s.findings.size());
       (*results)[f] = std::move(s);
     }

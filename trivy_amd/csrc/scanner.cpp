@@ -549,56 +549,169 @@ class GoSort {
   }
 };
 
-// scanner.go:495-558 on the censored buffer, with a newline index built once.
-struct LineIndex {
-  const uint8_t* c;
-  size_t n;
-  std::vector<size_t> nl;    // positions of '\n'
-  LineIndex(const uint8_t* cc, size_t nn) : c(cc), n(nn) {
-    const uint8_t* p = c;
-    const uint8_t* end = c + n;
-    while (p < end) {
-      const void* q = memchr(p, '\n', end - p);
-      if (!q) break;
-      nl.push_back(static_cast<const uint8_t*>(q) - c);
-      p = static_cast<const uint8_t*>(q) + 1;
+// The censored buffer of scanner.go:431-435 (content with every matched span
+// overwritten by '*'), represented virtually: original bytes + merged spans.
+class CensoredView {
+ public:
+  CensoredView(const uint8_t* c, size_t n, std::vector<Loc> spans, const NlSource* nl) : c_(c), n_(n) {
+    std::sort(spans.begin(), spans.end(), [](const Loc& a, const Loc& b) { return a.start < b.start; });
+    for (const Loc& l : spans) {
+      if (l.end <= l.start) continue;
+      if (!iv_.empty() && l.start <= iv_.back().end) iv_.back().end = std::max(iv_.back().end, l.end);
+      else iv_.push_back(l);
+    }
+    if (nl && nl->prefix) {
+      nl_ = *nl;
+    } else {
+      // local prefix over this file (reference / host-only paths)
+      const uint32_t ch = 4096;
+      local_.assign(n / ch + 2, 0);
+      uint64_t acc = 0;
+      for (size_t k = 0; k * ch < n; ++k) {
+        local_[k] = acc;
+        const size_t e = std::min(n, (k + 1) * ch);
+        for (size_t x = k * ch; x < e; ++x) acc += c_[x] == '\n';
+      }
+      local_[n / ch + 1] = acc;
+      if (n % ch == 0) local_[n / ch] = acc;
+      nl_.prefix = local_.data();
+      nl_.data = c_;
+      nl_.file_off = 0;
+      nl_.chunk = ch;
     }
   }
-  size_t count_before(size_t pos) const { return std::lower_bound(nl.begin(), nl.end(), pos) - nl.begin(); }
-  // bytes of line k (0-based) of bytes.Split(content, "\n")
-  void line(size_t k, size_t* b, size_t* e) const {
-    *b = k == 0 ? 0 : nl[k - 1] + 1;
-    *e = k < nl.size() ? nl[k] : n;
+  uint8_t at(size_t i) const { return censored(static_cast<long>(i)) ? '*' : c_[i]; }
+  bool censored(long i) const {
+    auto it = std::upper_bound(iv_.begin(), iv_.end(), i, [](long v, const Loc& l) { return v < l.start; });
+    if (it == iv_.begin()) return false;
+    --it;
+    return i < it->end;
+  }
+  // '\n' count of the censored buffer in [a, b)
+  uint64_t count_nl(size_t a, size_t b) const {
+    if (b <= a) return 0;
+    uint64_t n = orig_nl(a, b);
+    for (const Loc& l : iv_) {
+      size_t x = std::max<size_t>(a, l.start), y = std::min<size_t>(b, l.end);
+      if (x < y) n -= orig_nl(x, y);
+    }
+    return n;
+  }
+  // last censored-buffer '\n' position < pos, or -1
+  long prev_nl(size_t pos) const {
+    long i = static_cast<long>(pos) - 1;
+    while (i >= 0) {
+      const void* q = memrchr(c_, '\n', static_cast<size_t>(i) + 1);
+      if (!q) return -1;
+      long k = static_cast<const uint8_t*>(q) - c_;
+      if (!censored(k)) return k;
+      auto it = std::upper_bound(iv_.begin(), iv_.end(), k, [](long v, const Loc& l) { return v < l.start; });
+      --it;
+      i = it->start - 1;
+    }
+    return -1;
+  }
+  // first censored-buffer '\n' position >= pos, or n
+  size_t next_nl(size_t pos) const {
+    size_t i = pos;
+    while (i < n_) {
+      const void* q = memchr(c_ + i, '\n', n_ - i);
+      if (!q) return n_;
+      size_t k = static_cast<const uint8_t*>(q) - c_;
+      if (!censored(static_cast<long>(k))) return k;
+      auto it = std::upper_bound(iv_.begin(), iv_.end(), static_cast<long>(k), [](long v, const Loc& l) { return v < l.start; });
+      --it;
+      i = static_cast<size_t>(it->end);
+    }
+    return n_;
+  }
+  std::string str(size_t a, size_t b) const {
+    std::string s(reinterpret_cast<const char*>(c_) + a, b - a);
+    for (const Loc& l : iv_) {
+      size_t x = std::max<size_t>(a, l.start), y = std::min<size_t>(b, l.end);
+      for (size_t k = x; k < y; ++k) s[k - a] = '*';
+    }
+    return s;
+  }
+  size_t size() const { return n_; }
+
+ private:
+  const uint8_t* c_;
+  size_t n_;
+  std::vector<Loc> iv_;
+  NlSource nl_;
+  std::vector<uint64_t> local_;
+
+  uint64_t prefix_at(uint64_t g) const {   // '\n' in data[0, g) (global coordinates)
+    const uint64_t k = g / nl_.chunk;
+    const uint64_t base = k * nl_.chunk;
+    uint64_t n = nl_.prefix[k];
+    const uint8_t* d = nl_.data;
+    for (uint64_t x = base; x < g; ++x) n += d[x] == '\n';
+    return n;
+  }
+  uint64_t orig_nl(size_t a, size_t b) const {
+    if (b - a <= 2 * static_cast<size_t>(nl_.chunk)) {
+      uint64_t n = 0;
+      for (size_t x = a; x < b; ++x) n += c_[x] == '\n';
+      return n;
+    }
+    return prefix_at(nl_.file_off + b) - prefix_at(nl_.file_off + a);
   }
 };
 
-Finding to_finding(const Rule& rule, Loc loc, const uint8_t* c, size_t n, const LineIndex& li) {
+// scanner.go:495-558 on the (virtual) censored buffer.
+Finding to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlines) {
   Finding f;                                          // scanner.go:475-488
   f.rule_id = rule.id;
   f.category = rule.category;
   f.severity = rule.severity.empty() ? "UNKNOWN" : rule.severity;
   f.title = rule.title;
+  const size_t n = cv.size();
   const size_t start = static_cast<size_t>(loc.start), end = static_cast<size_t>(loc.end);
-  const size_t start_line = li.count_before(start);
-  size_t line_start, line_end;
-  li.line(start_line, &line_start, &line_end);        // LastIndex / Index of '\n' around start
+  const size_t start_line = cv.count_nl(0, start);
+  const long pn = cv.prev_nl(start);
+  const size_t line0_b = pn < 0 ? 0 : static_cast<size_t>(pn) + 1;   // LastIndex('\n') + 1
+  const size_t line0_e = cv.next_nl(start);                             // Index('\n') from start
+  size_t line_start = line0_b, line_end = line0_e;
   if (line_end - line_start > 100) {
     line_start = (static_cast<long>(start) - static_cast<long>(line_start) - 30 < 0) ? line_start : start - 30;
     line_end = (end + 20 > line_end) ? line_end : end + 20;
   }
-  std::string match_line(reinterpret_cast<const char*>(c) + line_start, line_end - line_start);
-  const size_t end_line = start_line + (li.count_before(end) - li.count_before(start));
-  const size_t nlines = li.nl.size() + 1;
+  std::string match_line = cv.str(line_start, line_end);
+  const size_t end_line = start_line + cv.count_nl(start, end);
   const size_t code_start = start_line >= 2 ? start_line - 2 : 0;
-  const size_t code_end = std::min(end_line + 2, nlines);
+  const size_t code_end = std::min<size_t>(end_line + 2, nlines);
+  // bounds of lines code_start .. code_end-1 (bytes.Split of the censored buffer)
+  std::vector<std::pair<size_t, size_t>> lines;
+  {
+    std::vector<std::pair<size_t, size_t>> before;
+    size_t b = line0_b;
+    for (size_t k = start_line; k > code_start; --k) {   // walk back
+      const size_t e = b - 1;                            // the '\n' ending line k-1
+      const long q = cv.prev_nl(e);
+      const size_t bb = q < 0 ? 0 : static_cast<size_t>(q) + 1;
+      before.push_back({bb, e});
+      b = bb;
+    }
+    for (auto it = before.rbegin(); it != before.rend(); ++it) lines.push_back(*it);
+    size_t e = line0_e;
+    lines.push_back({line0_b, line0_e});
+    for (size_t k = start_line + 1; k < code_end; ++k) {
+      const size_t bb = e + 1;
+      e = bb <= n ? cv.next_nl(bb) : n;
+      lines.push_back({bb, e});
+    }
+  }
   bool found_first = false;
-  for (size_t k = code_start; k < code_end; ++k) {
-    size_t b, e;
-    li.line(k, &b, &e);
+  for (size_t idx = 0; idx < lines.size(); ++idx) {
+    const size_t k = code_start + idx;
+    if (k >= code_end) break;
+    const size_t b = lines[idx].first, e = lines[idx].second;
     const bool in_cause = k >= start_line && k <= end_line;
     std::string s;
-    if (e - b > 100) s = in_cause ? match_line : std::string(reinterpret_cast<const char*>(c) + b, 100);
-    else s.assign(reinterpret_cast<const char*>(c) + b, e - b);
+    if (e - b > 100) s = in_cause ? match_line : cv.str(b, b + 100);
+    else s = cv.str(b, e);
     Line ln;
     ln.number = static_cast<int>(k + 1);
     ln.content = s;
@@ -629,7 +742,7 @@ bool keywords_match(const Rule& r, const std::string& lower) {   // scanner.go:1
 }  // namespace
 
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
-                 bool binary, const FilePlan* plan) {
+                 bool binary, const FilePlan* plan, const NlSource* nl) {
   Secret out;
   if (allow_path(rs.allow_rules, path)) { out.file_path = path; return out; }   // scanner.go:381-386
   std::string lower;
@@ -641,7 +754,6 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
   Blocks gblocks(content, len, rs.exclude_block);
   struct M { const Rule* rule; Loc loc; };
   std::vector<M> matched;
-  std::vector<uint8_t> censored;
   size_t cand_i = 0;
   std::vector<Loc> locs;
   for (size_t ri = 0; ri < rs.rules.size(); ++ri) {
@@ -667,16 +779,16 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
     for (const Loc& l : locs) {
       if (l.start < 0) continue;                      // reference panics here (error flagged)
       if (gblocks.match(l) || lblocks.match(l)) continue;
-      matched.push_back({&rule, l});
-      if (censored.empty() && len > 0) censored.assign(content, content + len);
-      if (censored.size() < len) censored.resize(len);
-      for (long k = l.start; k < l.end; ++k) censored[k] = '*';
+      matched.push_back({&rule, l});                  // censorLocation: applied virtually below
     }
   }
   if (matched.empty()) return out;                    // types.Secret{}
-  LineIndex li(censored.data(), len);
+  std::vector<Loc> spans;
+  for (const auto& m : matched) spans.push_back(m.loc);
+  CensoredView cv(content, len, std::move(spans), nl);
+  const uint64_t nlines = cv.count_nl(0, len) + 1;
   for (const auto& m : matched) {
-    Finding f = to_finding(*m.rule, m.loc, censored.data(), len, li);
+    Finding f = to_finding(*m.rule, m.loc, cv, nlines);
     if (binary) {
       f.match = "Binary file " + go_quote(path) + " matches a rule " + go_quote(m.rule->title);
       f.code.clear();

@@ -85,6 +85,15 @@ struct FilePlan {
   std::vector<RuleCandidates> cands;     // sorted by rule
 };
 
+// Newline counts for findLocation without rescanning a file: global per-chunk
+// prefix sums (from K1's per-chunk '\n' counts) over the packed batch.
+struct NlSource {
+  const uint64_t* prefix = nullptr;   // prefix[c] = '\n' count in data[0, c*chunk)
+  const uint8_t* data = nullptr;      // packed batch (host)
+  uint64_t file_off = 0;              // global offset of this file in data
+  uint32_t chunk = 0;
+};
+
 // bytes.ToLower (ASCII fast path; Map(unicode.ToLower) with invalid bytes -> U+FFFD)
 std::string go_bytes_to_lower(const uint8_t* s, size_t n);
 std::string go_str_to_lower(const std::string& s);
@@ -93,7 +102,7 @@ std::string go_quote(const std::string& s);
 
 // Scanner.Scan (scanner.go:377-463).  plan == nullptr: reference algorithm.
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
-                 bool binary, const FilePlan* plan);
+                 bool binary, const FilePlan* plan, const NlSource* nl = nullptr);
 
 // Exact Go FindAll(Submatch)Index restricted to candidate start offsets.
 // `starts` must be a sorted superset of every position where an anchored
