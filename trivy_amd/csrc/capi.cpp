@@ -337,7 +337,11 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   auto* r = new tsg_result();
   r->files.resize(nfiles);
   r->cands.resize(nfiles);
-  const size_t nr = rs->rs->rules.size();
+  // per-chunk newline counts over the packed batch, as K1 produces them
+  const uint32_t ch = 2048;
+  const uint64_t total = nfiles ? offsets[nfiles] : 0;
+  std::vector<uint32_t> chunk_nl(total / ch + 2, 0);
+  for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += data[x] == '\n';
   for (uint32_t f = 0; f < nfiles; ++f) {
     const uint8_t* c = data + offsets[f];
     const size_t len = offsets[f + 1] - offsets[f];
@@ -347,7 +351,12 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
     std::vector<std::vector<uint64_t>> tmp = r->cands[f];
     FilePlan plan;
     plan_from_candidates(pf, &tmp, &plan);
-    r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, &plan);
+    NlSource nls;
+    nls.chunk_nl = chunk_nl.data();
+    nls.data = data;
+    nls.file_off = offsets[f];
+    nls.chunk = ch;
+    r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, &plan, &nls);
   }
   *out = r;
   return TSG_OK;

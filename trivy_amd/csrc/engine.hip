@@ -67,28 +67,31 @@ constexpr uint32_t kHitBuf = 4096;             // per-block LDS hit buffer (8-by
 // One DFA step + outputs.  Keyword ids < 128 accumulate in two per-thread
 // 64-bit masks (flushed with atomicOr at file changes / chunk end); anchor
 // hits go to the block's LDS buffer.
-#define TSG_STEP(BYTE, Q)                                                                   \
+#define TSG_OUT(S, Q)                                                                       \
   do {                                                                                      \
-    s = next[s * nclasses + cls[(BYTE)]];                                                   \
-    if (s >= first_out) {                                                                   \
-      const uint32_t o_ = s - first_out;                                                    \
-      for (uint32_t j_ = out_off[o_]; j_ < out_off[o_ + 1]; ++j_) {                          \
-        const uint32_t id_ = out_ids[j_];                                                   \
-        if (id_ < nkw) {                                                                    \
-          if (id_ < 64) kw0 |= 1ull << id_;                                                 \
-          else if (id_ < 128) kw1 |= 1ull << (id_ - 64);                                    \
-          else atomicOr(kwbits + static_cast<size_t>(f) * kw_words + (id_ >> 5), 1u << (id_ & 31)); \
-        } else {                                                                            \
-          const unsigned long long h_ = ((Q) << 24) | (id_ - nkw);                          \
-          const uint32_t li_ = atomicAdd(s_hitcnt, 1u);                                     \
-          if (li_ < kHitBuf) s_hits[li_] = h_;                                              \
-          else {                                                                            \
-            const unsigned int gi_ = atomicAdd(&counters[0], 1u);                           \
-            if (gi_ < hit_cap) hits[gi_] = h_;                                              \
-          }                                                                                 \
+    const uint32_t o_ = (S) - first_out;                                                    \
+    for (uint32_t j_ = out_off[o_]; j_ < out_off[o_ + 1]; ++j_) {                            \
+      const uint32_t id_ = out_ids[j_];                                                     \
+      if (id_ < nkw) {                                                                      \
+        if (id_ < 64) kw0 |= 1ull << id_;                                                   \
+        else if (id_ < 128) kw1 |= 1ull << (id_ - 64);                                      \
+        else atomicOr(kwbits + static_cast<size_t>(f) * kw_words + (id_ >> 5), 1u << (id_ & 31)); \
+      } else {                                                                              \
+        const unsigned long long h_ = ((Q) << 24) | (id_ - nkw);                            \
+        const uint32_t li_ = atomicAdd(s_hitcnt, 1u);                                       \
+        if (li_ < kHitBuf) s_hits[li_] = h_;                                                \
+        else {                                                                              \
+          const unsigned int gi_ = atomicAdd(&counters[0], 1u);                             \
+          if (gi_ < hit_cap) hits[gi_] = h_;                                                \
         }                                                                                   \
       }                                                                                     \
     }                                                                                       \
+  } while (0)
+
+#define TSG_STEP(BYTE, Q)                                                                   \
+  do {                                                                                      \
+    s = next[s * nclasses + cls[(BYTE)]];                                                   \
+    if (s >= first_out) TSG_OUT(s, Q);                                                      \
   } while (0)
 
 __device__ __forceinline__ void flush_kw(uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t f,
@@ -187,10 +190,25 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
         }
         if (p + 16 <= fend && p + 16 <= c1) {
           nl += nl_in_word(w[0]) + nl_in_word(w[1]) + nl_in_word(w[2]) + nl_in_word(w[3]);
+          // the 16 class lookups do not depend on the DFA state: issue them
+          // first, then walk the dependent transition chain, and look at
+          // outputs only if some state in this word has one
+          uint32_t cl[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) cl[k] = cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
+          uint32_t st[16];
+          uint32_t mx = 0;
 #pragma unroll
           for (int k = 0; k < 16; ++k) {
-            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-            TSG_STEP(b, p + k);
+            s = next[s * nclasses + cl[k]];
+            st[k] = s;
+            mx = max(mx, s);
+          }
+          if (mx >= first_out) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+              if (st[k] >= first_out) TSG_OUT(st[k], p + k);
+            }
           }
           p2 = (w[3] >> 16) & 0xffu;
           p1 = w[3] >> 24;
@@ -230,6 +248,7 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
   }
 }
 #undef TSG_STEP
+#undef TSG_OUT
 
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
@@ -591,14 +610,16 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     std::vector<uint32_t> pos(per_file.begin(), per_file.end() - 1);
     for (const CandDev& c : m.h_cands) sorted[pos[c.file]++] = c;
   }
-  // global newline prefix over K1's per-chunk counts (findLocation line numbers)
-  std::vector<uint64_t> nl_prefix(m.h_nl.size() + 1, 0);
-  for (size_t c = 0; c < m.h_nl.size(); ++c) nl_prefix[c + 1] = nl_prefix[c] + m.h_nl[c];
   bool any_full = false;
   for (const auto& gi : pf_.rules) if (gi.mode == 1) any_full = true;
   results->assign(in.nfiles, Secret());
-  std::vector<uint32_t> work;
-  for (uint32_t f = 0; f < in.nfiles; ++f) work.push_back(f);
+  // largest files first (LPT): the per-file confirm cost grows with size
+  std::vector<uint32_t> work(in.nfiles);
+  for (uint32_t f = 0; f < in.nfiles; ++f) work[f] = f;
+  std::sort(work.begin(), work.end(), [&](uint32_t a, uint32_t b) {
+    const uint64_t sa = in.offsets[a + 1] - in.offsets[a], sb = in.offsets[b + 1] - in.offsets[b];
+    return sa != sb ? sa > sb : a < b;
+  });
   std::atomic<uint32_t> next{0};
   std::atomic<uint64_t> nfind{0}, nconf{0};
   auto worker = [&]() {
@@ -656,7 +677,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         plan.cands.push_back(std::move(rc));
       }
       NlSource nls;
-      nls.prefix = nl_prefix.data();
+      nls.chunk_nl = m.h_nl.data();
       nls.data = in.h_data;
       nls.file_off = in.offsets[f];
       nls.chunk = kChunk;

@@ -560,24 +560,29 @@ class CensoredView {
       if (!iv_.empty() && l.start <= iv_.back().end) iv_.back().end = std::max(iv_.back().end, l.end);
       else iv_.push_back(l);
     }
-    if (nl && nl->prefix) {
-      nl_ = *nl;
+    if (nl && nl->chunk_nl) {
+      // local prefix over the batch chunks this file touches
+      ch_ = nl->chunk;
+      data_ = nl->data;
+      off_ = nl->file_off;
+      first_ = off_ / ch_;
+      const uint64_t last = (off_ + n) / ch_;
+      local_.assign(last - first_ + 2, 0);
+      for (uint64_t k = first_; k <= last; ++k) local_[k - first_ + 1] = local_[k - first_] + nl->chunk_nl[k];
     } else {
       // local prefix over this file (reference / host-only paths)
-      const uint32_t ch = 4096;
-      local_.assign(n / ch + 2, 0);
-      uint64_t acc = 0;
-      for (size_t k = 0; k * ch < n; ++k) {
-        local_[k] = acc;
-        const size_t e = std::min(n, (k + 1) * ch);
-        for (size_t x = k * ch; x < e; ++x) acc += c_[x] == '\n';
+      ch_ = 4096;
+      data_ = c_;
+      off_ = 0;
+      first_ = 0;
+      const size_t nch = n / ch_ + 1;
+      local_.assign(nch + 1, 0);
+      for (size_t k = 0; k < nch; ++k) {
+        const size_t b = k * ch_, e = std::min<size_t>(n, b + ch_);
+        uint64_t cnt = 0;
+        for (size_t x = b; x < e; ++x) cnt += c_[x] == '\n';
+        local_[k + 1] = local_[k] + cnt;
       }
-      local_[n / ch + 1] = acc;
-      if (n % ch == 0) local_[n / ch] = acc;
-      nl_.prefix = local_.data();
-      nl_.data = c_;
-      nl_.file_off = 0;
-      nl_.chunk = ch;
     }
   }
   uint8_t at(size_t i) const { return censored(static_cast<long>(i)) ? '*' : c_[i]; }
@@ -639,24 +644,24 @@ class CensoredView {
   const uint8_t* c_;
   size_t n_;
   std::vector<Loc> iv_;
-  NlSource nl_;
-  std::vector<uint64_t> local_;
+  std::vector<uint64_t> local_;     // local_[k] = '\n' in data_[first_*ch_, (first_+k)*ch_)
+  const uint8_t* data_ = nullptr;
+  uint64_t off_ = 0, first_ = 0;
+  uint32_t ch_ = 4096;
 
-  uint64_t prefix_at(uint64_t g) const {   // '\n' in data[0, g) (global coordinates)
-    const uint64_t k = g / nl_.chunk;
-    const uint64_t base = k * nl_.chunk;
-    uint64_t n = nl_.prefix[k];
-    const uint8_t* d = nl_.data;
-    for (uint64_t x = base; x < g; ++x) n += d[x] == '\n';
+  uint64_t prefix_at(uint64_t g) const {   // '\n' in data_[first_*ch_, g)
+    const uint64_t k = g / ch_;
+    uint64_t n = local_[k - first_];
+    for (uint64_t x = k * ch_; x < g; ++x) n += data_[x] == '\n';
     return n;
   }
   uint64_t orig_nl(size_t a, size_t b) const {
-    if (b - a <= 2 * static_cast<size_t>(nl_.chunk)) {
+    if (b - a <= 2 * static_cast<size_t>(ch_)) {
       uint64_t n = 0;
       for (size_t x = a; x < b; ++x) n += c_[x] == '\n';
       return n;
     }
-    return prefix_at(nl_.file_off + b) - prefix_at(nl_.file_off + a);
+    return prefix_at(off_ + b) - prefix_at(off_ + a);
   }
 };
 

@@ -85,10 +85,10 @@ struct FilePlan {
   std::vector<RuleCandidates> cands;     // sorted by rule
 };
 
-// Newline counts for findLocation without rescanning a file: global per-chunk
-// prefix sums (from K1's per-chunk '\n' counts) over the packed batch.
+// Newline counts for findLocation without rescanning a file: K1's per-chunk
+// '\n' counts over the packed batch (chunk c covers data[c*chunk, (c+1)*chunk)).
 struct NlSource {
-  const uint64_t* prefix = nullptr;   // prefix[c] = '\n' count in data[0, c*chunk)
+  const uint32_t* chunk_nl = nullptr;
   const uint8_t* data = nullptr;      // packed batch (host)
   uint64_t file_off = 0;              // global offset of this file in data
   uint32_t chunk = 0;
