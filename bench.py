@@ -173,6 +173,8 @@ def main():
     k2_ms = float(np.mean([s["k2_ms"] for s in stats]))
     host_ms = float(np.mean([s["host_ms"] for s in stats]))
     d2h_ms = float(np.mean([s["d2h_ms"] for s in stats]))
+    gpu_wall_ms = float(np.mean([s["gpu_wall_ms"] for s in stats]))
+    eng_total_ms = float(np.mean([s["total_ms"] for s in stats]))
     k1_gbps = corpus.nbytes / (k1_ms / 1e3) / 1e9
     gpu_results = _lib.result_json(last)
     L.tsg_result_free(last)
@@ -214,7 +216,8 @@ def main():
             "bytes_per_launch": corpus.nbytes,
             "avg_launch_ms": round(k1_ms, 4),
         },
-        "breakdown_ms": {"k1": round(k1_ms, 3), "k2": round(k2_ms, 3), "d2h": round(d2h_ms, 3),
+        "breakdown_ms": {"gpu_phase_wall": round(gpu_wall_ms, 3), "engine_total": round(eng_total_ms, 3),
+                         "k1": round(k1_ms, 3), "k2": round(k2_ms, 3), "d2h": round(d2h_ms, 3),
                          "host_confirm": round(host_ms, 3), "hits": stats[-1]["hits"],
                          "candidates": stats[-1]["candidates"], "confirm_files": stats[-1]["confirm_files"],
                          "findings": findings, "rules_with_findings": len(rules_hit)},

@@ -82,6 +82,7 @@ typedef struct tsg_stats {
   uint64_t bytes, files, hits, candidates, confirm_files, findings;
   uint32_t k1_blocks, k1_threads, chunk_bytes;
   int32_t table_in_lds;
+  double gpu_wall_ms;   /* wall time of the GPU phase incl. launches, syncs and copies */
 } tsg_stats;
 
 const char* tsg_last_error(void);

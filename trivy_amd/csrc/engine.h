@@ -13,6 +13,7 @@ namespace tsg {
 
 struct ScanStats {
   double k1_ms = 0, k2_ms = 0, h2d_ms = 0, d2h_ms = 0, host_ms = 0, total_ms = 0;
+  double gpu_wall_ms = 0;               // run_gpu() wall time (launches + syncs + copies)
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, confirm_files = 0, findings = 0;
   uint32_t k1_blocks = 0, k1_threads = 0, chunk_bytes = 0;
   int table_in_lds = 0;

@@ -62,38 +62,12 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
   return f;
 }
 
-constexpr uint32_t kHitBuf = 4096;             // per-block LDS hit buffer (8-byte hits)
+constexpr uint32_t kHitBuf = 4096;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));             // per-block LDS hit buffer (8-byte hits)
 
 // One DFA step + outputs.  Keyword ids < 128 accumulate in two per-thread
 // 64-bit masks (flushed with atomicOr at file changes / chunk end); anchor
 // hits go to the block's LDS buffer.
-#define TSG_OUT(S, Q)                                                                       \
-  do {                                                                                      \
-    const uint32_t o_ = (S) - first_out;                                                    \
-    for (uint32_t j_ = out_off[o_]; j_ < out_off[o_ + 1]; ++j_) {                            \
-      const uint32_t id_ = out_ids[j_];                                                     \
-      if (id_ < nkw) {                                                                      \
-        if (id_ < 64) kw0 |= 1ull << id_;                                                   \
-        else if (id_ < 128) kw1 |= 1ull << (id_ - 64);                                      \
-        else atomicOr(kwbits + static_cast<size_t>(f) * kw_words + (id_ >> 5), 1u << (id_ & 31)); \
-      } else {                                                                              \
-        const unsigned long long h_ = ((Q) << 24) | (id_ - nkw);                            \
-        const uint32_t li_ = atomicAdd(s_hitcnt, 1u);                                       \
-        if (li_ < kHitBuf) s_hits[li_] = h_;                                                \
-        else {                                                                              \
-          const unsigned int gi_ = atomicAdd(&counters[0], 1u);                             \
-          if (gi_ < hit_cap) hits[gi_] = h_;                                                \
-        }                                                                                   \
-      }                                                                                     \
-    }                                                                                       \
-  } while (0)
-
-#define TSG_STEP(BYTE, Q)                                                                   \
-  do {                                                                                      \
-    s = next[s * nclasses + cls[(BYTE)]];                                                   \
-    if (s >= first_out) TSG_OUT(s, Q);                                                      \
-  } while (0)
-
 __device__ __forceinline__ void flush_kw(uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t f,
                                          unsigned long long& kw0, unsigned long long& kw1) {
   uint32_t* w = kwbits + static_cast<size_t>(f) * kw_words;
@@ -115,14 +89,136 @@ __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
   return __popc(y);
 }
 
+// Per-stream state of K1 (a thread walks kStreams independent byte ranges so
+// the LDS latency of one DFA chain hides behind the others).
+struct K1Stream {
+  unsigned long long p, end, fend;
+  uint32_t f, s, p1, p2, nl;
+  unsigned long long kw0, kw1;
+};
+
+// Output metadata of a state with outputs, in LDS: its keyword ids < 128 as
+// two masks, and a list of the other output ids (anchors, keywords >= 128).
+struct OutMeta { unsigned long long kw0, kw1; uint32_t list_begin, list_count; };
+
+template <bool kLds>
+struct K1Ctx {
+  const uint8_t* __restrict__ data;
+  const uint64_t* __restrict__ offsets;
+  uint32_t nfiles;
+  const uint16_t* next;   // pre-multiplied: next[s + c] is the next state's row offset
+  const uint8_t* cls;
+  uint32_t first_out;     // row offset of the first state with outputs
+  uint32_t nclasses;      // row slot `nclasses` holds the output-state index
+  const OutMeta* meta;
+  const uint32_t* list;
+  uint32_t nkw;
+  uint32_t* __restrict__ kwbits;
+  uint32_t kw_words;
+  unsigned long long* __restrict__ hits;
+  unsigned int* __restrict__ counters;
+  uint32_t hit_cap;
+  unsigned long long* s_hits;
+  uint32_t* s_hitcnt;
+  uint32_t* __restrict__ fflags;
+};
+
+// Output metadata of a state with outputs, in LDS: its keyword ids < 128 as
+// two masks, and a list of the other output ids (anchors, keywords >= 128).
+
+template <bool kLds>
+__device__ __forceinline__ void k1_out(const K1Ctx<kLds>& x, K1Stream& t, uint32_t st, unsigned long long q) {
+  const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
+  const OutMeta m = x.meta[o];
+  t.kw0 |= m.kw0;
+  t.kw1 |= m.kw1;
+  for (uint32_t j = 0; j < m.list_count; ++j) {
+    const uint32_t id = x.list[m.list_begin + j];
+    if (id < x.nkw) {
+      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
+    } else {
+      const unsigned long long h = (q << 24) | (id - x.nkw);
+      const uint32_t li = atomicAdd(x.s_hitcnt, 1u);
+      if (li < kHitBuf) x.s_hits[li] = h;
+      else {
+        const unsigned int gi = atomicAdd(&x.counters[0], 1u);
+        if (gi < x.hit_cap) x.hits[gi] = h;
+      }
+    }
+  }
+}
+
+// U+0130 / U+017F / U+212A fold onto ASCII letters: flag every file that
+// overlaps a 16-byte word ending such a sequence (host re-scans it exactly).
+template <bool kLds>
+__device__ __forceinline__ void k1_special(const K1Ctx<kLds>& x, const K1Stream& t, const uint32_t w[4]) {
+  uint32_t a = t.p1, bb = t.p2;
+  bool hit = false;
+  for (int k = 0; k < 16 && t.p + k < t.end; ++k) {
+    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    if (t.p + k == t.fend) { a = bb = 0; }
+    if ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)) hit = true;
+    bb = a;
+    a = b;
+  }
+  if (hit) {
+    for (unsigned long long q = t.p; q < min(t.p + 16, t.end); ++q) atomicOr(&x.fflags[file_of(x.offsets, x.nfiles, q)], 1u);
+  }
+}
+
+// One 16-byte word of one stream with file-boundary checks.
+template <bool kLds>
+__device__ __forceinline__ void k1_word_slow(const K1Ctx<kLds>& x, K1Stream& t, const uint32_t w[4]) {
+  for (int k = 0; k < 16; ++k) {
+    const unsigned long long q = t.p + k;
+    if (q >= t.end) break;
+    if (q >= t.fend) {
+      flush_kw(x.kwbits, x.kw_words, t.f, t.kw0, t.kw1);
+      do { ++t.f; t.fend = x.offsets[t.f + 1]; } while (q >= t.fend);
+      t.s = 0;
+      t.p1 = t.p2 = 0;
+    }
+    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    t.nl += (b == 0x0au);
+    t.s = x.next[t.s + x.cls[b]];
+    if (t.s >= x.first_out) k1_out(x, t, t.s, q);
+    t.p2 = t.p1;
+    t.p1 = b;
+  }
+  t.p += 16;
+}
+
+template <bool kLds>
+__device__ __forceinline__ void k1_init(const K1Ctx<kLds>& x, K1Stream& t, unsigned long long b, unsigned long long e,
+                                        uint32_t warmup) {
+  t.p = b;
+  t.end = e;
+  t.s = 0;
+  t.p1 = t.p2 = 0;
+  t.nl = 0;
+  t.kw0 = t.kw1 = 0;
+  if (b >= e) { t.f = 0; t.fend = 0; return; }
+  t.f = file_of(x.offsets, x.nfiles, b);
+  const unsigned long long fstart = x.offsets[t.f];
+  t.fend = x.offsets[t.f + 1];
+  // warm the DFA up over the preceding bytes of the same file (outputs there
+  // belong to the previous stream)
+  for (unsigned long long q = (b - fstart > warmup) ? b - warmup : fstart; q < b; ++q) {
+    const uint32_t c = x.data[q];
+    t.s = x.next[t.s + x.cls[c]];
+    t.p2 = t.p1;
+    t.p1 = c;
+  }
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     const uint8_t* __restrict__ data, unsigned long long total,
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
     uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
-    const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_ids, uint32_t nkw,
-    uint32_t warmup, unsigned long long nchunks,
+    const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
+    uint32_t nkw, uint32_t warmup, unsigned long long nchunks,
     uint32_t* __restrict__ kwbits, uint32_t kw_words,
     unsigned long long* __restrict__ hits, unsigned int* __restrict__ counters, uint32_t hit_cap,
     uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
@@ -132,8 +228,14 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
   uint32_t* s_hitcnt = reinterpret_cast<uint32_t*>(smem + kHitBuf * 8);
   uint32_t* s_base = s_hitcnt + 1;
   uint8_t* s_tab = smem + kHitBuf * 8 + 16;
-  const uint16_t* next = g_next;
-  const uint8_t* cls = g_cls;
+  K1Ctx<kLds> x;
+  x.data = data; x.offsets = offsets; x.nfiles = nfiles;
+  x.next = g_next; x.cls = g_cls;
+  x.first_out = first_out; x.nclasses = nclasses;
+  x.meta = g_meta; x.list = g_list; x.nkw = nkw;
+  x.kwbits = kwbits; x.kw_words = kw_words;
+  x.hits = hits; x.counters = counters; x.hit_cap = hit_cap;
+  x.s_hits = s_hits; x.s_hitcnt = s_hitcnt; x.fflags = fflags;
   if (kLds) {
     uint16_t* s_next = reinterpret_cast<uint16_t*>(s_tab);
     const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
@@ -142,8 +244,14 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     uint4* dst = reinterpret_cast<uint4*>(s_next);
     for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = g_cls[i];
-    next = s_next;
-    cls = s_cls;
+    OutMeta* s_meta = reinterpret_cast<OutMeta*>(s_cls + 256);
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_meta + nmeta);
+    for (uint32_t i = threadIdx.x; i < nmeta; i += blockDim.x) s_meta[i] = g_meta[i];
+    for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
+    x.next = s_next;
+    x.cls = s_cls;
+    x.meta = s_meta;
+    x.list = s_list;
   }
   const unsigned long long per_iter = static_cast<unsigned long long>(gridDim.x) * blockDim.x;
   for (unsigned long long base = static_cast<unsigned long long>(blockIdx.x) * blockDim.x; base < nchunks;
@@ -154,84 +262,61 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     if (c < nchunks) {
       const unsigned long long c0 = c * kChunk;
       const unsigned long long c1 = min(c0 + kChunk, total);
-      uint32_t f = file_of(offsets, nfiles, c0);
-      unsigned long long fstart = offsets[f], fend = offsets[f + 1];
-      uint32_t s = 0;
-      unsigned long long kw0 = 0, kw1 = 0;
-      unsigned long long p = (c0 - fstart > warmup) ? c0 - warmup : fstart;
-      uint32_t p1 = 0, p2 = 0;   // previous two bytes (fold-special detection)
-      for (; p < c0; ++p) {
-        const uint32_t b = data[p];
-        s = next[s * nclasses + cls[b]];
-        p2 = p1;
-        p1 = b;
-      }
-      // warm-up outputs are not ours: drop them
-      uint32_t nl = 0;
-      for (p = c0; p < c1; p += 16) {
-        const uint4 v = *reinterpret_cast<const uint4*>(data + p);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        if ((v.x | v.y | v.z | v.w) & 0x80808080u) {
-          // a non-ASCII byte: check for U+0130 / U+017F / U+212A (fold onto ASCII letters)
-          unsigned long long q0 = p;
-          uint32_t a = p1, bb = p2;
-          bool hit = false;
-          for (int k = 0; k < 16 && q0 + k < c1; ++k) {
-            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-            if (q0 + k == fend) { a = bb = 0; }
-            if ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)) hit = true;
-            bb = a;
-            a = b;
-          }
-          if (hit) {
-            // attribute to every file overlapping this word (conservative)
-            for (unsigned long long q = p; q < min(p + 16, c1); ++q) atomicOr(&fflags[file_of(offsets, nfiles, q)], 1u);
+      K1Stream A;
+      k1_init(x, A, c0, c1, warmup);
+      while (A.p < A.end) {
+        // one whole 128-byte line per lane per iteration: the 8 loads are
+        // issued back to back so the line is fetched from HBM once (issuing
+        // them one per 16 bytes let the line be evicted in between: 8x fetch)
+        uint4 line[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned long long q = A.p + 16 * i;
+          if (q < A.end) {
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + q));
+            line[i] = make_uint4(t.x, t.y, t.z, t.w);
+          } else {
+            line[i] = make_uint4(0, 0, 0, 0);
           }
         }
-        if (p + 16 <= fend && p + 16 <= c1) {
-          nl += nl_in_word(w[0]) + nl_in_word(w[1]) + nl_in_word(w[2]) + nl_in_word(w[3]);
-          // the 16 class lookups do not depend on the DFA state: issue them
-          // first, then walk the dependent transition chain, and look at
-          // outputs only if some state in this word has one
-          uint32_t cl[16];
 #pragma unroll
-          for (int k = 0; k < 16; ++k) cl[k] = cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
-          uint32_t st[16];
-          uint32_t mx = 0;
+        for (int i = 0; i < 8; ++i) {
+          if (A.p >= A.end) break;
+          const uint32_t w[4] = {line[i].x, line[i].y, line[i].z, line[i].w};
+          if ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) k1_special(x, A, w);
+          if (A.p + 16 <= A.end && A.p + 16 <= A.fend) {
+            A.nl += nl_in_word(w[0]) + nl_in_word(w[1]) + nl_in_word(w[2]) + nl_in_word(w[3]);
+            // the 16 class lookups do not depend on the state: issue them
+            // first, then walk the dependent transition chain; outputs are
+            // rare, so a word with one is walked again to emit them
+            uint32_t cl[16];
 #pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            s = next[s * nclasses + cl[k]];
-            st[k] = s;
-            mx = max(mx, s);
-          }
-          if (mx >= first_out) {
+            for (int k = 0; k < 16; ++k) cl[k] = x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
+            uint32_t st[16];
+            uint32_t sA = A.s, mx = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-              if (st[k] >= first_out) TSG_OUT(st[k], p + k);
+              sA = x.next[sA + cl[k]];
+              st[k] = sA;
+              mx = max(mx, sA);
             }
-          }
-          p2 = (w[3] >> 16) & 0xffu;
-          p1 = w[3] >> 24;
-        } else {
-          for (int k = 0; k < 16; ++k) {
-            const unsigned long long q = p + k;
-            if (q >= c1) break;
-            if (q >= fend) {
-              flush_kw(kwbits, kw_words, f, kw0, kw1);
-              do { ++f; fstart = fend; fend = offsets[f + 1]; } while (q >= fend);
-              s = 0;
-              p1 = p2 = 0;
+            A.s = sA;
+            if (mx >= first_out) {
+#pragma unroll
+              for (int k = 0; k < 16; ++k) {
+                if (st[k] >= first_out) k1_out(x, A, st[k], A.p + k);
+              }
             }
-            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-            nl += (b == 0x0au);
-            TSG_STEP(b, q);
-            p2 = p1;
-            p1 = b;
+            A.p2 = (w[3] >> 16) & 0xffu;
+            A.p1 = w[3] >> 24;
+            A.p += 16;
+          } else {
+            k1_word_slow(x, A, w);
           }
         }
       }
-      flush_kw(kwbits, kw_words, f, kw0, kw1);
-      nl_count[c] = nl;
+      flush_kw(kwbits, kw_words, A.f, A.kw0, A.kw1);
+      nl_count[c] = A.nl;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -247,8 +332,6 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     __syncthreads();
   }
 }
-#undef TSG_STEP
-#undef TSG_OUT
 
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
@@ -337,8 +420,9 @@ struct Engine::Impl {
   // tables
   uint16_t* scan_next = nullptr;
   uint8_t* scan_cls = nullptr;
-  uint32_t* out_off = nullptr;
-  uint32_t* out_ids = nullptr;
+  OutMeta* out_meta = nullptr;
+  uint32_t* out_list = nullptr;
+  uint32_t nmeta = 0, nlist = 0;
   AnchorDev* anchors = nullptr;
   RuleDev* rules = nullptr;
   uint32_t* rule_kw = nullptr;
@@ -347,6 +431,8 @@ struct Engine::Impl {
   uint8_t* v_acc = nullptr;
   uint8_t* v_cls = nullptr;
   uint32_t table_words16 = 0;
+  uint32_t scan_stride = 0;
+  size_t meta_bytes = 0;
   bool table_in_lds = false;
   uint32_t kw_words = 1;
   // batch buffers
@@ -389,11 +475,45 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess) { *err = "hipStreamCreate failed"; return nullptr; }
   for (auto& ev : m.ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
   const Prefilter& pf = e->pf_;
-  // scan table (padded to 16 B for vector LDS fill)
-  std::vector<uint16_t> sn = pf.scan.t.next;
+  // scan table with an odd dword row stride: next[s*stride + c] then spreads
+  // the same class of different states over different LDS banks (a 64-class
+  // row is 32 dwords, which would put every state's class c in one bank)
+  const uint32_t C = pf.scan.t.nclasses;
+  uint32_t stride = (C + 2) & ~1u;            // >= C+1: slot C holds the output-state index
+  if (((stride / 2) & 1u) == 0) stride += 2;
+  m.scan_stride = stride;
+  std::vector<uint16_t> sn(static_cast<size_t>(pf.scan.t.nstates) * stride, 0);
+  // entries hold the next state's row offset (state * stride): the DFA chain
+  // is then one add + one LDS read per byte (no multiply)
+  if (static_cast<uint64_t>(pf.scan.t.nstates) * stride > 65535) {
+    *err = "scan DFA too large for 16-bit pre-multiplied offsets";
+    return nullptr;
+  }
+  for (uint32_t st = 0; st < pf.scan.t.nstates; ++st) {
+    for (uint32_t c = 0; c < C; ++c)
+      sn[static_cast<size_t>(st) * stride + c] = static_cast<uint16_t>(pf.scan.t.next[static_cast<size_t>(st) * C + c] * stride);
+    if (st >= pf.scan.first_out_state) sn[static_cast<size_t>(st) * stride + C] = static_cast<uint16_t>(st - pf.scan.first_out_state);
+  }
+  // per output state: keyword masks (ids < 128) + list of other output ids
+  std::vector<OutMeta> meta;
+  std::vector<uint32_t> olist;
+  for (uint32_t o = 0; o + 1 < pf.scan.out_off.size(); ++o) {
+    OutMeta om{0, 0, static_cast<uint32_t>(olist.size()), 0};
+    for (uint32_t k = pf.scan.out_off[o]; k < pf.scan.out_off[o + 1]; ++k) {
+      const uint32_t id = pf.scan.out_ids[k];
+      if (id < pf.nkw && id < 64) om.kw0 |= 1ull << id;
+      else if (id < pf.nkw && id < 128) om.kw1 |= 1ull << (id - 64);
+      else olist.push_back(id);
+    }
+    om.list_count = static_cast<uint32_t>(olist.size()) - om.list_begin;
+    meta.push_back(om);
+  }
+  m.nmeta = static_cast<uint32_t>(meta.size());
+  m.nlist = static_cast<uint32_t>(olist.size());
+  m.meta_bytes = ((meta.size() * sizeof(OutMeta) + olist.size() * 4) + 15) & ~size_t(15);
+  m.table_in_lds = static_cast<size_t>(m.table_words16) * 2 + kHitBuf * 8 + 512 + m.meta_bytes <= kLdsTableMax;
   m.table_words16 = static_cast<uint32_t>(sn.size());
   sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
-  m.table_in_lds = static_cast<size_t>(m.table_words16) * 2 + kHitBuf * 8 + 512 <= kLdsTableMax;
   std::vector<uint8_t> cls(pf.scan.t.byte_class, pf.scan.t.byte_class + 256);
   std::vector<AnchorDev> an;
   for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
@@ -416,7 +536,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   }
   m.kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
   if (!dev_upload(sn, &m.scan_next, err) || !dev_upload(cls, &m.scan_cls, err) ||
-      !dev_upload(pf.scan.out_off, &m.out_off, err) || !dev_upload(pf.scan.out_ids, &m.out_ids, err) ||
+      !dev_upload(meta, &m.out_meta, err) || !dev_upload(olist, &m.out_list, err) ||
       !dev_upload(an, &m.anchors, err) || !dev_upload(rd, &m.rules, err) ||
       !dev_upload(pf.rule_kw, &m.rule_kw, err) || !dev_upload(vd, &m.vdfa, err) ||
       !dev_upload(vn, &m.v_next, err) || !dev_upload(va, &m.v_acc, err) || !dev_upload(vc, &m.v_cls, err)) {
@@ -430,7 +550,7 @@ Engine::~Engine() {
   if (!impl_) return;
   Impl& m = *impl_;
   hipSetDevice(device_);
-  void* ps[] = {m.scan_next, m.scan_cls, m.out_off, m.out_ids, m.anchors, m.rules, m.rule_kw, m.vdfa,
+  void* ps[] = {m.scan_next, m.scan_cls, m.out_meta, m.out_list, m.anchors, m.rules, m.rule_kw, m.vdfa,
                 m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw, m.d_hits, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& ev : m.ev) if (ev) hipEventDestroy(ev);
@@ -479,7 +599,7 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
     uint64_t want_blocks = (nchunks + kBlock - 1) / kBlock;
     uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * 2ull)));
     const uint32_t warm = pf.scan.max_pattern_bytes > 0 ? pf.scan.max_pattern_bytes - 1 : 0;
-    const size_t lds = kHitBuf * 8 + 16 + (m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 : 0);
+    const size_t lds = kHitBuf * 8 + 16 + (m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 + m.meta_bytes : 0);
     if (m.table_in_lds) {
       HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tsg_k1_scan<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
@@ -495,14 +615,14 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
       if (m.table_in_lds) {
         hipLaunchKernelGGL(tsg_k1_scan<true>, dim3(blocks), dim3(kBlock), lds, m.stream,
                            d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
-                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state, m.out_off, m.out_ids,
-                           pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
+                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state * m.scan_stride,
+                           m.out_meta, m.nmeta, m.out_list, m.nlist, pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
                            static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
       } else {
         hipLaunchKernelGGL(tsg_k1_scan<false>, dim3(blocks), dim3(kBlock), lds, m.stream,
                            d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
-                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state, m.out_off, m.out_ids,
-                           pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
+                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state * m.scan_stride,
+                           m.out_meta, m.nmeta, m.out_list, m.nlist, pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
                            static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
       }
       HIP_OK(hipGetLastError());
@@ -598,6 +718,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   auto t0 = std::chrono::steady_clock::now();
   if (!run_gpu(in, st, err)) return false;
   auto t_host = std::chrono::steady_clock::now();
+  st->gpu_wall_ms = ms_since(t0);
   Impl& m = *impl_;
   const Ruleset& rs = *rs_;
   const size_t nr = rs.rules.size();
