@@ -32,6 +32,7 @@ struct tsg_engine {
 };
 
 struct tsg_result {
+  std::shared_ptr<const Ruleset> rs;     // findings point at its rules
   std::vector<Secret> files;
   ScanStats stats;
   std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
@@ -111,6 +112,7 @@ static int do_scan(tsg_engine* e, const void* d_data, const uint8_t* h_data, con
   in.path_lens = path_lens;
   in.binary = binary;
   auto* r = new tsg_result();
+  r->rs = e->eng->ruleset();
   std::string err;
   {
     std::lock_guard<std::mutex> lk(e->mu);
@@ -172,38 +174,42 @@ int tsg_result_file_error(const tsg_result* r, uint32_t f) {
 
 int tsg_result_finding(const tsg_result* r, uint32_t f, uint32_t k, tsg_finding* out) {
   if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
-  const Finding& x = r->files[f].findings[k];
-  out->rule_id = x.rule_id.data(); out->rule_id_len = x.rule_id.size();
-  out->category = x.category.data(); out->category_len = x.category.size();
-  out->severity = x.severity.data(); out->severity_len = x.severity.size();
-  out->title = x.title.data(); out->title_len = x.title.size();
+  const Secret& sec = r->files[f];
+  const FindingRec& x = sec.findings[k];
+  const Rule& ru = *x.rule;
+  const std::string& sev = Secret::severity(x);
+  out->rule_id = ru.id.data(); out->rule_id_len = ru.id.size();
+  out->category = ru.category.data(); out->category_len = ru.category.size();
+  out->severity = sev.data(); out->severity_len = sev.size();
+  out->title = ru.title.data(); out->title_len = ru.title.size();
   out->start_line = x.start_line;
   out->end_line = x.end_line;
-  out->match = x.match.data(); out->match_len = x.match.size();
-  out->num_lines = static_cast<uint32_t>(x.code.size());
+  out->match = sec.ptr(x.match); out->match_len = x.match.len;
+  out->num_lines = x.line_count;
   return TSG_OK;
 }
 
 int tsg_result_line(const tsg_result* r, uint32_t f, uint32_t k, uint32_t l, tsg_line* out) {
   if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
-  const Finding& x = r->files[f].findings[k];
-  if (l >= x.code.size()) return fail(TSG_ERR_INVALID, "line index out of range");
-  const Line& ln = x.code[l];
+  const Secret& sec = r->files[f];
+  const FindingRec& x = sec.findings[k];
+  if (l >= x.line_count) return fail(TSG_ERR_INVALID, "line index out of range");
+  const LineRec& ln = sec.lines[x.line_begin + l];
   out->number = ln.number;
-  out->content = ln.content.data(); out->content_len = ln.content.size();
+  out->content = sec.ptr(ln.content); out->content_len = ln.content.len;
   out->is_cause = ln.is_cause;
-  out->annotation = ln.annotation.data(); out->annotation_len = ln.annotation.size();
-  out->truncated = ln.truncated;
-  out->highlighted = ln.highlighted.data(); out->highlighted_len = ln.highlighted.size();
+  out->annotation = ""; out->annotation_len = 0;
+  out->truncated = 0;
+  out->highlighted = sec.ptr(ln.content); out->highlighted_len = ln.content.len;
   out->first_cause = ln.first_cause;
   out->last_cause = ln.last_cause;
   return TSG_OK;
 }
 
-static void json_str(std::string* o, const std::string& s) {
+static void json_bytes(std::string* o, const char* data, size_t n) {
   o->push_back('"');
-  const uint8_t* p = reinterpret_cast<const uint8_t*>(s.data());
-  size_t i = 0, n = s.size();
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(data);
+  size_t i = 0;
   char buf[16];
   while (i < n) {
     uint8_t c = p[i];
@@ -221,11 +227,13 @@ static void json_str(std::string* o, const std::string& s) {
     int32_t r; int w;
     re::decode_rune(p + i, n - i, &r, &w);
     if (r == 0xFFFD && w == 1) { snprintf(buf, sizeof buf, "\\udc%02x", c); *o += buf; i += 1; continue; }
-    o->append(s, i, w);
+    o->append(data + i, w);
     i += w;
   }
   o->push_back('"');
 }
+
+static void json_str(std::string* o, const std::string& s) { json_bytes(o, s.data(), s.size()); }
 
 int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
   if (!r || !json) return fail(TSG_ERR_INVALID, "NULL argument");
@@ -237,30 +245,30 @@ int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
     json_str(&o, s.file_path);
     o += ",\"Findings\":[";
     for (size_t k = 0; k < s.findings.size(); ++k) {
-      const Finding& x = s.findings[k];
+      const FindingRec& x = s.findings[k];
       if (k) o += ",";
-      o += "{\"RuleID\":"; json_str(&o, x.rule_id);
-      o += ",\"Category\":"; json_str(&o, x.category);
-      o += ",\"Severity\":"; json_str(&o, x.severity);
-      o += ",\"Title\":"; json_str(&o, x.title);
+      o += "{\"RuleID\":"; json_str(&o, x.rule->id);
+      o += ",\"Category\":"; json_str(&o, x.rule->category);
+      o += ",\"Severity\":"; json_str(&o, Secret::severity(x));
+      o += ",\"Title\":"; json_str(&o, x.rule->title);
       o += ",\"StartLine\":" + std::to_string(x.start_line);
       o += ",\"EndLine\":" + std::to_string(x.end_line);
       o += ",\"Code\":{\"Lines\":[";
-      for (size_t l = 0; l < x.code.size(); ++l) {
-        const Line& ln = x.code[l];
+      for (uint32_t l = 0; l < x.line_count; ++l) {
+        const LineRec& ln = s.lines[x.line_begin + l];
         if (l) o += ",";
         o += "{\"Number\":" + std::to_string(ln.number);
-        o += ",\"Content\":"; json_str(&o, ln.content);
+        o += ",\"Content\":"; json_bytes(&o, s.ptr(ln.content), ln.content.len);
         o += std::string(",\"IsCause\":") + (ln.is_cause ? "true" : "false");
-        o += ",\"Annotation\":"; json_str(&o, ln.annotation);
-        o += std::string(",\"Truncated\":") + (ln.truncated ? "true" : "false");
-        o += ",\"Highlighted\":"; json_str(&o, ln.highlighted);
+        o += ",\"Annotation\":\"\"";
+        o += ",\"Truncated\":false";
+        o += ",\"Highlighted\":"; json_bytes(&o, s.ptr(ln.content), ln.content.len);
         o += std::string(",\"FirstCause\":") + (ln.first_cause ? "true" : "false");
         o += std::string(",\"LastCause\":") + (ln.last_cause ? "true" : "false");
         o += "}";
       }
       o += "]},\"Match\":";
-      json_str(&o, x.match);
+      json_bytes(&o, s.ptr(x.match), x.match.len);
       o += "}";
     }
     o += "]";
@@ -309,6 +317,7 @@ int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const ui
                             tsg_result** out) {
   if (!rs || !out || !offsets || (nfiles && (!paths || !data))) return fail(TSG_ERR_INVALID, "NULL argument");
   auto* r = new tsg_result();
+  r->rs = rs->rs;
   r->files.resize(nfiles);
   std::atomic<uint32_t> next{0};
   auto worker = [&]() {
@@ -336,6 +345,7 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   std::string err;
   if (!build_prefilter(*rs->rs, &pf, &err)) return fail(TSG_ERR_INTERNAL, err);
   auto* r = new tsg_result();
+  r->rs = rs->rs;
   r->files.resize(nfiles);
   r->cands.resize(nfiles);
   // per-chunk newline counts over the packed batch, as K1 produces them

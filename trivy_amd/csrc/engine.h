@@ -46,6 +46,7 @@ class Engine {
                       ScanStats* stats, std::string* err);
 
   const Prefilter& prefilter() const { return pf_; }
+  std::shared_ptr<const Ruleset> ruleset() const { return rs_; }
   int device() const { return device_; }
   void set_threads(int n) { threads_ = n; }
 

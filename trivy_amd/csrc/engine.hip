@@ -27,6 +27,7 @@
 #include <thread>
 
 #include "engine.h"
+#include "threadpool.h"
 
 namespace tsg {
 
@@ -450,6 +451,7 @@ struct Engine::Impl {
   std::vector<uint32_t> h_nl;
   std::vector<uint32_t> h_kw;
   std::vector<uint32_t> h_ff;
+  std::unique_ptr<ThreadPool> pool;
   int sms = 256;
 };
 
@@ -808,10 +810,8 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     }
   };
   int nt = threads_ > 0 ? threads_ : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
-  std::vector<std::thread> pool;
-  for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
-  worker();
-  for (auto& t : pool) t.join();
+  if (!m.pool || m.pool->size() != nt) m.pool.reset(new ThreadPool(nt));
+  m.pool->run([&](int) { worker(); });
   st->host_ms = ms_since(t_host);
   st->confirm_files = nconf.load();
   st->findings = nfind.load();

@@ -387,10 +387,11 @@ void find_locations(const Ruleset& rs, const Rule& rule, const uint8_t* c, size_
 }
 
 // sort.Slice (go1.23 sort/zsortfunc.go pdqsort_func), restated.
+template <typename T>
 class GoSort {
  public:
   using Less = std::function<bool(size_t, size_t)>;
-  GoSort(std::vector<Finding>* v, Less less) : v_(v), less_(std::move(less)) {}
+  GoSort(std::vector<T>* v, Less less) : v_(v), less_(std::move(less)) {}
   void run() {
     size_t n = v_->size();
     int limit = 0;
@@ -399,7 +400,7 @@ class GoSort {
   }
 
  private:
-  std::vector<Finding>* v_;
+  std::vector<T>* v_;
   Less less_;
   bool lt(long i, long j) { return less_(i, j); }
   void sw(long i, long j) { std::swap((*v_)[i], (*v_)[j]); }
@@ -665,13 +666,16 @@ class CensoredView {
   }
 };
 
-// scanner.go:495-558 on the (virtual) censored buffer.
-Finding to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlines) {
-  Finding f;                                          // scanner.go:475-488
-  f.rule_id = rule.id;
-  f.category = rule.category;
-  f.severity = rule.severity.empty() ? "UNKNOWN" : rule.severity;
-  f.title = rule.title;
+StrRef put(std::string* arena, const std::string& v) {
+  StrRef r{static_cast<uint32_t>(arena->size()), static_cast<uint32_t>(v.size())};
+  arena->append(v);
+  return r;
+}
+
+// scanner.go:475-558 on the (virtual) censored buffer; appends to `out`.
+void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlines, Secret* out) {
+  FindingRec f;
+  f.rule = &rule;
   const size_t n = cv.size();
   const size_t start = static_cast<size_t>(loc.start), end = static_cast<size_t>(loc.end);
   const size_t start_line = cv.count_nl(0, start);
@@ -683,56 +687,56 @@ Finding to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t n
     line_start = (static_cast<long>(start) - static_cast<long>(line_start) - 30 < 0) ? line_start : start - 30;
     line_end = (end + 20 > line_end) ? line_end : end + 20;
   }
-  std::string match_line = cv.str(line_start, line_end);
+  f.match = put(&out->arena, cv.str(line_start, line_end));
   const size_t end_line = start_line + cv.count_nl(start, end);
   const size_t code_start = start_line >= 2 ? start_line - 2 : 0;
   const size_t code_end = std::min<size_t>(end_line + 2, nlines);
   // bounds of lines code_start .. code_end-1 (bytes.Split of the censored buffer)
-  std::vector<std::pair<size_t, size_t>> lines;
+  std::pair<size_t, size_t> lines[8];
+  size_t nl = 0;
   {
-    std::vector<std::pair<size_t, size_t>> before;
+    std::pair<size_t, size_t> before[2];
+    size_t nb = 0;
     size_t b = line0_b;
-    for (size_t k = start_line; k > code_start; --k) {   // walk back
+    for (size_t k = start_line; k > code_start; --k) {   // walk back (at most 2 lines)
       const size_t e = b - 1;                            // the '\n' ending line k-1
       const long q = cv.prev_nl(e);
       const size_t bb = q < 0 ? 0 : static_cast<size_t>(q) + 1;
-      before.push_back({bb, e});
+      before[nb++] = {bb, e};
       b = bb;
     }
-    for (auto it = before.rbegin(); it != before.rend(); ++it) lines.push_back(*it);
+    while (nb > 0) lines[nl++] = before[--nb];
     size_t e = line0_e;
-    lines.push_back({line0_b, line0_e});
-    for (size_t k = start_line + 1; k < code_end; ++k) {
+    lines[nl++] = {line0_b, line0_e};
+    for (size_t k = start_line + 1; k < code_end && nl < 8; ++k) {
       const size_t bb = e + 1;
       e = bb <= n ? cv.next_nl(bb) : n;
-      lines.push_back({bb, e});
+      lines[nl++] = {bb, e};
     }
   }
+  f.line_begin = static_cast<uint32_t>(out->lines.size());
   bool found_first = false;
-  for (size_t idx = 0; idx < lines.size(); ++idx) {
+  size_t last_cause = SIZE_MAX;
+  for (size_t idx = 0; idx < nl; ++idx) {
     const size_t k = code_start + idx;
     if (k >= code_end) break;
     const size_t b = lines[idx].first, e = lines[idx].second;
     const bool in_cause = k >= start_line && k <= end_line;
-    std::string s;
-    if (e - b > 100) s = in_cause ? match_line : cv.str(b, b + 100);
-    else s = cv.str(b, e);
-    Line ln;
+    LineRec ln;
     ln.number = static_cast<int>(k + 1);
-    ln.content = s;
+    if (e - b > 100) ln.content = in_cause ? f.match : put(&out->arena, cv.str(b, b + 100));
+    else ln.content = put(&out->arena, cv.str(b, e));
     ln.is_cause = in_cause;
-    ln.highlighted = s;
     ln.first_cause = !found_first && in_cause;
     found_first = found_first || in_cause;
-    f.code.push_back(std::move(ln));
+    if (in_cause) last_cause = out->lines.size();
+    out->lines.push_back(ln);
   }
-  for (size_t k = f.code.size(); k-- > 0;) {
-    if (f.code[k].is_cause) { f.code[k].last_cause = true; break; }
-  }
+  if (last_cause != SIZE_MAX) out->lines[last_cause].last_cause = true;
+  f.line_count = static_cast<uint32_t>(out->lines.size()) - f.line_begin;
   f.start_line = static_cast<int>(start_line + 1);
   f.end_line = static_cast<int>(end_line + 1);
-  f.match = std::move(match_line);
-  return f;
+  out->findings.push_back(f);
 }
 
 bool keywords_match(const Rule& r, const std::string& lower) {   // scanner.go:174-186
@@ -792,18 +796,22 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
   for (const auto& m : matched) spans.push_back(m.loc);
   CensoredView cv(content, len, std::move(spans), nl);
   const uint64_t nlines = cv.count_nl(0, len) + 1;
+  out.findings.reserve(matched.size());
+  out.lines.reserve(matched.size() * 4);
   for (const auto& m : matched) {
-    Finding f = to_finding(*m.rule, m.loc, cv, nlines);
-    if (binary) {
-      f.match = "Binary file " + go_quote(path) + " matches a rule " + go_quote(m.rule->title);
-      f.code.clear();
+    to_finding(*m.rule, m.loc, cv, nlines, &out);
+    if (binary) {                                     // scanner.go:440-444
+      FindingRec& f = out.findings.back();
+      out.lines.resize(f.line_begin);
+      f.line_count = 0;
+      f.match = put(&out.arena, "Binary file " + go_quote(path) + " matches a rule " + go_quote(m.rule->title));
     }
-    out.findings.push_back(std::move(f));
   }
   auto& fs = out.findings;
-  GoSort(&fs, [&fs](size_t i, size_t j) {
-    if (fs[i].rule_id != fs[j].rule_id) return fs[i].rule_id < fs[j].rule_id;
-    return fs[i].match < fs[j].match;
+  const std::string& ar = out.arena;
+  GoSort<FindingRec>(&fs, [&fs, &ar](size_t i, size_t j) {
+    if (fs[i].rule->id != fs[j].rule->id) return fs[i].rule->id < fs[j].rule->id;
+    return ar.compare(fs[i].match.off, fs[i].match.len, ar, fs[j].match.off, fs[j].match.len) < 0;
   }).run();
   out.file_path = path;
   return out;

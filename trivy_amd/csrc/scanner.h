@@ -43,27 +43,35 @@ struct Ruleset {                         // scanner.go:45-49 (Global)
 // (scanner.go:277-364).  cfg == nullptr -> builtins only.
 bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err);
 
-struct Line {                            // types.Line (misconf.go:51-60)
+// Results are stored compactly: every string of one file's findings lives in
+// that Secret's arena (one allocation per file instead of ~13 per finding).
+struct StrRef { uint32_t off = 0, len = 0; };
+
+struct LineRec {                         // types.Line (misconf.go:51-60)
   int number = 0;
-  std::string content;
-  bool is_cause = false;
-  std::string annotation;
-  bool truncated = false;
-  std::string highlighted;
+  StrRef content;                        // Highlighted == Content (scanner.go:538-545);
+  bool is_cause = false;                 // Annotation "" and Truncated false always
   bool first_cause = false, last_cause = false;
 };
 
-struct Finding {                         // types.SecretFinding (secret.go:10-20)
-  std::string rule_id, category, severity, title;
+struct FindingRec {                      // types.SecretFinding (secret.go:10-20)
+  const Rule* rule = nullptr;            // RuleID, Category, Title; Severity ("" -> "UNKNOWN")
   int start_line = 0, end_line = 0;
-  std::vector<Line> code;
-  std::string match;
+  StrRef match;
+  uint32_t line_begin = 0, line_count = 0;
 };
 
 struct Secret {                          // types.Secret
   std::string file_path;
-  std::vector<Finding> findings;
+  std::string arena;
+  std::vector<FindingRec> findings;
+  std::vector<LineRec> lines;
   int error = 0;                         // nonzero: the reference would panic on this file
+  const char* ptr(StrRef r) const { return arena.data() + r.off; }
+  static const std::string& severity(const FindingRec& f) {
+    static const std::string kUnknown = "UNKNOWN";
+    return f.rule->severity.empty() ? kUnknown : f.rule->severity;
+  }
 };
 
 // Per-(file, rule) plan from the GPU prefilter.
