@@ -23,6 +23,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -33,9 +35,7 @@ namespace tsg {
 
 namespace {
 
-constexpr uint32_t kBlock = 1024;              // one K1 workgroup per CU: 16 waves share the LDS table
-constexpr uint32_t kChunk = 2048;              // bytes per thread-chunk (multiple of 16)
-constexpr uint32_t kLdsTableMax = 140 * 1024;  // scan table bytes kept in LDS (160 KiB per CU)
+constexpr uint32_t kLdsBytes = 160 * 1024;     // LDS per CU
 
 struct AnchorDev { uint32_t rule, min_len, max_len, dmin, dmax; };
 struct RuleDev { uint32_t mode, gate_on_gpu, always_gate, kw_begin, kw_count, verify_dfa, verify_limit, pad; };
@@ -63,22 +63,31 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
   return f;
 }
 
-constexpr uint32_t kHitBuf = 4096;
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));             // per-block LDS hit buffer (8-byte hits)
+constexpr uint32_t kWaveHits = 1024;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
+constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
+constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
-// One DFA step + outputs.  Keyword ids < 128 accumulate in two per-thread
-// 64-bit masks (flushed with atomicOr at file changes / chunk end); anchor
-// hits go to the block's LDS buffer.
+// Keyword ids < 128 accumulate in two per-stream 64-bit masks, flushed with
+// atomicOr at file changes and at the end of the stream's chunk.
+// Most chunks of a file repeat keywords an earlier chunk already set, and many
+// lanes OR into the same words of a large file: read first, and only issue
+// the (memory-side, serialising) atomic for bits not yet visible.  A stale
+// read only costs a redundant atomic.
+__device__ __forceinline__ void or_bits(uint32_t* w, uint32_t bits) {
+  if (bits && (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bits) != bits) atomicOr(w, bits);
+}
+
 __device__ __forceinline__ void flush_kw(uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t f,
                                          unsigned long long& kw0, unsigned long long& kw1) {
   uint32_t* w = kwbits + static_cast<size_t>(f) * kw_words;
   if (kw0) {
-    if (static_cast<uint32_t>(kw0)) atomicOr(w + 0, static_cast<uint32_t>(kw0));
-    if (static_cast<uint32_t>(kw0 >> 32)) atomicOr(w + 1, static_cast<uint32_t>(kw0 >> 32));
+    or_bits(w + 0, static_cast<uint32_t>(kw0));
+    or_bits(w + 1, static_cast<uint32_t>(kw0 >> 32));
   }
   if (kw1) {
-    if (static_cast<uint32_t>(kw1)) atomicOr(w + 2, static_cast<uint32_t>(kw1));
-    if (static_cast<uint32_t>(kw1 >> 32)) atomicOr(w + 3, static_cast<uint32_t>(kw1 >> 32));
+    or_bits(w + 2, static_cast<uint32_t>(kw1));
+    or_bits(w + 3, static_cast<uint32_t>(kw1 >> 32));
   }
   kw0 = kw1 = 0;
 }
@@ -90,11 +99,16 @@ __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
   return __popc(y);
 }
 
-// Per-stream state of K1 (a thread walks kStreams independent byte ranges so
-// the LDS latency of one DFA chain hides behind the others).
+// Per-stream state of K1.  A lane walks kS independent byte ranges (streams)
+// with their transition chains interleaved, so the LDS latency of one
+// dependent chain hides behind the others.  A stream starts on the 128-byte
+// line at or before (chunk start - warm-up): the bytes before the chunk only
+// warm the DFA up (no outputs, no newline counts); the chunk's own bytes
+// start at `emit`.  Starting earlier than needed is harmless: the scan DFA's
+// state depends only on the last max_pattern_bytes - 1 bytes of the file.
 struct K1Stream {
-  unsigned long long p, end, fend;
-  uint32_t f, s, p1, p2, nl;
+  unsigned long long p, lim, emit;   // next byte; min(stream end, file end); first byte with outputs
+  uint32_t f, s, p12, nl;            // file; DFA row offset; previous two bytes (p1 | p2 << 8); newlines
   unsigned long long kw0, kw1;
 };
 
@@ -102,13 +116,14 @@ struct K1Stream {
 // two masks, and a list of the other output ids (anchors, keywords >= 128).
 struct OutMeta { unsigned long long kw0, kw1; uint32_t list_begin, list_count; };
 
-template <bool kLds>
 struct K1Ctx {
   const uint8_t* __restrict__ data;
+  unsigned long long total;
+  uint32_t chunk;
   const uint64_t* __restrict__ offsets;
   uint32_t nfiles;
   const uint16_t* next;   // pre-multiplied: next[s + c] is the next state's row offset
-  const uint8_t* cls;
+  const uint8_t* cls;     // byte -> class * 2
   uint32_t first_out;     // row offset of the first state with outputs
   uint32_t nclasses;      // row slot `nclasses` holds the output-state index
   const OutMeta* meta;
@@ -116,19 +131,27 @@ struct K1Ctx {
   uint32_t nkw;
   uint32_t* __restrict__ kwbits;
   uint32_t kw_words;
-  unsigned long long* __restrict__ hits;
-  unsigned int* __restrict__ counters;
-  uint32_t hit_cap;
-  unsigned long long* s_hits;
-  uint32_t* s_hitcnt;
+  unsigned long long* __restrict__ hits;   // this workgroup's region of the hit list
+  uint32_t region_cap;
+  uint32_t* b_hitcnt;           // LDS: fill count of the workgroup's region
+  uint32_t* w_hits;             // this wave's LDS hit buffer
+  unsigned long long item_base; // first byte of the wave's current item
+  uint32_t* w_hitcnt;           // and its fill count
   uint32_t* __restrict__ fflags;
 };
 
-// Output metadata of a state with outputs, in LDS: its keyword ids < 128 as
-// two masks, and a list of the other output ids (anchors, keywords >= 128).
+// One transition: `s` is the current state's row offset (state * stride, in
+// uint16 elements) and `c2` the byte's class times 2 (the class map is stored
+// pre-doubled), so the LDS byte address is (s << 1) + c2.
+__device__ __forceinline__ uint32_t k1_step(const uint16_t* next, uint32_t s, uint32_t c2) {
+  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(next) + ((s << 1) + c2));
+}
 
-template <bool kLds>
-__device__ __forceinline__ void k1_out(const K1Ctx<kLds>& x, K1Stream& t, uint32_t st, unsigned long long q) {
+__device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Stream& t) {
+  return min(t.emit + x.chunk, x.total);
+}
+
+__device__ __forceinline__ void k1_out(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
   const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
   const OutMeta m = x.meta[o];
   t.kw0 |= m.kw0;
@@ -138,12 +161,12 @@ __device__ __forceinline__ void k1_out(const K1Ctx<kLds>& x, K1Stream& t, uint32
     if (id < x.nkw) {
       atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
     } else {
-      const unsigned long long h = (q << 24) | (id - x.nkw);
-      const uint32_t li = atomicAdd(x.s_hitcnt, 1u);
-      if (li < kHitBuf) x.s_hits[li] = h;
-      else {
-        const unsigned int gi = atomicAdd(&x.counters[0], 1u);
-        if (gi < x.hit_cap) x.hits[gi] = h;
+      const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
+      if (li < kWaveHits) {
+        x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
+      } else {                                           // buffer full: straight to the region
+        const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
+        if (gi < x.region_cap) x.hits[gi] = (q << 24) | (id - x.nkw);
       }
     }
   }
@@ -151,92 +174,110 @@ __device__ __forceinline__ void k1_out(const K1Ctx<kLds>& x, K1Stream& t, uint32
 
 // U+0130 / U+017F / U+212A fold onto ASCII letters: flag every file that
 // overlaps a 16-byte word ending such a sequence (host re-scans it exactly).
-template <bool kLds>
-__device__ __forceinline__ void k1_special(const K1Ctx<kLds>& x, const K1Stream& t, const uint32_t w[4]) {
-  uint32_t a = t.p1, bb = t.p2;
+// A superset is safe (a flagged file is only scanned more carefully).
+__device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, const uint32_t w[4],
+                                           unsigned long long fend, unsigned long long end) {
+  uint32_t a = t.p12 & 0xffu, bb = t.p12 >> 8;
   bool hit = false;
-  for (int k = 0; k < 16 && t.p + k < t.end; ++k) {
+  for (int k = 0; k < 16 && t.p + k < end; ++k) {
     const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-    if (t.p + k == t.fend) { a = bb = 0; }
+    if (t.p + k == fend) { a = bb = 0; }
     if ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)) hit = true;
     bb = a;
     a = b;
   }
   if (hit) {
-    for (unsigned long long q = t.p; q < min(t.p + 16, t.end); ++q) atomicOr(&x.fflags[file_of(x.offsets, x.nfiles, q)], 1u);
+    for (unsigned long long q = t.p; q < min(t.p + 16, end); ++q) atomicOr(&x.fflags[file_of(x.offsets, x.nfiles, q)], 1u);
   }
 }
 
-// One 16-byte word of one stream with file-boundary checks.
-template <bool kLds>
-__device__ __forceinline__ void k1_word_slow(const K1Ctx<kLds>& x, K1Stream& t, const uint32_t w[4]) {
+// One 16-byte word of one stream with file-boundary and stream-end checks.
+__device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4]) {
+  const unsigned long long end = k1_end(x, t);
+  unsigned long long fend = x.offsets[t.f + 1];
+  if (((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
   for (int k = 0; k < 16; ++k) {
     const unsigned long long q = t.p + k;
-    if (q >= t.end) break;
-    if (q >= t.fend) {
+    if (q >= end) break;
+    if (q >= fend) {
       flush_kw(x.kwbits, x.kw_words, t.f, t.kw0, t.kw1);
-      do { ++t.f; t.fend = x.offsets[t.f + 1]; } while (q >= t.fend);
+      do { ++t.f; fend = x.offsets[t.f + 1]; } while (q >= fend);
       t.s = 0;
-      t.p1 = t.p2 = 0;
+      t.p12 = 0;
     }
     const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-    t.nl += (b == 0x0au);
-    t.s = x.next[t.s + x.cls[b]];
-    if (t.s >= x.first_out) k1_out(x, t, t.s, q);
-    t.p2 = t.p1;
-    t.p1 = b;
+    t.s = k1_step(x.next, t.s, x.cls[b]);
+    if (q >= t.emit) {
+      t.nl += (b == 0x0au);
+      if (t.s >= x.first_out) k1_out(x, t, t.s, q);
+    }
+    t.p12 = ((t.p12 << 8) & 0xff00u) | b;
   }
   t.p += 16;
+  t.lim = min(end, fend);
 }
 
-template <bool kLds>
-__device__ __forceinline__ void k1_init(const K1Ctx<kLds>& x, K1Stream& t, unsigned long long b, unsigned long long e,
-                                        uint32_t warmup) {
-  t.p = b;
-  t.end = e;
-  t.s = 0;
-  t.p1 = t.p2 = 0;
-  t.nl = 0;
-  t.kw0 = t.kw1 = 0;
-  if (b >= e) { t.f = 0; t.fend = 0; return; }
-  t.f = file_of(x.offsets, x.nfiles, b);
-  const unsigned long long fstart = x.offsets[t.f];
-  t.fend = x.offsets[t.f + 1];
-  // warm the DFA up over the preceding bytes of the same file (outputs there
-  // belong to the previous stream)
-  for (unsigned long long q = (b - fstart > warmup) ? b - warmup : fstart; q < b; ++q) {
-    const uint32_t c = x.data[q];
-    t.s = x.next[t.s + x.cls[c]];
-    t.p2 = t.p1;
-    t.p1 = c;
+// Outputs of a fast word (rare): walk it again from its start state and emit.
+__device__ __forceinline__ void k1_word_emit(const K1Ctx& x, K1Stream& t, uint32_t s0, uint32_t w0, uint32_t w1,
+                                             uint32_t w2, uint32_t w3) {
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t s = s0;
+  for (int k = 0; k < 16; ++k) {
+    s = k1_step(x.next, s, x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu]);
+    if (s >= x.first_out) k1_out(x, t, s, t.p + k);
   }
 }
 
-template <bool kLds>
-__global__ __launch_bounds__(kBlock) void tsg_k1_scan(
+__device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned long long c0, uint32_t warm_lines) {
+  t.emit = c0;
+  t.p = c0 > warm_lines * 128ull ? c0 - warm_lines * 128ull : 0;   // c0 is a multiple of 128
+  t.s = 0;
+  t.p12 = 0;
+  t.nl = 0;
+  t.kw0 = t.kw1 = 0;
+  const unsigned long long end = k1_end(x, t);
+  if (c0 >= end) { t.p = t.lim = end; t.f = 0; return; }
+  t.f = file_of(x.offsets, x.nfiles, t.p);
+  t.lim = min(end, x.offsets[t.f + 1]);
+}
+
+// K1: one pass over the batch.  Workgroup b scans a contiguous range of wave
+// work items (an item = 64 lanes x kS consecutive chunks); its waves take
+// items from an LDS counter.  Each wave owns an LDS hit buffer, flushed once
+// per item into the workgroup's own region of the hit list (LDS atomics
+// only: no global atomic is shared between workgroups, which serialise at the
+// memory side).  block_hits[b] = hits written by workgroup b (> region_cap:
+// overflow, the host grows the list and runs K1 again).
+template <bool kLds, int kS, int kThreads>
+__global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     const uint8_t* __restrict__ data, unsigned long long total,
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
     uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
     const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
-    uint32_t nkw, uint32_t warmup, unsigned long long nchunks,
+    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
     uint32_t* __restrict__ kwbits, uint32_t kw_words,
-    unsigned long long* __restrict__ hits, unsigned int* __restrict__ counters, uint32_t hit_cap,
+    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // LDS layout: [hit buffer | hit count | base | (scan table | class map)]
-  unsigned long long* s_hits = reinterpret_cast<unsigned long long*>(smem);
-  uint32_t* s_hitcnt = reinterpret_cast<uint32_t*>(smem + kHitBuf * 8);
-  uint32_t* s_base = s_hitcnt + 1;
-  uint8_t* s_tab = smem + kHitBuf * 8 + 16;
-  K1Ctx<kLds> x;
-  x.data = data; x.offsets = offsets; x.nfiles = nfiles;
+  // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | (scan table | class map |
+  //              output meta | output list)]
+  constexpr uint32_t kWaves = kThreads / 64;
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
+  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count, [1] next item
+  uint8_t* s_tab = smem + kWaves * kWaveHits * 4 + kMaxWaves * 4 + 16;
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) { s_block[0] = 0; s_block[1] = 0; }
+  K1Ctx x;
+  x.data = data; x.total = total; x.chunk = chunk;
+  x.offsets = offsets; x.nfiles = nfiles;
   x.next = g_next; x.cls = g_cls;
   x.first_out = first_out; x.nclasses = nclasses;
   x.meta = g_meta; x.list = g_list; x.nkw = nkw;
   x.kwbits = kwbits; x.kw_words = kw_words;
-  x.hits = hits; x.counters = counters; x.hit_cap = hit_cap;
-  x.s_hits = s_hits; x.s_hitcnt = s_hitcnt; x.fflags = fflags;
+  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
+  x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
   if (kLds) {
     uint16_t* s_next = reinterpret_cast<uint16_t*>(s_tab);
     const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
@@ -254,97 +295,144 @@ __global__ __launch_bounds__(kBlock) void tsg_k1_scan(
     x.meta = s_meta;
     x.list = s_list;
   }
-  const unsigned long long per_iter = static_cast<unsigned long long>(gridDim.x) * blockDim.x;
-  for (unsigned long long base = static_cast<unsigned long long>(blockIdx.x) * blockDim.x; base < nchunks;
-       base += per_iter) {   // block-uniform trip count
-    if (threadIdx.x == 0) *s_hitcnt = 0;
-    __syncthreads();
-    const unsigned long long c = base + threadIdx.x;
-    if (c < nchunks) {
-      const unsigned long long c0 = c * kChunk;
-      const unsigned long long c1 = min(c0 + kChunk, total);
-      K1Stream A;
-      k1_init(x, A, c0, c1, warmup);
-      while (A.p < A.end) {
-        // one whole 128-byte line per lane per iteration: the 8 loads are
-        // issued back to back so the line is fetched from HBM once (issuing
-        // them one per 16 bytes let the line be evicted in between: 8x fetch)
-        uint4 line[8];
+  __syncthreads();
+  const unsigned long long nwork = (nchunks + kS - 1) / kS;   // lane work units (kS chunks each)
+  const unsigned long long nitems = (nwork + 63) / 64;       // wave work items
+  const unsigned long long per_block = (nitems + gridDim.x - 1) / gridDim.x;
+  const unsigned long long first_item = per_block * blockIdx.x;
+  const unsigned long long last_item = min(first_item + per_block, nitems);
+  for (;;) {
+    unsigned long long item = 0;
+    if (lane == 0) {
+      item = first_item + atomicAdd(&s_block[1], 1u);
+      *x.w_hitcnt = 0;
+    }
+    item = __shfl(item, 0);
+    if (item >= last_item) break;                              // wave-uniform exit
+    __builtin_amdgcn_wave_barrier();
+    x.item_base = item * 64 * kS * static_cast<unsigned long long>(chunk);
+    const unsigned long long wi = item * 64 + lane;
+    if (wi < nwork) {
+      K1Stream S[kS];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const unsigned long long q = A.p + 16 * i;
-          if (q < A.end) {
-            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + q));
-            line[i] = make_uint4(t.x, t.y, t.z, t.w);
-          } else {
-            line[i] = make_uint4(0, 0, 0, 0);
-          }
+      for (int j = 0; j < kS; ++j) k1_init(x, S[j], min((wi * kS + j) * chunk, total), warm_lines);
+      for (;;) {
+        bool any = false, all_fast = true;
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
+          any |= S[j].p < S[j].lim || S[j].p < k1_end(x, S[j]);
+          all_fast &= S[j].p + 128 <= S[j].lim;   // a whole line inside the stream and one file
         }
+        if (!any) break;
+        if (all_fast) {
+          uint4 line[kS][8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (A.p >= A.end) break;
-          const uint32_t w[4] = {line[i].x, line[i].y, line[i].z, line[i].w};
-          if ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) k1_special(x, A, w);
-          if (A.p + 16 <= A.end && A.p + 16 <= A.fend) {
-            A.nl += nl_in_word(w[0]) + nl_in_word(w[1]) + nl_in_word(w[2]) + nl_in_word(w[3]);
-            // the 16 class lookups do not depend on the state: issue them
-            // first, then walk the dependent transition chain; outputs are
-            // rare, so a word with one is walked again to emit them
-            uint32_t cl[16];
+          for (int j = 0; j < kS; ++j) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) cl[k] = x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
-            uint32_t st[16];
-            uint32_t sA = A.s, mx = 0;
+            for (int i = 0; i < 8; ++i) {
+              // the 8 loads of a line are issued back to back so the line is
+              // fetched from HBM once
+              const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + S[j].p + 16 * i));
+              line[j][i] = make_uint4(v.x, v.y, v.z, v.w);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            // the class lookups do not depend on the state: issue them all,
+            // then walk the kS dependent transition chains interleaved
+            uint32_t cl[kS][16];
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+              const uint32_t w[4] = {line[j][i].x, line[j][i].y, line[j][i].z, line[j][i].w};
+              if (((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && S[j].p >= S[j].emit)
+                k1_special(x, S[j], w, ~0ull, ~0ull);
+#pragma unroll
+              for (int k = 0; k < 16; ++k) cl[j][k] = x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
+            }
+            uint32_t st[kS][16], mx[kS];
+#pragma unroll
+            for (int j = 0; j < kS; ++j) mx[j] = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-              sA = x.next[sA + cl[k]];
-              st[k] = sA;
-              mx = max(mx, sA);
-            }
-            A.s = sA;
-            if (mx >= first_out) {
 #pragma unroll
-              for (int k = 0; k < 16; ++k) {
-                if (st[k] >= first_out) k1_out(x, A, st[k], A.p + k);
+              for (int j = 0; j < kS; ++j) {
+                st[j][k] = k1_step(x.next, k ? st[j][k - 1] : S[j].s, cl[j][k]);
+                mx[j] = max(mx[j], st[j][k]);
               }
             }
-            A.p2 = (w[3] >> 16) & 0xffu;
-            A.p1 = w[3] >> 24;
-            A.p += 16;
-          } else {
-            k1_word_slow(x, A, w);
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+              const uint32_t w0 = line[j][i].x, w1 = line[j][i].y, w2 = line[j][i].z, w3 = line[j][i].w;
+              S[j].s = st[j][15];
+              if (S[j].p >= S[j].emit) {
+                S[j].nl += nl_in_word(w0) + nl_in_word(w1) + nl_in_word(w2) + nl_in_word(w3);
+                // outputs (a few % of lane-words): the states are in
+                // registers; each position is skipped by the whole wave
+                // unless one of its lanes has an output there
+                if (mx[j] >= first_out) {
+#pragma unroll
+                  for (int k = 0; k < 16; ++k)
+                    if (st[j][k] >= first_out) k1_out(x, S[j], st[j][k], S[j].p + k);
+                }
+              }
+              S[j].p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
+              S[j].p += 16;
+            }
+          }
+        } else {
+          // a line with a file boundary or a stream end (rare): word by word,
+          // one stream at a time, words re-read from memory (L2 hits)
+          for (int j = 0; j < kS; ++j) {
+            for (int i = 0; i < 8 && S[j].p < k1_end(x, S[j]); ++i) {
+              const v4u v = *reinterpret_cast<const v4u*>(data + S[j].p);
+              const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+              k1_word_slow(x, S[j], w);
+            }
           }
         }
       }
-      flush_kw(kwbits, kw_words, A.f, A.kw0, A.kw1);
-      nl_count[c] = A.nl;
+#pragma unroll
+      for (int j = 0; j < kS; ++j) {
+        const unsigned long long c = wi * kS + j;
+        if (c < nchunks) {
+          flush_kw(kwbits, kw_words, S[j].f, S[j].kw0, S[j].kw1);
+          nl_count[c] = S[j].nl;
+        }
+      }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t n = min(*s_hitcnt, kHitBuf);
-      *s_base = n ? atomicAdd(&counters[0], n) : 0u;
+    // flush this wave's hit buffer (the wave has reconverged here)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t n = min(*x.w_hitcnt, kWaveHits);
+    uint32_t b0 = 0;
+    if (lane == 0 && n) b0 = atomicAdd(x.b_hitcnt, n);
+    b0 = __shfl(b0, 0);
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t h = x.w_hits[i];
+      if (b0 + i < region_cap) x.hits[b0 + i] = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
     }
-    __syncthreads();
-    const uint32_t n = min(*s_hitcnt, kHitBuf);
-    const uint32_t b0 = *s_base;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      if (b0 + i < hit_cap) hits[b0 + i] = s_hits[i];
-    }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
+  __syncthreads();
+  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
 }
 
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
-    const unsigned long long* __restrict__ hits, uint32_t nhits,
-    const AnchorDev* __restrict__ anchors, const RuleDev* __restrict__ rules,
+    const unsigned long long* __restrict__ hits, const uint32_t* __restrict__ block_hits, uint32_t region_cap,
+    uint32_t nregions, const AnchorDev* __restrict__ anchors, const RuleDev* __restrict__ rules,
     const uint32_t* __restrict__ rule_kw, const uint32_t* __restrict__ kwbits, uint32_t kw_words,
     const VDfaDev* __restrict__ vd, const uint16_t* __restrict__ v_next,
     const uint8_t* __restrict__ v_acc, const uint8_t* __restrict__ v_cls,
     CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nhits; i += stride) {
-    const unsigned long long h = hits[i];
+  // K2 workgroup (r, k) verifies region r's hits k*256+tid, stride 256*(grid/nregions)
+  const uint32_t r = blockIdx.x % nregions;
+  const uint32_t nsub = gridDim.x / nregions;
+  const uint32_t nhits = min(block_hits[r], region_cap);
+  const unsigned long long* __restrict__ rh = hits + static_cast<size_t>(r) * region_cap;
+  for (uint32_t i = (blockIdx.x / nregions) * blockDim.x + threadIdx.x; i < nhits; i += nsub * blockDim.x) {
+    const unsigned long long h = rh[i];
     const unsigned long long q = h >> 24;
     const AnchorDev an = anchors[h & 0xffffffu];
     const RuleDev r = rules[an.rule];
@@ -387,6 +475,18 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
       }
     }
   }
+}
+
+// K1 instantiations: (workgroup size, interleaved streams per lane)
+template <bool kLds>
+const void* k1_kernel_t(uint32_t threads, int ks) {
+  if (threads == 1024 && ks == 1) return reinterpret_cast<const void*>(&tsg_k1_scan<kLds, 1, 1024>);
+  if (threads == 512 && ks == 2) return reinterpret_cast<const void*>(&tsg_k1_scan<kLds, 2, 512>);
+  return nullptr;
+}
+
+const void* k1_kernel(bool lds, uint32_t threads, int ks) {
+  return lds ? k1_kernel_t<true>(threads, ks) : k1_kernel_t<false>(threads, ks);
 }
 
 template <typename T>
@@ -441,6 +541,8 @@ struct Engine::Impl {
   uint64_t* d_off = nullptr; size_t d_off_cap = 0;
   uint32_t* d_kw = nullptr; size_t d_kw_cap = 0;
   unsigned long long* d_hits = nullptr; size_t d_hits_cap = 0;
+  uint32_t* d_bh = nullptr; size_t d_bh_cap = 0;    // hits written per K1 workgroup (its region of d_hits)
+  std::vector<uint32_t> h_bh;
   CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
   uint32_t* d_nl = nullptr; size_t d_nl_cap = 0;
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
@@ -453,6 +555,9 @@ struct Engine::Impl {
   std::vector<uint32_t> h_ff;
   std::unique_ptr<ThreadPool> pool;
   int sms = 256;
+  int k1_streams = 1;                 // interleaved DFA streams per K1 lane  } TSG_K1_CFG="threads,streams"
+  uint32_t k1_threads = 1024;         // K1 workgroup size                  }
+  uint32_t chunk = 4096;              // bytes per K1 stream chunk (multiple of 128; TSG_K1_CHUNK)
 };
 
 int device_count() {
@@ -474,6 +579,17 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   if (hipSetDevice(device) != hipSuccess) { *err = "hipSetDevice failed"; return nullptr; }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) m.sms = prop.multiProcessorCount;
+  if (const char* c = std::getenv("TSG_K1_CHUNK")) {
+    const long v = std::atol(c);
+    if (v >= 256 && v % 128 == 0) m.chunk = static_cast<uint32_t>(v);
+  }
+  if (const char* cfg = std::getenv("TSG_K1_CFG")) {
+    unsigned t = 0, k = 0;
+    if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k))) {
+      m.k1_threads = t;
+      m.k1_streams = static_cast<int>(k);
+    }
+  }
   if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess) { *err = "hipStreamCreate failed"; return nullptr; }
   for (auto& ev : m.ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
   const Prefilter& pf = e->pf_;
@@ -513,10 +629,16 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   m.nmeta = static_cast<uint32_t>(meta.size());
   m.nlist = static_cast<uint32_t>(olist.size());
   m.meta_bytes = ((meta.size() * sizeof(OutMeta) + olist.size() * 4) + 15) & ~size_t(15);
-  m.table_in_lds = static_cast<size_t>(m.table_words16) * 2 + kHitBuf * 8 + 512 + m.meta_bytes <= kLdsTableMax;
   m.table_words16 = static_cast<uint32_t>(sn.size());
+  // LDS: per-wave hit buffers (16 waves) + scan table + class map + output metadata
+  m.table_in_lds = kMaxWaves * kWaveHits * 4 + kMaxWaves * 4 + static_cast<size_t>(m.table_words16) * 2 + 16 + 256 +
+                   m.meta_bytes <= kLdsBytes;
+  if (pf.anchors.size() >= (1u << kAnchorBits)) { *err = "too many anchor literals for K1's hit encoding"; return nullptr; }
   sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
-  std::vector<uint8_t> cls(pf.scan.t.byte_class, pf.scan.t.byte_class + 256);
+  // K1's class map holds class * 2 (see k1_step)
+  if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return nullptr; }
+  std::vector<uint8_t> cls(256);
+  for (int b = 0; b < 256; ++b) cls[b] = static_cast<uint8_t>(pf.scan.t.byte_class[b] * 2);
   std::vector<AnchorDev> an;
   for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
   std::vector<RuleDev> rd;
@@ -553,7 +675,7 @@ Engine::~Engine() {
   Impl& m = *impl_;
   hipSetDevice(device_);
   void* ps[] = {m.scan_next, m.scan_cls, m.out_meta, m.out_list, m.anchors, m.rules, m.rule_kw, m.vdfa,
-                m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw, m.d_hits, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
+                m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw, m.d_hits, m.d_bh, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& ev : m.ev) if (ev) hipEventDestroy(ev);
   if (m.stream) hipStreamDestroy(m.stream);
@@ -569,6 +691,7 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
   }
   st->bytes = total;
   st->files = in.nfiles;
+  const uint32_t kChunk = m.chunk;
   st->chunk_bytes = kChunk;
   const uint8_t* d_data = static_cast<const uint8_t*>(in.d_data);
   auto t_h2d = std::chrono::steady_clock::now();
@@ -587,7 +710,9 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
   if (!ensure(&m.d_kw, &m.d_kw_cap, kw_n, err)) return false;
   const unsigned long long nchunks = (total + kChunk - 1) / kChunk;
   if (!ensure(&m.d_nl, &m.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
+  m.hit_cap = std::max<size_t>(m.hit_cap, total / 256);   // ~1 hit per 670 B on source text
   if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
+  if (!ensure(&m.d_bh, &m.d_bh_cap, 2ull * std::max(m.sms, 1), err)) return false;
   if (!ensure(&m.d_ff, &m.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
   HIP_OK(hipStreamSynchronize(m.stream));
   st->h2d_ms = in.d_data ? 0.0 : ms_since(t_h2d);
@@ -598,59 +723,64 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
     HIP_OK(hipMemsetAsync(m.d_kw, 0, kw_n * sizeof(uint32_t), m.stream));
     HIP_OK(hipMemsetAsync(m.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), m.stream));
     HIP_OK(hipMemsetAsync(m.d_cnt, 0, 64, m.stream));
-    uint64_t want_blocks = (nchunks + kBlock - 1) / kBlock;
-    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * 2ull)));
+    const int ks = m.k1_streams;
+    const uint32_t nthr = m.k1_threads;
+    const uint64_t want_blocks = (nchunks + static_cast<uint64_t>(nthr) * ks - 1) / (static_cast<uint64_t>(nthr) * ks);
+    // one resident workgroup per CU (the LDS table takes most of the CU's
+    // 160 KiB): a grid of exactly one workgroup per CU, grid-stride
+    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, m.table_in_lds ? sms : sms * 2ull)));
     const uint32_t warm = pf.scan.max_pattern_bytes > 0 ? pf.scan.max_pattern_bytes - 1 : 0;
-    const size_t lds = kHitBuf * 8 + 16 + (m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 + m.meta_bytes : 0);
-    if (m.table_in_lds) {
-      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tsg_k1_scan<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    } else {
-      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tsg_k1_scan<false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    }
+    const uint32_t warm_lines = (warm + 127) / 128;   // warm-up = whole 128-byte lines before the chunk
+    const size_t lds = (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 +
+                       (m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 + m.meta_bytes : 0);
+    const void* kfn = k1_kernel(m.table_in_lds, nthr, ks);
+    if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
+    HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
     st->k1_blocks = blocks;
-    st->k1_threads = kBlock;
+    st->k1_threads = nthr;
     st->table_in_lds = m.table_in_lds;
+    uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(m.hit_cap / blocks, 0xffffffffu));
+    HIP_OK(hipMemsetAsync(m.d_bh, 0, blocks * sizeof(uint32_t), m.stream));
     HIP_OK(hipEventRecord(m.ev[0], m.stream));
     if (nchunks > 0) {
-      if (m.table_in_lds) {
-        hipLaunchKernelGGL(tsg_k1_scan<true>, dim3(blocks), dim3(kBlock), lds, m.stream,
-                           d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
-                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state * m.scan_stride,
-                           m.out_meta, m.nmeta, m.out_list, m.nlist, pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
-                           static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
-      } else {
-        hipLaunchKernelGGL(tsg_k1_scan<false>, dim3(blocks), dim3(kBlock), lds, m.stream,
-                           d_data, (unsigned long long)total, m.d_off, in.nfiles, m.scan_next, m.scan_cls,
-                           pf.scan.t.nclasses, m.table_words16, pf.scan.first_out_state * m.scan_stride,
-                           m.out_meta, m.nmeta, m.out_list, m.nlist, pf.nkw, warm, nchunks, m.d_kw, m.kw_words, m.d_hits, m.d_cnt,
-                           static_cast<uint32_t>(m.hit_cap), m.d_nl, m.d_ff);
-      }
-      HIP_OK(hipGetLastError());
+      unsigned long long a_total = total;
+      uint32_t a_nfiles = in.nfiles, a_ncls = pf.scan.t.nclasses, a_tw = m.table_words16;
+      uint32_t a_first = pf.scan.first_out_state * m.scan_stride, a_nmeta = m.nmeta, a_nlist = m.nlist, a_nkw = pf.nkw;
+      unsigned long long a_nchunks = nchunks;
+      uint32_t a_chunk = kChunk;
+      uint32_t a_kww = m.kw_words;
+      const uint8_t* a_data = d_data;
+      void* args[] = {&a_data, &a_total, &m.d_off, &a_nfiles, &m.scan_next, &m.scan_cls, &a_ncls, &a_tw, &a_first,
+                      &m.out_meta, &a_nmeta, &m.out_list, &a_nlist, &a_nkw, const_cast<uint32_t*>(&warm_lines), &a_chunk, &a_nchunks,
+                      &m.d_kw, &a_kww, &m.d_hits, &m.d_bh, &region_cap, &m.d_nl, &m.d_ff};
+      HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, m.stream));
     }
     HIP_OK(hipEventRecord(m.ev[1], m.stream));
-    unsigned int cnt[2] = {0, 0};
-    HIP_OK(hipMemcpyAsync(cnt, m.d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, m.stream));
+    m.h_bh.resize(blocks);
+    HIP_OK(hipMemcpyAsync(m.h_bh.data(), m.d_bh, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
     HIP_OK(hipStreamSynchronize(m.stream));
     float k1 = 0;
     HIP_OK(hipEventElapsedTime(&k1, m.ev[0], m.ev[1]));
     st->k1_ms += k1;
-    if (cnt[0] > m.hit_cap) {                          // hit buffer overflow: grow, rerun K1
-      m.hit_cap = static_cast<size_t>(cnt[0]) * 5 / 4 + 1024;
+    uint64_t nhits = 0;
+    uint32_t maxr = 0;
+    for (uint32_t b : m.h_bh) { nhits += b; maxr = std::max(maxr, b); }
+    if (maxr > region_cap) {                           // a workgroup's region overflowed: grow, rerun K1
+      m.hit_cap = static_cast<size_t>(maxr) * 5 / 4 * blocks + 1024;
       if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
       continue;
     }
-    st->hits = cnt[0];
+    st->hits = nhits;
     // K2 (re-run only if the candidate buffer overflows)
     for (int a2 = 0; a2 < 3; ++a2) {
       if (!ensure(&m.d_cands, &m.d_cands_cap, m.cand_cap, err)) return false;
       HIP_OK(hipMemsetAsync(m.d_cnt + 1, 0, 4, m.stream));
       HIP_OK(hipEventRecord(m.ev[2], m.stream));
-      if (cnt[0] > 0) {
-        uint32_t b2 = static_cast<uint32_t>(std::min<uint64_t>((cnt[0] + 255) / 256, sms * 16ull));
-        hipLaunchKernelGGL(tsg_k2_verify, dim3(b2), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles, m.d_hits,
-                           cnt[0], m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
+      if (nhits > 0) {
+        // (region, sub-block) grid: enough sub-blocks that the fullest region is done in ~4 strides
+        const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(64, (maxr + 1023) / 1024)));
+        hipLaunchKernelGGL(tsg_k2_verify, dim3(blocks * nsub), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles,
+                           m.d_hits, m.d_bh, region_cap, blocks, m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
                            m.v_cls, m.d_cands, m.d_cnt, static_cast<uint32_t>(m.cand_cap));
         HIP_OK(hipGetLastError());
       }
@@ -803,7 +933,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       nls.chunk_nl = m.h_nl.data();
       nls.data = in.h_data;
       nls.file_off = in.offsets[f];
-      nls.chunk = kChunk;
+      nls.chunk = m.chunk;
       Secret s = scan_file(rs, path, content, len, binary, &plan, &nls);
       nfind.fetch_add(s.findings.size());
       (*results)[f] = std::move(s);
