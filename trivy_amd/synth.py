@@ -430,3 +430,135 @@ def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4,
                 p = fo + rng.randrange(fs)
                 data[p] = rng.choice((0x80, 0xC3, 0xE2, 0xFF, 0xED))
     return Corpus(data, offsets, paths, planted, nmiss)
+
+
+# ------------------------------------------------------------ config 5
+EXCLUDE_BLOCKS = [
+    r"--- ignore block start ---(.|\s)*--- ignore block stop ---",   # scanner_test exclude-block.yaml
+    r"(?s)BEGIN NOSCAN.*?END NOSCAN",
+    r"#\s*nosec-block-\d+[^\n]*",
+    r"<<<SKIP>>>[^<]*<<<ENDSKIP>>>",
+    r"(?m)^# vault: .*$",
+]
+
+
+def _vendor_names(n, rng):
+    cons, vows = "bcdfghjklmnprstvwxz", "aeiou"
+    out, seen = [], set()
+    while len(out) < n:
+        k = rng.randint(3, 5)
+        v = "".join(rng.choice(cons) + rng.choice(vows) for _ in range(k))[:rng.randint(5, 9)]
+        if v in seen or "example" in v:
+            continue
+        seen.add(v)
+        out.append(v)
+    return out
+
+
+def config5(n_rules=500, seed=DEFAULT_SEED, n_allow=20):
+    """trivy-secret.yaml of BASELINE.json configs[4]:
+    n_rules custom rules from the builtin templates (vendor key=value form and
+    prefix-token form), 10% without keywords, severities needing
+    normalisation, some per-rule allow-rules / exclude-blocks / paths; plus
+    n_allow global allow rules (path and regex) and 5 global exclude blocks.
+    Builtins stay enabled.  Returns (config dict in the YAML schema of
+    scanner.go:29-43, plant descriptors for plant_custom)."""
+    rng = random.Random(seed ^ 0xC0F5)
+    names = _vendor_names(n_rules, rng)
+    sev = ["HIGH", "critical", "Medium", "low", "UNKNOWN", "severe", ""]
+    rules, plants = [], []
+    for i, v in enumerate(names):
+        n = rng.randint(16, 40)
+        r = {"id": "custom-%s" % v, "category": "Custom%d" % (i % 7), "title": "%s secret" % v.capitalize(),
+             "severity": rng.choice(sev)}
+        if i % 10 < 6:
+            r["regex"] = (r"(?i)(?P<key>%s[a-z0-9_ .\-,]{0,25})(=|>|:=|\|\|:|<=|=>|:).{0,5}['\"]"
+                          r"(?P<secret>[a-z0-9]{%d})['\"]" % (v, n))
+            r["secret-group-name"] = "secret"
+            kind = "kv"
+        else:
+            p = v[:4] + "_" + rng.choice(("pat", "tok", "live", "sk"))
+            if i % 3 == 0:
+                r["regex"] = r"(^|[^0-9a-zA-Z])(?P<secret>%s_[A-Za-z0-9]{%d})($|[^0-9a-zA-Z])" % (p, n)
+                r["secret-group-name"] = "secret"
+            else:
+                r["regex"] = r"%s_[A-Za-z0-9]{%d}" % (p, n)
+            kind = "tok"
+            v = p
+        if i % 10 != 9:                                  # 10% have no keywords: gate always true
+            r["keywords"] = [v if i % 4 else v.upper()]
+        if i % 25 == 3:
+            r["allow-rules"] = [{"id": "allow-%d" % i, "description": "dummy values", "regex": "(?i)dummy"}]
+        if i % 40 == 5:
+            r["exclude-block"] = {"description": "rule block", "regexes": [r"(?s)<%s-ignore>.*?</%s-ignore>" % (v, v)]}
+        if i % 50 == 7:
+            r["path"] = r"\.(env|conf|ini|yaml)$"
+        rules.append(r)
+        plants.append((kind, v, n))
+    allow = []
+    for k in range(n_allow):
+        if k % 2 == 0:
+            allow.append({"id": "global-path-%d" % k, "description": "fixture dirs", "path": r"/fixtures_%d/" % k})
+        else:
+            allow.append({"id": "global-rx-%d" % k, "description": "placeholders", "regex": r"(?i)notasecret%02d" % k})
+    cfg = {"rules": rules, "allow-rules": allow,
+           "exclude-block": {"description": "global exclude blocks", "regexes": list(EXCLUDE_BLOCKS)}}
+    return cfg, plants
+
+
+def plant_custom(corpus, plants, seed=DEFAULT_SEED, rate=1e-4):
+    """Overwrite whole lines of `corpus` (in place) with strings matching the
+    config5() rules, some inside exclude blocks or carrying allow-rule text;
+    moves ~1% of files under allow-listed fixtures_k/ dirs and ~2% to .env."""
+    rng = random.Random(seed ^ 0x9A47)
+    n = len(corpus.paths)
+    alnum_lo = "abcdefghijklmnopqrstuvwxyz0123456789"
+    alnum = alnum_lo + "ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+    n_plants = max(1, int(corpus.nbytes / 40 * rate))
+    placed = 0
+    for _ in range(n_plants):
+        kind, v, nlen = plants[rng.randrange(len(plants))]
+        if kind == "kv":
+            name = "".join(c.upper() if rng.random() < 0.3 else c for c in v)
+            sec = "".join(rng.choice(alnum_lo) for _ in range(nlen))
+            op = rng.choice(("=", ": ", ":=", "=>", None))
+            if op is None:
+                s = '%s_api_key = "%s"' % (name, sec)
+            else:
+                s = "%s%s%s'%s'" % (name, rng.choice(("_key", "_token", " secret", "")), op, sec)
+        else:
+            s = "%s_%s" % (v, "".join(rng.choice(alnum) for _ in range(nlen)))
+        r = rng.random()
+        if r < 0.05:
+            s = s + " # dummy"                                   # per-rule allow (some rules)
+        elif r < 0.10:
+            s = s + " notasecret%02d" % rng.choice((1, 3, 5))   # global allow regex
+        elif r < 0.15:
+            s = "--- ignore block start ---\n%s\n--- ignore block stop ---" % s
+        elif r < 0.18:
+            s = "BEGIN NOSCAN %s END NOSCAN" % s
+        elif r < 0.20:
+            s = "<%s-ignore>\n%s\n</%s-ignore>" % (v, s, v)
+        elif r < 0.22:
+            s = "# vault: " + s
+        line = ("\n" + s + "\n").encode()
+        f = rng.randrange(n)
+        fo, fs = int(corpus.offsets[f]), int(corpus.offsets[f + 1] - corpus.offsets[f])
+        if len(line) >= fs:
+            continue
+        p = fo + rng.randrange(fs - len(line) + 1)
+        corpus.data[p:p + len(line)] = np.frombuffer(line, dtype=np.uint8)
+        placed += 1
+    for f in range(n):
+        r = rng.random()
+        if r < 0.01:
+            corpus.paths[f] = "repo/fixtures_%d/%s" % (2 * rng.randrange(10), corpus.paths[f])
+        elif r < 0.03:
+            corpus.paths[f] = corpus.paths[f].rsplit(".", 1)[0] + ".env"
+    return placed
+
+
+def write_yaml(cfg, path):
+    import yaml
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f, sort_keys=False, allow_unicode=False, width=1 << 20)
