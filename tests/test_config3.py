@@ -1,0 +1,56 @@
+"""Config 3 (BASELINE.json configs[2]): extracted container-image layers --
+many small files, rootfs paths (some under the builtin allow-paths, half with
+the "/" prefix image scans add), empty files in the batch.  Stresses the
+offset table, per-file keyword bits and host path gating.
+
+CPU: oracle == C++ confirmer == CPU model of the GPU tables.
+GPU: ~100k files in one batch; the HIP path equals the C++ exact confirmer on
+every file (the confirmer is pinned to the oracle by the CPU tests) and the
+oracle on a sample."""
+import random
+
+import pytest
+
+from oracle import secret_oracle as so
+from trivy_amd import secret as S
+from trivy_amd import synth
+
+
+def _args(nbytes, seed, sizes):
+    c = synth.generate(nbytes, seed=seed, sizes=sizes, plant_rate=2e-3, base_bytes=1 << 20, layout="image")
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    rng = random.Random(seed)
+    for k in range(0, len(args), max(1, len(args) // 20)):      # empty files scattered through the batch
+        args.insert(k, S.ScanArgs("/etc/empty_%d.conf" % k, b""))
+    rng.shuffle(args)
+    return args
+
+
+@pytest.mark.parametrize("seed,sizes", [(31, "small"), (32, "tiny")])
+def test_config3_parity_cpu(seed, sizes):
+    args = _args(500_000, seed, sizes)
+    ref = so.Scanner(None)
+    want = [ref.scan(a.FilePath, a.Content) for a in args]
+    sc = S.Scanner(None)
+    host = S.scan_host_reference(sc, args, threads=4)
+    model = S.scan_table_model(sc, args)
+    assert sum(len(w["Findings"]) for w in want) > 5
+    assert sum(1 for w in want if w["FilePath"] and not w["Findings"]) > 0     # path-allowed files
+    for i, a in enumerate(args):
+        assert host[i] == want[i], a.FilePath
+        assert model[i] == want[i], a.FilePath
+
+
+@pytest.mark.gpu
+def test_config3_many_files_gpu():
+    args = _args(30_000_000, 33, "tiny")
+    assert len(args) > 50_000
+    sc = S.Scanner(None)
+    got = sc.ScanBatch(args)
+    host = S.scan_host_reference(sc, args, threads=16)
+    assert sum(len(h["Findings"]) for h in host) > 100
+    for a, g, h in zip(args, got, host):
+        assert g == h, a.FilePath
+    ref = so.Scanner(None)
+    for i in random.Random(3).sample(range(len(args)), 2000):
+        assert got[i] == ref.scan(args[i].FilePath, args[i].Content), args[i].FilePath

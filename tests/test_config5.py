@@ -1,0 +1,65 @@
+"""Config 5 (BASELINE.json configs[4]): a trivy-secret.yaml with 500 custom
+rules (10% without keywords), 20 global allow rules, per-rule allow rules,
+per-rule and global exclude blocks, severities needing normalisation, builtins
+enabled -- 587 rules.  The scan DFA no longer fits one K1 pass, so the
+prefilter splits it into groups (one K1 launch each).
+
+CPU: oracle == C++ confirmer (reference mode) == CPU model of the grouped GPU
+tables, file by file.  GPU: the HIP path == oracle on the same corpus."""
+import os
+
+import pytest
+
+from oracle import secret_oracle as so
+from trivy_amd import secret as S
+from trivy_amd import synth
+
+
+def _setup(tmp_path, nbytes, seed):
+    cfg, plants = synth.config5(500, seed=seed)
+    path = os.path.join(str(tmp_path), "trivy-secret.yaml")
+    synth.write_yaml(cfg, path)
+    c = synth.generate(nbytes, seed=seed, sizes="lognormal", plant_rate=5e-4, base_bytes=1 << 20)
+    placed = synth.plant_custom(c, plants, seed=seed, rate=4e-3)
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    return path, args, placed
+
+
+def _want(path, args):
+    ref = so.Scanner(so.parse_config(path))
+    return [ref.scan(a.FilePath, a.Content) for a in args]
+
+
+def test_config5_groups_compile(tmp_path):
+    path, _, _ = _setup(tmp_path, 50_000, 5)
+    sc = S.Scanner(S.ParseConfig(path))
+    assert len(sc.rule_ids) == 587
+    rep = S.prefilter_report(sc)
+    ngroups = int(rep.splitlines()[1].split()[0])
+    assert ngroups > 1, rep[:400]
+    assert "FULL" not in rep
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_config5_parity_cpu(tmp_path, seed):
+    path, args, placed = _setup(tmp_path, 400_000, seed)
+    assert placed > 20
+    want = _want(path, args)
+    sc = S.Scanner(S.ParseConfig(path))
+    host = S.scan_host_reference(sc, args, threads=4)
+    model = S.scan_table_model(sc, args)
+    ids = {f["RuleID"] for w in want for f in w["Findings"]}
+    assert sum(1 for i in ids if i.startswith("custom-")) > 10
+    for i, a in enumerate(args):
+        assert host[i] == want[i], a.FilePath
+        assert model[i] == want[i], a.FilePath
+
+
+@pytest.mark.gpu
+def test_config5_parity_gpu(tmp_path):
+    path, args, _ = _setup(tmp_path, 1_000_000, 7)
+    want = _want(path, args)
+    got = S.Scanner(S.ParseConfig(path)).ScanBatch(args)
+    assert sum(len(w["Findings"]) for w in want) > 20
+    for a, g, w in zip(args, got, want):
+        assert g == w, a.FilePath

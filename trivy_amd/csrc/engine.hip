@@ -130,7 +130,9 @@ struct K1Ctx {
   const uint32_t* list;
   uint32_t nkw;
   uint32_t* __restrict__ kwbits;
+  uint32_t* __restrict__ kwmask;  // kwbits + kw_base / 32: the register masks' first word
   uint32_t kw_words;
+  bool primary;                   // first scan group: also counts newlines and flags fold-special files
   unsigned long long* __restrict__ hits;   // this workgroup's region of the hit list
   uint32_t region_cap;
   uint32_t* b_hitcnt;           // LDS: fill count of the workgroup's region
@@ -195,12 +197,12 @@ __device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, co
 __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4]) {
   const unsigned long long end = k1_end(x, t);
   unsigned long long fend = x.offsets[t.f + 1];
-  if (((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
+  if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
   for (int k = 0; k < 16; ++k) {
     const unsigned long long q = t.p + k;
     if (q >= end) break;
     if (q >= fend) {
-      flush_kw(x.kwbits, x.kw_words, t.f, t.kw0, t.kw1);
+      flush_kw(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
       do { ++t.f; fend = x.offsets[t.f + 1]; } while (q >= fend);
       t.s = 0;
       t.p12 = 0;
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
     const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
     uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
-    uint32_t* __restrict__ kwbits, uint32_t kw_words,
+    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
   x.next = g_next; x.cls = g_cls;
   x.first_out = first_out; x.nclasses = nclasses;
   x.meta = g_meta; x.list = g_list; x.nkw = nkw;
-  x.kwbits = kwbits; x.kw_words = kw_words;
+  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
   x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
   x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
   if (kLds) {
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
 #pragma unroll
             for (int j = 0; j < kS; ++j) {
               const uint32_t w[4] = {line[j][i].x, line[j][i].y, line[j][i].z, line[j][i].w};
-              if (((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && S[j].p >= S[j].emit)
+              if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && S[j].p >= S[j].emit)
                 k1_special(x, S[j], w, ~0ull, ~0ull);
 #pragma unroll
               for (int k = 0; k < 16; ++k) cl[j][k] = x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
@@ -395,8 +397,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
       for (int j = 0; j < kS; ++j) {
         const unsigned long long c = wi * kS + j;
         if (c < nchunks) {
-          flush_kw(kwbits, kw_words, S[j].f, S[j].kw0, S[j].kw1);
-          nl_count[c] = S[j].nl;
+          flush_kw(x.kwmask, kw_words, S[j].f, S[j].kw0, S[j].kw1);
+          if (x.primary) nl_count[c] = S[j].nl;
         }
       }
     }
@@ -515,15 +517,23 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 }  // namespace
 
+// Device tables of one scan DFA group (one K1 launch per group).
+struct K1Group {
+  uint16_t* next = nullptr;    // pre-multiplied uint16 row offsets, row stride `stride`
+  uint8_t* cls = nullptr;      // byte -> class * 2
+  OutMeta* meta = nullptr;
+  uint32_t* list = nullptr;
+  uint32_t nmeta = 0, nlist = 0, table_words16 = 0, stride = 0, nclasses = 0, first_out = 0;
+  uint32_t kw_base = 0, warm_lines = 0;
+  size_t meta_bytes = 0;
+  bool in_lds = false;
+};
+
 struct Engine::Impl {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   // tables
-  uint16_t* scan_next = nullptr;
-  uint8_t* scan_cls = nullptr;
-  OutMeta* out_meta = nullptr;
-  uint32_t* out_list = nullptr;
-  uint32_t nmeta = 0, nlist = 0;
+  std::vector<K1Group> k1g;
   AnchorDev* anchors = nullptr;
   RuleDev* rules = nullptr;
   uint32_t* rule_kw = nullptr;
@@ -531,10 +541,6 @@ struct Engine::Impl {
   uint16_t* v_next = nullptr;
   uint8_t* v_acc = nullptr;
   uint8_t* v_cls = nullptr;
-  uint32_t table_words16 = 0;
-  uint32_t scan_stride = 0;
-  size_t meta_bytes = 0;
-  bool table_in_lds = false;
   uint32_t kw_words = 1;
   // batch buffers
   uint8_t* d_data = nullptr; size_t d_data_cap = 0;
@@ -593,52 +599,65 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess) { *err = "hipStreamCreate failed"; return nullptr; }
   for (auto& ev : m.ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
   const Prefilter& pf = e->pf_;
-  // scan table with an odd dword row stride: next[s*stride + c] then spreads
-  // the same class of different states over different LDS banks (a 64-class
-  // row is 32 dwords, which would put every state's class c in one bank)
-  const uint32_t C = pf.scan.t.nclasses;
-  uint32_t stride = (C + 2) & ~1u;            // >= C+1: slot C holds the output-state index
-  if (((stride / 2) & 1u) == 0) stride += 2;
-  m.scan_stride = stride;
-  std::vector<uint16_t> sn(static_cast<size_t>(pf.scan.t.nstates) * stride, 0);
-  // entries hold the next state's row offset (state * stride): the DFA chain
-  // is then one add + one LDS read per byte (no multiply)
-  if (static_cast<uint64_t>(pf.scan.t.nstates) * stride > 65535) {
-    *err = "scan DFA too large for 16-bit pre-multiplied offsets";
-    return nullptr;
-  }
-  for (uint32_t st = 0; st < pf.scan.t.nstates; ++st) {
-    for (uint32_t c = 0; c < C; ++c)
-      sn[static_cast<size_t>(st) * stride + c] = static_cast<uint16_t>(pf.scan.t.next[static_cast<size_t>(st) * C + c] * stride);
-    if (st >= pf.scan.first_out_state) sn[static_cast<size_t>(st) * stride + C] = static_cast<uint16_t>(st - pf.scan.first_out_state);
-  }
-  // per output state: keyword masks (ids < 128) + list of other output ids
-  std::vector<OutMeta> meta;
-  std::vector<uint32_t> olist;
-  for (uint32_t o = 0; o + 1 < pf.scan.out_off.size(); ++o) {
-    OutMeta om{0, 0, static_cast<uint32_t>(olist.size()), 0};
-    for (uint32_t k = pf.scan.out_off[o]; k < pf.scan.out_off[o + 1]; ++k) {
-      const uint32_t id = pf.scan.out_ids[k];
-      if (id < pf.nkw && id < 64) om.kw0 |= 1ull << id;
-      else if (id < pf.nkw && id < 128) om.kw1 |= 1ull << (id - 64);
-      else olist.push_back(id);
-    }
-    om.list_count = static_cast<uint32_t>(olist.size()) - om.list_begin;
-    meta.push_back(om);
-  }
-  m.nmeta = static_cast<uint32_t>(meta.size());
-  m.nlist = static_cast<uint32_t>(olist.size());
-  m.meta_bytes = ((meta.size() * sizeof(OutMeta) + olist.size() * 4) + 15) & ~size_t(15);
-  m.table_words16 = static_cast<uint32_t>(sn.size());
-  // LDS: per-wave hit buffers (16 waves) + scan table + class map + output metadata
-  m.table_in_lds = kMaxWaves * kWaveHits * 4 + kMaxWaves * 4 + static_cast<size_t>(m.table_words16) * 2 + 16 + 256 +
-                   m.meta_bytes <= kLdsBytes;
   if (pf.anchors.size() >= (1u << kAnchorBits)) { *err = "too many anchor literals for K1's hit encoding"; return nullptr; }
-  sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
-  // K1's class map holds class * 2 (see k1_step)
-  if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return nullptr; }
-  std::vector<uint8_t> cls(256);
-  for (int b = 0; b < 256; ++b) cls[b] = static_cast<uint8_t>(pf.scan.t.byte_class[b] * 2);
+  m.kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
+  for (const ScanDfa& sd : pf.groups) {
+    K1Group g;
+    // scan table with an odd dword row stride: next[s*stride + c] then spreads
+    // the same class of different states over different LDS banks (a 64-class
+    // row is 32 dwords, which would put every state's class c in one bank)
+    const uint32_t C = sd.t.nclasses;
+    const uint32_t stride = k1_row_stride(C);   // slot C holds the output-state index
+    g.stride = stride;
+    g.nclasses = C;
+    g.first_out = sd.first_out_state * stride;
+    g.kw_base = sd.kw_base;
+    const uint32_t warm = sd.max_pattern_bytes > 0 ? sd.max_pattern_bytes - 1 : 0;
+    g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk
+    // entries hold the next state's row offset (state * stride): the DFA chain
+    // is then one add + one LDS read per byte (no multiply)
+    if (static_cast<uint64_t>(sd.t.nstates) * stride > 65535) {
+      *err = "scan DFA group too large for 16-bit pre-multiplied offsets";
+      return nullptr;
+    }
+    if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return nullptr; }
+    std::vector<uint16_t> sn(static_cast<size_t>(sd.t.nstates) * stride, 0);
+    for (uint32_t st = 0; st < sd.t.nstates; ++st) {
+      for (uint32_t c = 0; c < C; ++c)
+        sn[static_cast<size_t>(st) * stride + c] = static_cast<uint16_t>(sd.t.next[static_cast<size_t>(st) * C + c] * stride);
+      if (st >= sd.first_out_state) sn[static_cast<size_t>(st) * stride + C] = static_cast<uint16_t>(st - sd.first_out_state);
+    }
+    // per output state: keyword masks (ids kw_base .. kw_base+127) + list of other output ids
+    std::vector<OutMeta> meta;
+    std::vector<uint32_t> olist;
+    for (uint32_t o = 0; o + 1 < sd.out_off.size(); ++o) {
+      OutMeta om{0, 0, static_cast<uint32_t>(olist.size()), 0};
+      for (uint32_t k = sd.out_off[o]; k < sd.out_off[o + 1]; ++k) {
+        const uint32_t id = sd.out_ids[k];
+        if (id < pf.nkw && id >= g.kw_base && id < g.kw_base + 64) om.kw0 |= 1ull << (id - g.kw_base);
+        else if (id < pf.nkw && id >= g.kw_base + 64 && id < g.kw_base + 128) om.kw1 |= 1ull << (id - g.kw_base - 64);
+        else olist.push_back(id);
+      }
+      om.list_count = static_cast<uint32_t>(olist.size()) - om.list_begin;
+      meta.push_back(om);
+    }
+    g.nmeta = static_cast<uint32_t>(meta.size());
+    g.nlist = static_cast<uint32_t>(olist.size());
+    g.meta_bytes = ((meta.size() * sizeof(OutMeta) + olist.size() * 4) + 15) & ~size_t(15);
+    g.table_words16 = static_cast<uint32_t>(sn.size());
+    // LDS: per-wave hit buffers (16 waves) + counters + scan table + class map + output metadata
+    g.in_lds = kK1HitLdsBytes + ((static_cast<size_t>(g.table_words16) * 2 + 15) & ~size_t(15)) + 256 + g.meta_bytes <= kLdsBytes;
+    sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
+    // K1's class map holds class * 2 (see k1_step)
+    std::vector<uint8_t> cls(256);
+    for (int b = 0; b < 256; ++b) cls[b] = static_cast<uint8_t>(sd.t.byte_class[b] * 2);
+    if (!dev_upload(sn, &g.next, err) || !dev_upload(cls, &g.cls, err) || !dev_upload(meta, &g.meta, err) ||
+        !dev_upload(olist, &g.list, err)) {
+      return nullptr;
+    }
+    m.kw_words = std::max<uint32_t>(m.kw_words, g.kw_base / 32 + 4);   // a group's masks span 4 words from kw_base
+    m.k1g.push_back(g);
+  }
   std::vector<AnchorDev> an;
   for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
   std::vector<RuleDev> rd;
@@ -658,10 +677,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
     vc.insert(vc.end(), t.byte_class, t.byte_class + 256);
     vd.push_back(d);
   }
-  m.kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
-  if (!dev_upload(sn, &m.scan_next, err) || !dev_upload(cls, &m.scan_cls, err) ||
-      !dev_upload(meta, &m.out_meta, err) || !dev_upload(olist, &m.out_list, err) ||
-      !dev_upload(an, &m.anchors, err) || !dev_upload(rd, &m.rules, err) ||
+  if (!dev_upload(an, &m.anchors, err) || !dev_upload(rd, &m.rules, err) ||
       !dev_upload(pf.rule_kw, &m.rule_kw, err) || !dev_upload(vd, &m.vdfa, err) ||
       !dev_upload(vn, &m.v_next, err) || !dev_upload(va, &m.v_acc, err) || !dev_upload(vc, &m.v_cls, err)) {
     return nullptr;
@@ -674,9 +690,13 @@ Engine::~Engine() {
   if (!impl_) return;
   Impl& m = *impl_;
   hipSetDevice(device_);
-  void* ps[] = {m.scan_next, m.scan_cls, m.out_meta, m.out_list, m.anchors, m.rules, m.rule_kw, m.vdfa,
-                m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw, m.d_hits, m.d_bh, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
+  void* ps[] = {m.anchors, m.rules, m.rule_kw, m.vdfa, m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw,
+                m.d_hits, m.d_bh, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
   for (void* p : ps) if (p) hipFree(p);
+  for (K1Group& g : m.k1g) {
+    void* gs[] = {g.next, g.cls, g.meta, g.list};
+    for (void* p : gs) if (p) hipFree(p);
+  }
   for (auto& ev : m.ev) if (ev) hipEventDestroy(ev);
   if (m.stream) hipStreamDestroy(m.stream);
 }
@@ -712,7 +732,8 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
   if (!ensure(&m.d_nl, &m.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
   m.hit_cap = std::max<size_t>(m.hit_cap, total / 256);   // ~1 hit per 670 B on source text
   if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
-  if (!ensure(&m.d_bh, &m.d_bh_cap, 2ull * std::max(m.sms, 1), err)) return false;
+  const uint32_t ngroups = static_cast<uint32_t>(m.k1g.size());
+  if (!ensure(&m.d_bh, &m.d_bh_cap, 2ull * std::max(m.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
   if (!ensure(&m.d_ff, &m.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
   HIP_OK(hipStreamSynchronize(m.stream));
   st->h2d_ms = in.d_data ? 0.0 : ms_since(t_h2d);
@@ -728,36 +749,45 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
     const uint64_t want_blocks = (nchunks + static_cast<uint64_t>(nthr) * ks - 1) / (static_cast<uint64_t>(nthr) * ks);
     // one resident workgroup per CU (the LDS table takes most of the CU's
     // 160 KiB): a grid of exactly one workgroup per CU, grid-stride
-    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, m.table_in_lds ? sms : sms * 2ull)));
-    const uint32_t warm = pf.scan.max_pattern_bytes > 0 ? pf.scan.max_pattern_bytes - 1 : 0;
-    const uint32_t warm_lines = (warm + 127) / 128;   // warm-up = whole 128-byte lines before the chunk
-    const size_t lds = (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 +
-                       (m.table_in_lds ? ((m.table_words16 * 2 + 15) & ~15u) + 256 + m.meta_bytes : 0);
-    const void* kfn = k1_kernel(m.table_in_lds, nthr, ks);
-    if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
-    HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    bool all_lds = true;
+    for (const K1Group& g : m.k1g) all_lds &= g.in_lds;
+    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, all_lds ? sms : sms * 2ull)));
     st->k1_blocks = blocks;
     st->k1_threads = nthr;
-    st->table_in_lds = m.table_in_lds;
-    uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(m.hit_cap / blocks, 0xffffffffu));
-    HIP_OK(hipMemsetAsync(m.d_bh, 0, blocks * sizeof(uint32_t), m.stream));
+    st->table_in_lds = all_lds;
+    // one hit region per (group, workgroup); K2 walks all of them
+    const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
+    uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(m.hit_cap / nregions, 0xffffffffu));
+    HIP_OK(hipMemsetAsync(m.d_bh, 0, nregions * sizeof(uint32_t), m.stream));
     HIP_OK(hipEventRecord(m.ev[0], m.stream));
-    if (nchunks > 0) {
+    for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
+      const K1Group& g = m.k1g[gi];
+      const size_t lds = (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 + (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
+      const void* kfn = k1_kernel(g.in_lds, nthr, ks);
+      if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
+      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
       unsigned long long a_total = total;
-      uint32_t a_nfiles = in.nfiles, a_ncls = pf.scan.t.nclasses, a_tw = m.table_words16;
-      uint32_t a_first = pf.scan.first_out_state * m.scan_stride, a_nmeta = m.nmeta, a_nlist = m.nlist, a_nkw = pf.nkw;
+      uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
+      uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
+      uint32_t a_warm = g.warm_lines;
       unsigned long long a_nchunks = nchunks;
       uint32_t a_chunk = kChunk;
-      uint32_t a_kww = m.kw_words;
+      uint32_t a_kww = m.kw_words, a_kwbase = g.kw_base, a_primary = gi == 0;
       const uint8_t* a_data = d_data;
-      void* args[] = {&a_data, &a_total, &m.d_off, &a_nfiles, &m.scan_next, &m.scan_cls, &a_ncls, &a_tw, &a_first,
-                      &m.out_meta, &a_nmeta, &m.out_list, &a_nlist, &a_nkw, const_cast<uint32_t*>(&warm_lines), &a_chunk, &a_nchunks,
-                      &m.d_kw, &a_kww, &m.d_hits, &m.d_bh, &region_cap, &m.d_nl, &m.d_ff};
+      unsigned long long* a_hits = m.d_hits + static_cast<size_t>(gi) * blocks * region_cap;
+      uint32_t* a_bh = m.d_bh + static_cast<size_t>(gi) * blocks;
+      uint16_t* a_next = g.next;
+      uint8_t* a_cls = g.cls;
+      OutMeta* a_meta = g.meta;
+      uint32_t* a_list = g.list;
+      void* args[] = {&a_data, &a_total, &m.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
+                      &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
+                      &m.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &region_cap, &m.d_nl, &m.d_ff};
       HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, m.stream));
     }
     HIP_OK(hipEventRecord(m.ev[1], m.stream));
-    m.h_bh.resize(blocks);
-    HIP_OK(hipMemcpyAsync(m.h_bh.data(), m.d_bh, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+    m.h_bh.resize(nregions);
+    HIP_OK(hipMemcpyAsync(m.h_bh.data(), m.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
     HIP_OK(hipStreamSynchronize(m.stream));
     float k1 = 0;
     HIP_OK(hipEventElapsedTime(&k1, m.ev[0], m.ev[1]));
@@ -766,7 +796,7 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
     uint32_t maxr = 0;
     for (uint32_t b : m.h_bh) { nhits += b; maxr = std::max(maxr, b); }
     if (maxr > region_cap) {                           // a workgroup's region overflowed: grow, rerun K1
-      m.hit_cap = static_cast<size_t>(maxr) * 5 / 4 * blocks + 1024;
+      m.hit_cap = static_cast<size_t>(maxr) * 5 / 4 * nregions + 1024;
       if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
       continue;
     }
@@ -779,8 +809,8 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
       if (nhits > 0) {
         // (region, sub-block) grid: enough sub-blocks that the fullest region is done in ~4 strides
         const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(64, (maxr + 1023) / 1024)));
-        hipLaunchKernelGGL(tsg_k2_verify, dim3(blocks * nsub), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles,
-                           m.d_hits, m.d_bh, region_cap, blocks, m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
+        hipLaunchKernelGGL(tsg_k2_verify, dim3(nregions * nsub), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles,
+                           m.d_hits, m.d_bh, region_cap, nregions, m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
                            m.v_cls, m.d_cands, m.d_cnt, static_cast<uint32_t>(m.cand_cap));
         HIP_OK(hipGetLastError());
       }

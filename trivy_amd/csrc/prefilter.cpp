@@ -667,21 +667,25 @@ bool make_scan_dfa(const Nfa& nfa, int s0, uint32_t maxb, ScanDfa* out, std::str
   return true;
 }
 
-// The two passes on the host over one file with a given scan DFA.
-void two_pass(const Prefilter& pf, const ScanDfa& sd, const std::vector<AnchorInfo>& anchors,
+// The two passes on the host over one file with the given scan DFAs (K1 runs
+// each group's DFA over the whole batch; outputs are unioned).
+void two_pass(const Prefilter& pf, const ScanDfa* dfas, size_t ndfa, const std::vector<AnchorInfo>& anchors,
               const uint8_t* data, size_t len, std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
-  const DfaTable& t = sd.t;
   std::vector<uint8_t> kwbit(pf.nkw, 0);
   struct Hit { uint64_t end; uint32_t anchor; };
   std::vector<Hit> hits;
-  uint32_t s = 0;
-  for (size_t p = 0; p < len; ++p) {
-    s = t.next[static_cast<size_t>(s) * t.nclasses + t.byte_class[data[p]]];
-    if (s >= sd.first_out_state) {
-      uint32_t o = s - sd.first_out_state;
-      for (uint32_t k = sd.out_off[o]; k < sd.out_off[o + 1]; ++k) {
-        uint32_t id = sd.out_ids[k];
-        if (id < pf.nkw) kwbit[id] = 1; else hits.push_back({p, id - pf.nkw});
+  for (size_t g = 0; g < ndfa; ++g) {
+    const ScanDfa& sd = dfas[g];
+    const DfaTable& t = sd.t;
+    uint32_t s = 0;
+    for (size_t p = 0; p < len; ++p) {
+      s = t.next[static_cast<size_t>(s) * t.nclasses + t.byte_class[data[p]]];
+      if (s >= sd.first_out_state) {
+        uint32_t o = s - sd.first_out_state;
+        for (uint32_t k = sd.out_off[o]; k < sd.out_off[o + 1]; ++k) {
+          uint32_t id = sd.out_ids[k];
+          if (id < pf.nkw) kwbit[id] = 1; else hits.push_back({p, id - pf.nkw});
+        }
       }
     }
   }
@@ -720,7 +724,134 @@ void two_pass(const Prefilter& pf, const ScanDfa& sd, const std::vector<AnchorIn
   }
 }
 
+// ------------------------------------------------------ K1 scan groups
+struct Pattern {
+  Seq seq;          // scan form (ASCII units, case-folded)
+  uint32_t id;      // output id: keyword (< nkw) or nkw + anchor
+};
+
+// Sort key: the lowered first alternative of every unit, so patterns that
+// share a prefix (a vendor keyword and the same rule's anchor) sit together
+// and share trie states inside a group.
+std::string pattern_key(const Seq& s) {
+  std::string k;
+  for (const auto& u : s) k.push_back(static_cast<char>(tolower(static_cast<unsigned char>(u.front().front()))));
+  return k;
+}
+
+bool build_group(const std::vector<Pattern>& ps, ScanDfa* out, std::string* err) {
+  Nfa nfa;
+  int s0 = nfa.add();
+  uint32_t maxb = 1;
+  for (const auto& p : ps) maxb = std::max(maxb, add_seq(&nfa, s0, p.seq, static_cast<int>(p.id)));
+  if (!make_scan_dfa(nfa, s0, maxb, out, err)) return false;
+  out->npatterns = static_cast<uint32_t>(ps.size());
+  return true;
+}
+
+// One group when everything fits K1 (the builtin rules); otherwise sorted
+// patterns are packed into runs of ~kGroupTrieNodes estimated trie nodes, and
+// a run whose DFA still does not fit is halved until it does.
+bool make_groups(Prefilter* pf, std::vector<Pattern> pats, std::string* err) {
+  constexpr uint32_t kGroupTrieNodes = 660;
+  pf->groups.clear();
+  std::string e;
+  {
+    ScanDfa all;
+    if (build_group(pats, &all, &e) && k1_fits(all)) {
+      pf->groups.push_back(std::move(all));
+      return true;
+    }
+  }
+  std::vector<std::string> keys(pats.size());
+  std::vector<size_t> order(pats.size());
+  for (size_t i = 0; i < pats.size(); ++i) { keys[i] = pattern_key(pats[i].seq); order[i] = i; }
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    return keys[a] != keys[b] ? keys[a] < keys[b] : pats[a].id < pats[b].id;
+  });
+  auto lcp_of = [](const std::string& a, const std::string& b) {
+    size_t l = 0;
+    while (l < a.size() && l < b.size() && a[l] == b[l]) ++l;
+    return l;
+  };
+  // balanced runs: as many as the total estimate needs, equal shares
+  uint64_t total = 0;
+  for (size_t j = 0; j < order.size(); ++j)
+    total += keys[order[j]].size() - (j ? lcp_of(keys[order[j]], keys[order[j - 1]]) : 0);
+  const uint64_t nruns = std::max<uint64_t>(1, (total + kGroupTrieNodes - 1) / kGroupTrieNodes);
+  const uint64_t share = (total + nruns - 1) / nruns;
+  std::vector<std::vector<Pattern>> runs(1);
+  uint64_t est = 0;
+  std::string prev;
+  for (size_t i : order) {
+    const std::string& k = keys[i];
+    size_t lcp = lcp_of(k, prev);
+    if (est + (k.size() - lcp) > share && !runs.back().empty() && runs.size() < nruns) { runs.emplace_back(); est = 0; lcp = 0; }
+    est += k.size() - lcp;
+    runs.back().push_back(pats[i]);
+    prev = k;
+  }
+  std::vector<std::vector<Pattern>> todo(runs.rbegin(), runs.rend());
+  while (!todo.empty()) {
+    std::vector<Pattern> ps = std::move(todo.back());
+    todo.pop_back();
+    ScanDfa d;
+    e.clear();
+    if (build_group(ps, &d, &e) && k1_fits(d)) { pf->groups.push_back(std::move(d)); continue; }
+    if (ps.size() == 1) { *err = "scan pattern does not fit K1 (" + (e.empty() ? std::string("LDS") : e) + ")"; return false; }
+    const size_t h = ps.size() / 2;
+    todo.emplace_back(ps.begin() + h, ps.end());
+    todo.emplace_back(ps.begin(), ps.begin() + h);
+  }
+  return true;
+}
+
+// Keyword ids are renumbered so that each group's keywords are contiguous:
+// K1 then ORs them into register masks relative to the group's kw_base.
+void renumber_keywords(Prefilter* pf) {
+  std::vector<uint32_t> newid(pf->nkw, 0xffffffffu);
+  uint32_t next = 0;
+  for (auto& g : pf->groups) {
+    std::vector<uint32_t> ids;
+    for (uint32_t id : g.out_ids) if (id < pf->nkw) ids.push_back(id);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    for (uint32_t id : ids) if (newid[id] == 0xffffffffu) newid[id] = next++;
+  }
+  for (uint32_t k = 0; k < pf->nkw; ++k) if (newid[k] == 0xffffffffu) newid[k] = next++;
+  auto remap = [&](std::vector<uint32_t>* v) { for (auto& id : *v) if (id < pf->nkw) id = newid[id]; };
+  for (auto& g : pf->groups) {
+    remap(&g.out_ids);
+    uint32_t lo = 0xffffffffu;
+    for (uint32_t id : g.out_ids) if (id < pf->nkw) lo = std::min(lo, id);
+    g.kw_base = lo == 0xffffffffu ? 0 : (lo & ~31u);
+  }
+  remap(&pf->host_scan.out_ids);
+  remap(&pf->rule_kw);
+  std::vector<std::string> text(pf->nkw);
+  for (uint32_t k = 0; k < pf->nkw; ++k) text[newid[k]] = pf->kw_text[k];
+  pf->kw_text.swap(text);
+}
+
 }  // namespace
+
+uint32_t k1_row_stride(uint32_t nclasses) {
+  uint32_t s = (nclasses + 2) & ~1u;      // >= nclasses + 1: slot nclasses holds the output-state index
+  if (((s / 2) & 1u) == 0) s += 2;        // odd dword stride spreads a class over LDS banks
+  return s;
+}
+
+size_t k1_lds_table_bytes(const ScanDfa& d) {
+  const size_t tab = (static_cast<size_t>(d.t.nstates) * k1_row_stride(d.t.nclasses) * 2 + 15) & ~size_t(15);
+  const size_t nout = d.t.nstates - d.first_out_state;
+  const size_t meta = (nout * 24 + d.out_ids.size() * 4 + 15) & ~size_t(15);   // OutMeta + (at most) every id listed
+  return tab + 256 + meta;
+}
+
+bool k1_fits(const ScanDfa& d) {
+  return static_cast<uint64_t>(d.t.nstates) * k1_row_stride(d.t.nclasses) <= 65535 &&
+         kK1HitLdsBytes + k1_lds_table_bytes(d) <= kK1LdsBytes;
+}
 
 bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
   *pf = Prefilter();
@@ -748,13 +879,14 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
   }
   pf->nkw = static_cast<uint32_t>(pf->kw_text.size());
 
-  // --- scan NFAs (GPU form and host variant form)
-  Nfa scan, host;
-  int s0 = scan.add();
+  // --- scan patterns (GPU form, partitioned into K1 groups below) and the
+  // host variant NFA
+  std::vector<Pattern> pats;
+  Nfa host;
   int h0 = host.add();
   uint32_t maxb = 1, hmaxb = 1;
   for (uint32_t k = 0; k < pf->nkw; ++k) {
-    maxb = std::max(maxb, add_seq(&scan, s0, keyword_seq(pf->kw_text[k], false), static_cast<int>(k)));
+    pats.push_back({keyword_seq(pf->kw_text[k], false), k});
     hmaxb = std::max(hmaxb, add_seq(&host, h0, keyword_seq(pf->kw_text[k], true), static_cast<int>(k)));
   }
   std::string rep;
@@ -784,7 +916,8 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
       a.dmax = ch.dmax;
       uint32_t id = pf->nkw + static_cast<uint32_t>(pf->anchors.size());
       pf->anchors.push_back(a);
-      maxb = std::max(maxb, add_seq(&scan, s0, s, static_cast<int>(id)));
+      pats.push_back({s, id});
+      maxb = std::max(maxb, seq_max_len(s));
       // host variant forms of every raw literal with this scan form
       AnchorInfo ha = a;
       ha.min_len = 0xffffffffu;
@@ -803,14 +936,24 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
            std::to_string(pf->verify.back().nstates) + " states x " + std::to_string(pf->verify.back().nclasses) +
            " classes, limit " + std::to_string(gi.verify_limit) + note + "\n";
   }
-  if (!make_scan_dfa(scan, s0, maxb, &pf->scan, err)) return false;
+  if (!make_groups(pf, pats, err)) return false;
   if (!make_scan_dfa(host, h0, hmaxb, &pf->host_scan, err)) return false;
+  renumber_keywords(pf);
+  std::string grep;
+  for (size_t g = 0; g < pf->groups.size(); ++g) {
+    const ScanDfa& d = pf->groups[g];
+    maxb = std::max(maxb, d.max_pattern_bytes);
+    grep += "scan DFA group " + std::to_string(g) + ": " + std::to_string(d.npatterns) + " patterns, " +
+            std::to_string(d.t.nstates) + " states x " + std::to_string(d.t.nclasses) + " classes (" +
+            std::to_string(d.first_out_state) + " silent), keyword base " + std::to_string(d.kw_base) +
+            ", max pattern " + std::to_string(d.max_pattern_bytes) + " B, LDS " +
+            std::to_string(k1_lds_table_bytes(d)) + " B\n";
+  }
   pf->report = "host variant DFA: " + std::to_string(pf->host_scan.t.nstates) + " states x " +
                std::to_string(pf->host_scan.t.nclasses) + " classes\n" +
-               "scan DFA: " + std::to_string(pf->scan.t.nstates) + " states x " + std::to_string(pf->scan.t.nclasses) +
-               " classes (" + std::to_string(pf->scan.first_out_state) + " silent), " + std::to_string(pf->nkw) +
+               std::to_string(pf->groups.size()) + " scan DFA group(s), " + std::to_string(pf->nkw) +
                " keywords, " + std::to_string(pf->anchors.size()) + " anchor literals, max pattern " +
-               std::to_string(maxb) + " B\n" + rep;
+               std::to_string(maxb) + " B\n" + grep + rep;
   return true;
 }
 
@@ -820,7 +963,7 @@ bool prefilter_reference_file(const Prefilter& pf, const uint8_t* data, size_t l
   for (size_t p = 1; p < len; ++p) {
     if (fold_special_at(p >= 2 ? data[p - 2] : 0, data[p - 1], data[p])) { special = true; break; }
   }
-  two_pass(pf, pf.scan, pf.anchors, data, len, cand, gate);
+  two_pass(pf, pf.groups.data(), pf.groups.size(), pf.anchors, data, len, cand, gate);
   return special;
 }
 
@@ -840,7 +983,7 @@ void plan_from_candidates(const Prefilter& pf, std::vector<std::vector<uint64_t>
 
 void prefilter_variant_file(const Prefilter& pf, const uint8_t* data, size_t len,
                             std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
-  two_pass(pf, pf.host_scan, pf.host_anchors, data, len, cand, gate);
+  two_pass(pf, &pf.host_scan, 1, pf.host_anchors, data, len, cand, gate);
 }
 
 }  // namespace tsg

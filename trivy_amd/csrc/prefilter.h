@@ -41,7 +41,18 @@ struct ScanDfa {
   std::vector<uint32_t> out_off;       // (nstates - first_out_state + 1) offsets into out_ids
   std::vector<uint32_t> out_ids;       // output ids: [0, nkw) keywords, [nkw, nkw+nanchor) anchors
   uint32_t max_pattern_bytes = 1;      // warm-up window = max_pattern_bytes - 1
+  uint32_t kw_base = 0;                // GPU group: keyword ids [kw_base, kw_base+128) kept in register masks
+  uint32_t npatterns = 0;
 };
+
+// K1 keeps one scan DFA in LDS next to 16 per-wave hit buffers of 4 KiB; its
+// transitions are uint16 row offsets (state * stride), so a GPU scan DFA
+// must satisfy nstates * stride <= 65535 and fit the LDS left over.
+constexpr uint32_t kK1LdsBytes = 160 * 1024;
+constexpr uint32_t kK1HitLdsBytes = 16 * 1024 * 4 + 16 * 4 + 16;
+uint32_t k1_row_stride(uint32_t nclasses);          // >= nclasses + 1, odd number of dwords
+size_t k1_lds_table_bytes(const ScanDfa& d);        // scan table + class map + output metadata
+bool k1_fits(const ScanDfa& d);
 
 struct AnchorInfo {                    // one literal of one rule
   uint32_t rule;
@@ -60,7 +71,12 @@ struct RuleGpuInfo {
 
 struct Prefilter {
   uint32_t nkw = 0;                    // distinct keyword patterns
-  ScanDfa scan;                        // GPU: ASCII-only, case-folded units
+  // GPU scan DFAs (ASCII-only, case-folded units), one K1 pass each.  The
+  // keyword and anchor patterns are partitioned over the groups (a pattern
+  // is in exactly one group), so the union of the groups' outputs equals the
+  // outputs of one DFA over all patterns.  The builtin rules need one group;
+  // large custom rule sets (config 5) are split until every group fits K1.
+  std::vector<ScanDfa> groups;
   ScanDfa host_scan;                   // host: + U+0130/U+212A/U+017F alternatives (fold-special files)
   std::vector<AnchorInfo> anchors;
   std::vector<AnchorInfo> host_anchors;   // same ids; byte lengths of the variant forms

@@ -354,6 +354,8 @@ def _sizes(kind, n_or_bytes, rng):
             s = int(min(max(rng.lognormvariate(np.log(16384), 1.2), 16), 8 << 20))
         elif kind == "loguniform":       # config 2: [64 B, 64 MB]
             s = int(np.exp(rng.uniform(np.log(64), np.log(64 << 20))))
+        elif kind == "tiny":             # offset-table stress: ~300 B files
+            s = int(min(max(rng.lognormvariate(np.log(200), 1.0), 1), 64 << 10))
         else:                            # small files (config 3): mean ~25 KB
             s = int(min(max(rng.lognormvariate(np.log(9000), 1.3), 16), 4 << 20))
         s = min(s, n_or_bytes - total) if n_or_bytes - total > 16 else s
@@ -362,8 +364,13 @@ def _sizes(kind, n_or_bytes, rng):
     return sizes
 
 
+IMAGE_DIRS = ("usr/share/doc/pkg%d", "usr/lib/python3.%d/site-packages/mod", "usr/local/lib/python3.%d/dist",
+              "usr/local/go/src/p%d", "etc/app%d", "opt/app%d/src", "var/lib/app%d", "home/user%d/app",
+              "srv/www%d", "root/.config/tool%d", "usr/src/wordpress/wp%d", "opt/yarn-v1.%d/lib")
+
+
 def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4, near_miss=0.1,
-             base_bytes=32 << 20, max_files=None):
+             base_bytes=32 << 20, max_files=None, layout="src"):
     rng = random.Random(seed)
     samples = load_samples()
     rule_ids = sorted(k for k, v in samples.items() if v)
@@ -392,9 +399,16 @@ def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4,
                 continue
             data[o + filled:o + filled + take] = base[st:st + take]
             filled += take
-        d1 = rng.choice(("src", "lib", "pkg", "app", "internal", "cmd", "deploy", "config", "scripts"))
-        paths.append("%s/%s_%d/%s_%d.%s" % (d1, rng.choice(WORDS), rng.randrange(100), rng.choice(WORDS), i,
+        if layout == "image":
+            # extracted-layer layout (config 3): rootfs dirs, some under the
+            # builtin allow-paths; image scans prefix "/" (analyzer secret.go:133-135)
+            d1 = rng.choice(IMAGE_DIRS) % rng.randrange(10)
+            paths.append("%s%s/%s_%d.%s" % ("/" if rng.random() < 0.5 else "", d1, rng.choice(WORDS), i,
                                             rng.choice(EXTS)))
+        else:
+            d1 = rng.choice(("src", "lib", "pkg", "app", "internal", "cmd", "deploy", "config", "scripts"))
+            paths.append("%s/%s_%d/%s_%d.%s" % (d1, rng.choice(WORDS), rng.randrange(100), rng.choice(WORDS), i,
+                                                rng.choice(EXTS)))
     # plants: ~plant_rate of lines (40 B mean line) -> one per 40/plant_rate bytes
     n_plants = max(1, int(total / 40 * plant_rate))
     planted = nmiss = 0
