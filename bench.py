@@ -37,10 +37,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def _oracle_worker_init():
+def _oracle_worker_init(cfg_path):
     global _ORACLE
     from oracle import secret_oracle as so
-    _ORACLE = so.Scanner(None)
+    _ORACLE = so.Scanner(so.parse_config(cfg_path) if cfg_path else None)
 
 
 def _oracle_scan(item):
@@ -48,13 +48,13 @@ def _oracle_scan(item):
     return _ORACLE.scan(path, content)
 
 
-def cpu_baseline(corpus, idx, procs):
+def cpu_baseline(corpus, idx, procs, cfg_path=None):
     """Oracle over files idx with a process pool; returns (GB/s, results, seconds)."""
     import multiprocessing as mp
     items = [(corpus.paths[i], corpus.file(i)) for i in idx]
     nbytes = sum(len(c) for _, c in items)
     ctx = mp.get_context("fork")
-    with ctx.Pool(procs, initializer=_oracle_worker_init) as pool:
+    with ctx.Pool(procs, initializer=_oracle_worker_init, initargs=(cfg_path,)) as pool:
         t0 = time.perf_counter()
         res = pool.map(_oracle_scan, items, chunksize=1)
         dt = time.perf_counter() - t0
@@ -82,6 +82,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--gb", type=float, default=10.0, help="corpus GB per GPU (config 2: 10)")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
+                    help="BASELINE.json config: 2 = 10 GB source corpus (the metric's workload), "
+                         "3 = image-layer small files, 5 = 500 custom rules")
     ap.add_argument("--sizes", default="loguniform", choices=["loguniform", "lognormal", "small"])
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--threads", type=int, default=16, help="host confirm threads per rank")
@@ -108,26 +111,39 @@ def main():
             print("[bench]", *a, file=sys.stderr, flush=True)
 
     t_gen = time.perf_counter()
-    corpus = synth.generate(int(args.gb * 1e9), seed=args.seed + rank, sizes=args.sizes)
+    cfg_path = None
+    if args.config == 3:      # extracted image layers: small files, rootfs paths
+        corpus = synth.generate(int(args.gb * 1e9), seed=args.seed + rank, sizes="small", layout="image")
+    else:
+        corpus = synth.generate(int(args.gb * 1e9), seed=args.seed + rank, sizes=args.sizes)
+    if args.config == 5:      # 500 custom rules + allow rules + exclude blocks (+ builtins)
+        cfg5, plants = synth.config5(500, seed=args.seed)
+        cfg_path = "/tmp/tsg_bench_config5_%d.yaml" % rank
+        synth.write_yaml(cfg5, cfg_path)
+        synth.plant_custom(corpus, plants, seed=args.seed + rank, rate=1e-4)
     log("corpus: %.2f GB, %d files, %d plants (%d near-miss), generated in %.1fs" % (
         corpus.nbytes / 1e9, len(corpus.paths), corpus.planted, corpus.near_miss, time.perf_counter() - t_gen))
 
     device = local_rank
     torch.cuda.set_device(device)
     host_t = torch.from_numpy(corpus.data)
-    # host-feed ceiling: pinned -> HBM copy rate (reported, never the metric)
-    pinned = torch.empty(len(corpus.data), dtype=torch.uint8, pin_memory=True)
-    pinned.copy_(host_t)
+    # host-feed ceiling: pinned -> HBM copy rate on a <= 4 GB slice (reported, never the metric)
+    n_pin = min(len(corpus.data), 4 << 30)
+    pinned = torch.empty(n_pin, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(host_t[:n_pin])
     d_data = torch.empty(len(corpus.data), dtype=torch.uint8, device="cuda:%d" % device)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    d_data.copy_(pinned, non_blocking=True)
+    d_data[:n_pin].copy_(pinned, non_blocking=True)
     torch.cuda.synchronize()
-    h2d_gbps = corpus.nbytes / (time.perf_counter() - t0) / 1e9
+    h2d_gbps = n_pin / (time.perf_counter() - t0) / 1e9
     del pinned
+    if n_pin < len(corpus.data):
+        d_data[n_pin:].copy_(host_t[n_pin:])
+        torch.cuda.synchronize()
     log("H2D (pinned) %.1f GB/s" % h2d_gbps)
 
-    sc = S.Scanner(None, device=device, threads=args.threads)
+    sc = S.Scanner(S.ParseConfig(cfg_path) if cfg_path else None, device=device, threads=args.threads)
     eng = sc.engine()
     L = _lib.lib()
     paths, lens, _keep = _lib.pack_paths(corpus.paths)
@@ -198,8 +214,14 @@ def main():
         "dtype": "u8",
         "data": "synthetic (trivy_amd/synth.py, seed %#x + rank)" % args.seed,
         "config": {
-            "workload": "config2: %.0f GB synthetic text/source corpus per GPU, %s file sizes, 0.01%% planted "
-                        "secrets (87 builtin rules), builtin rules, corpus resident in HBM" % (args.gb, args.sizes),
+            "workload": {
+                2: "config2: %.0f GB synthetic text/source corpus per GPU, %s file sizes, 0.01%% planted "
+                   "secrets (87 builtin rules), builtin rules, corpus resident in HBM" % (args.gb, args.sizes),
+                3: "config3: %.0f GB of extracted-image-layer small files per GPU (mean ~25 KB, rootfs paths), "
+                   "builtin rules, corpus resident in HBM" % args.gb,
+                5: "config5: %.0f GB synthetic source corpus per GPU, trivy-secret.yaml with 500 custom rules "
+                   "+ 87 builtins, 20 allow rules, 5 exclude blocks, corpus resident in HBM" % args.gb,
+            }[args.config],
             "bytes_per_gpu": corpus.nbytes,
             "files_per_gpu": nfiles,
             "parallelism": "file shards per GPU, no collective (dp%d)" % world,
@@ -229,7 +251,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         idx = pick_sample(corpus, int(args.cpu_sample_mb * 1e6), 8 << 20, args.seed)
-        gbps, ores, dt, nb = cpu_baseline(corpus, idx, args.cpu_procs)
+        gbps, ores, dt, nb = cpu_baseline(corpus, idx, args.cpu_procs, cfg_path)
         diff = [corpus.paths[i] for j, i in enumerate(idx) if ores[j] != gpu_results[i]]
         ofind = sum(len(r["Findings"]) for r in ores)
         out["cpu_baseline"] = {
@@ -238,10 +260,26 @@ def main():
                       "(Python restatement of pkg/fanal/secret/scanner.go) in a %d-process pool, %.1f s"
                       % (len(idx), nb / 1e6, args.cpu_procs, dt),
         }
+        # the C++ restatement of the reference algorithm (every rule's keyword
+        # gate + Go-regexp find-all over every file, no GPU prefilter) on the
+        # same sample: a compiled CPU scanner closer to the Go reference's speed
+        sub = corpus.subset(idx)
+        sargs = [S.ScanArgs(sub.paths[j], sub.file(j)) for j in range(len(idx))]
+        t0 = time.perf_counter()
+        cres = S.scan_host_reference(sc, sargs, threads=args.cpu_procs)
+        cdt = time.perf_counter() - t0
+        cdiff = sum(1 for j in range(len(idx)) if cres[j] != ores[j])
+        out["cpu_baseline_cxx"] = {
+            "value": round(nb / cdt / 1e9, 5), "unit": "GB/s", "cores": args.cpu_procs, "kind": "port",
+            "sample": "same %d files, C++ Go-regexp restatement of scanner.go on every (file, rule) pair "
+                      "(tsg_scan_host_reference), %d threads, %.2f s; diff vs oracle: %d files"
+                      % (len(idx), args.cpu_procs, cdt, cdiff),
+        }
         out["parity"] = {"sample_files": len(idx), "sample_findings": ofind, "diff_files": len(diff),
                          "diff_examples": diff[:5]}
-        log("cpu baseline %.4f GB/s on %d procs; parity diff files: %d (findings in sample: %d)" % (
-            gbps, args.cpu_procs, len(diff), ofind))
+        log("cpu baseline %.4f GB/s (oracle, %d procs), %.4f GB/s (C++ restatement, %d threads); "
+            "parity diff files: %d (findings in sample: %d)" % (
+                gbps, args.cpu_procs, nb / cdt / 1e9, args.cpu_procs, len(diff), ofind))
 
     if rank == 0:
         line = json.dumps(out)

@@ -1,0 +1,75 @@
+"""Per-launch HBM traffic of the scan kernels from tools/pmc_traffic.sh output.
+
+FETCH_SIZE (KB) is scaled by the calibration run of tools/calib_fetch, which
+reads a known byte count in K1's exact access pattern (lane-owned 4 KiB
+chunks, whole 128-byte lines, nontemporal 16-byte loads):
+    scale = bytes_read / (FETCH_SIZE_KB * 1024)   of calib_k1pattern
+    traffic(K1) = FETCH_SIZE_KB(K1 launch) * 1024 * scale
+WRITE_SIZE is reported as read (exact for streaming stores per the guide;
+K1's writes are keyword bits, hit records and per-chunk counts).
+
+  python tools/pmc_traffic.py gpurun_out/<run> > profiles/<round>_traffic.json
+"""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+
+def per_kernel(root, counter):
+    vals = collections.defaultdict(list)
+    for f in sorted(glob.glob(root + "/*_counter_collection.csv") + glob.glob(root + "/*/*_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            m = re.search(r"(tsg_k1_scan|tsg_k2_verify|calib_coalesced|calib_k1pattern)", name)
+            if m:
+                vals[(m.group(1), r["Dispatch_Id"])].append(float(r["Counter_Value"]))
+    out = collections.defaultdict(list)
+    for (k, _), v in vals.items():
+        out[k].append(sum(v))          # sum over XCD/instance rows of one dispatch
+    return out
+
+
+def main():
+    run = sys.argv[1]
+    calib = per_kernel(run + "/calib", "FETCH_SIZE")
+    calib_bytes = None
+    for line in open(run + "/calib.log"):
+        m = re.match(r"calib_k1pattern bytes (\d+)", line)
+        if m:
+            calib_bytes = int(m.group(1))
+    k1 = per_kernel(run + "/k1", "FETCH_SIZE")
+    k1w = per_kernel(run + "/k1w", "WRITE_SIZE")
+    cal = sorted(calib["calib_k1pattern"])[len(calib["calib_k1pattern"]) // 2]
+    scale = calib_bytes / (cal * 1024.0)
+    coal = calib.get("calib_coalesced")
+    bench = None
+    for line in open(run + "/k1.log"):
+        if line.startswith("{"):
+            bench = json.loads(line)
+    out = {
+        "kernel": "tsg_k1_scan",
+        "bytes_per_launch": bench["roofline"]["bytes_per_launch"] if bench else None,
+        "workload": bench["config"]["workload"] if bench else None,
+        "k1_fetch_size_kb_per_launch": sorted(k1["tsg_k1_scan"]),
+        "k1_write_size_kb_per_launch": sorted(k1w.get("tsg_k1_scan", [])),
+        "k2_fetch_size_kb_per_launch": sorted(k1.get("tsg_k2_verify", [])),
+        "calib_k1pattern": {"bytes": calib_bytes, "fetch_size_kb": cal, "scale": scale},
+        "calib_coalesced_fetch_size_kb": coal,
+    }
+    f = min(k1["tsg_k1_scan"]) * 1024.0 * scale
+    w = min(k1w.get("tsg_k1_scan", [0.0])) * 1024.0
+    out["traffic_bytes_per_launch"] = f + w
+    out["read_bytes_per_launch"] = f
+    out["write_bytes_per_launch"] = w
+    if out["bytes_per_launch"]:
+        out["traffic_over_algorithmic"] = (f + w) / out["bytes_per_launch"]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
