@@ -164,6 +164,12 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
                          const uint8_t* binary, tsg_result** out);
 /* Prefilter compile report without a GPU (NUL-terminated; free with tsg_free). */
 int tsg_prefilter_report(const tsg_ruleset* rs, char** out);
+/* Test hook for the host regexp engine: compiles `pattern` (Go syntax) and,
+ * for each of the n positions, writes the end of the leftmost-first match
+ * anchored there (-1: none) as computed by the lazy DFA (dfa_end) and by the
+ * Pike VM (vm_end).  Never used by tsg_scan_batch. */
+int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
+                    int64_t* dfa_end, int64_t* vm_end);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,13 @@ def test_config5_groups_compile(tmp_path):
     rep = S.prefilter_report(sc)
     ngroups = int(rep.splitlines()[1].split()[0])
     assert ngroups > 1, rep[:400]
-    assert "FULL" not in rep
+    # every rule gets a bounded anchor; the exclude-block regexes are compiled
+    # as pseudo-rules too, and the one without a bounded anchor
+    # (#\s*nosec-block-...) is evaluated on the host only where its required
+    # literal occurs
+    full = [ln for ln in rep.splitlines() if "FULL" in ln]
+    assert all(ln.startswith("exclude-block") and "where present" in ln for ln in full), full
+    assert sum(1 for ln in rep.splitlines() if ln.startswith("exclude-block")) == 5 + 13
 
 
 @pytest.mark.parametrize("seed", [5, 6])

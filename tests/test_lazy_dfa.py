@@ -1,0 +1,91 @@
+"""Host regexp engine: the lazy DFA that finds anchored match ends
+(goregexp.cpp LazyDfa, used by find_all_from_candidates) must agree with
+the Pike VM (Go's machine restated) at every position -- empty-width
+assertions, leftmost-first priority (lazy/greedy), invalid UTF-8 and
+non-ASCII included.  The rule patterns are the builtin rules
+(builtin-rules.go:101-849), the builtin allow rules and the config-5 custom
+rules and exclude blocks (scanner.go:223-275)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from trivy_amd import _lib, synth
+from trivy_amd import secret as S
+
+EDGE = [
+    r"\bfoo\b", r"\Boo", r"(?m)^abc$", r"^", r"$", r"(?m)^", r"(?m)$", r"a*", r"a*?", r"(a|ab)(c|bcd)(d*)",
+    r"(?s).*?END", r"(?s)BEGIN.*END", r"(?i)straße", r"(?i)k", r"\Aabc", r"abc\z", r"[^\n]*$", r"(?U)a+",
+    r"(?U)a+?", r"x{2,5}", r"(x|xy){3}", r"é+", r"[à-ÿ]{2}", r"\pL+", r"\PL", r".", r"(?s).",
+    r"--- ignore block start ---(.|\s)*--- ignore block stop ---", r"(^|[^0-9a-zA-Z])(tok_[A-Za-z0-9]{4})($|[^0-9a-zA-Z])",
+    r"(?m)^# vault: .*$", r"#\s*nosec-block-\d+[^\n]*", r"\b(a|b)+\b", r"(?i)(?P<key>ab[a-z0-9_ .\-,]{0,5})(=|:).{0,3}['\"]",
+]
+
+
+def _texts(rng):
+    alpha = ["a", "b", "c", "d", "x", "y", "o", "f", "E", "N", "D", "K", " ", "\n", "_", "-", "=", ":", "'", '"',
+             "#", "tok_", "abc", "foo", "END", "BEGIN", "ß", "é", "K", "ſ", "ab12", "--- ignore block start ---",
+             "--- ignore block stop ---", "# vault: ", "nosec-block-7", "\t"]
+    out = []
+    for _ in range(6):
+        s = "".join(rng.choice(alpha) for _ in range(rng.randint(0, 120))).encode()
+        if rng.random() < 0.5:                        # invalid UTF-8 bytes
+            b = bytearray(s)
+            for _ in range(rng.randint(1, 4)):
+                b.insert(rng.randint(0, len(b)), rng.choice([0x80, 0xC3, 0xE2, 0xFF, 0xBF]))
+            s = bytes(b)
+        out.append(s)
+    return out
+
+
+def _probe(pattern, text):
+    L = _lib.lib()
+    n = len(text) + 1
+    buf = np.frombuffer(text + b"\0", dtype=np.uint8)
+    pos = np.arange(n, dtype=np.uint64)
+    d = np.zeros(n, dtype=np.int64)
+    v = np.zeros(n, dtype=np.int64)
+    _lib.check(L.tsg_regex_probe(pattern.encode(), buf.ctypes.data, len(text), pos.ctypes.data, n,
+                                 d.ctypes.data, v.ctypes.data))
+    return d, v
+
+
+def _patterns():
+    pats = list(EDGE)
+    pats += [r["regex"] for r in S.GetBuiltinRules() if r.get("regex")]
+    cfg, _ = synth.config5(60, seed=3)
+    pats += [r["regex"] for r in cfg["rules"]]
+    pats += [r["regexes"][0] for r in [cfg["exclude-block"]]] + list(synth.EXCLUDE_BLOCKS)
+    return pats
+
+
+@pytest.mark.parametrize("chunk", range(4))
+def test_lazy_dfa_matches_vm(chunk):
+    rng = random.Random(1234 + chunk)
+    pats = _patterns()
+    pats = pats[chunk::4]
+    checked = 0
+    for p in pats:
+        for t in _texts(rng):
+            d, v = _probe(p, t)
+            bad = np.nonzero(d != v)[0]
+            assert len(bad) == 0, (p, t, int(bad[0]), int(d[bad[0]]), int(v[bad[0]]))
+            checked += len(t) + 1
+    assert checked > 1000
+
+
+def test_lazy_dfa_planted_rule_samples():
+    # the builtin rules' own sampled secrets, embedded in text: real matches
+    rng = random.Random(7)
+    samples = synth.load_samples()
+    rules = [r for r in S.GetBuiltinRules() if r.get("regex")]
+    hits = 0
+    for r in rules:
+        ss = samples.get(r["id"], [])[:3]
+        for smp in ss:
+            t = ("x = 1\n" + "key: '" + smp + "'\n").encode()
+            d, v = _probe(r["regex"], t)
+            assert (d == v).all(), r["id"]
+            hits += int((d >= 0).sum())
+    assert hits > 50

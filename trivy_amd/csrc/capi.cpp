@@ -386,4 +386,19 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
 
 const char* tsg_builtin_rules_json(void) { return tsg_builtin_json_ptr(); }
 
+int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
+                    int64_t* dfa_end, int64_t* vm_end) {
+  if (!pattern || (len && !text) || (n && (!pos || !dfa_end || !vm_end))) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string err;
+  auto rx = re::Regexp::compile(pattern, &err);
+  if (!rx) return fail(TSG_ERR_CONFIG, err);
+  std::vector<int> caps(2 * (rx->num_subexp() + 1));
+  for (size_t i = 0; i < n; ++i) {
+    if (pos[i] > len) return fail(TSG_ERR_INVALID, "position out of range");
+    dfa_end[i] = rx->match_end(text, len, pos[i]);
+    vm_end[i] = rx->match_at(text, len, pos[i], true, 0, caps.data()) ? caps[1] : -1;
+  }
+  return TSG_OK;
+}
+
 }  // extern "C"

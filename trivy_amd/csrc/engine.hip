@@ -439,6 +439,17 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     const AnchorDev an = anchors[h & 0xffffffu];
     const RuleDev r = rules[an.rule];
     const uint32_t f = file_of(offsets, nfiles, q);
+    if (r.mode == 3) {
+      // presence anchor of a rule evaluated in full on the host: the hit is
+      // the candidate (any one per file suffices)
+      const unsigned int idx = atomicAdd(&counters[1], 1u);
+      if (idx < cand_cap) {
+        cands[idx].file = f;
+        cands[idx].rule = an.rule;
+        cands[idx].start = q - offsets[f];
+      }
+      continue;
+    }
     if (!r.always_gate && r.gate_on_gpu) {
       uint32_t g = 0;
       for (uint32_t k = 0; k < r.kw_count && !g; ++k) {
@@ -848,7 +859,7 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
   if (!st) st = &local;
   if (!run_gpu(in, st, err)) return false;
   Impl& m = *impl_;
-  const size_t nr = pf_.rules.size();
+  const size_t nr = rs_->rules.size();   // real rules only (exclude pseudo-rules follow)
   if (kw_gate) {
     m.h_kw.resize(static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * m.kw_words);
     HIP_OK(hipMemcpy(m.h_kw.data(), m.d_kw, m.h_kw.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -867,7 +878,8 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
   }
   if (cands) {
     cands->assign(in.nfiles, std::vector<std::vector<uint64_t>>(nr));
-    for (const CandDev& c : m.h_cands) (*cands)[c.file][c.rule].push_back(c.start);
+    for (const CandDev& c : m.h_cands)
+      if (c.rule < nr) (*cands)[c.file][c.rule].push_back(c.start);
     for (auto& f : *cands)
       for (auto& v : f) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); }
   }
@@ -884,6 +896,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   Impl& m = *impl_;
   const Ruleset& rs = *rs_;
   const size_t nr = rs.rules.size();
+  const size_t nplan = pf_.rules.size();   // rules + exclude-block pseudo-rules
   // group candidates per file (counting sort by file, then sort each file's list)
   std::vector<uint32_t> per_file(in.nfiles + 1, 0);
   for (const CandDev& c : m.h_cands) per_file[c.file + 1]++;
@@ -894,7 +907,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     for (const CandDev& c : m.h_cands) sorted[pos[c.file]++] = c;
   }
   bool any_full = false;
-  for (const auto& gi : pf_.rules) if (gi.mode == 1) any_full = true;
+  for (size_t r = 0; r < nr; ++r) if (pf_.rules[r].mode == 1) any_full = true;
   results->assign(in.nfiles, Secret());
   // largest files first (LPT): the per-file confirm cost grows with size
   std::vector<uint32_t> work(in.nfiles);
@@ -939,11 +952,11 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         continue;
       }
       nconf.fetch_add(1);
-      plan.kind.assign(nr, kPlanNoMatch);
+      plan.kind.assign(nplan, kPlanNoMatch);
       plan.cands.clear();
-      for (size_t r = 0; r < nr; ++r) {
+      for (size_t r = 0; r < nplan; ++r) {
         const RuleGpuInfo& gi = pf_.rules[r];
-        if (gi.mode == 1) plan.kind[r] = kPlanFull;
+        if (gi.mode == 1) plan.kind[r] = kPlanFull;   // (mode 3: only with a presence candidate, below)
       }
       std::sort(sorted.begin() + cb, sorted.begin() + ce, [](const CandDev& a, const CandDev& b) {
         return a.rule != b.rule ? a.rule < b.rule : a.start < b.start;
@@ -956,7 +969,8 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
           if (rc.starts.empty() || rc.starts.back() != sorted[k].start) rc.starts.push_back(sorted[k].start);
           ++k;
         }
-        plan.kind[r] = pf_.rules[r].gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
+        plan.kind[r] = pf_.rules[r].mode == 3 ? kPlanFull
+                     : pf_.rules[r].gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
         plan.cands.push_back(std::move(rc));
       }
       NlSource nls;

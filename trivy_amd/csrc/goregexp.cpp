@@ -3,6 +3,8 @@
 // compile.go; regexp/exec.go, regexp.go allMatches).
 #include "goregexp.h"
 
+#include <unordered_map>
+
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -929,6 +931,179 @@ class Machine {
   }
 };
 
+// ------------------------------------------------------------- lazy DFA
+// End of the leftmost-first match anchored at a position, without captures,
+// as a DFA built lazily from the program (the RE2 construction).  A state is
+// the priority-ordered list of pcs the Pike VM above would add() to its
+// queue (before the closure), plus the category of the previous rune; the
+// closure is taken when the next rune is known, so empty-width assertions
+// see exactly the context Machine::match gives them.  Captures never affect
+// which thread wins (priority and dedupe are by pc only), so the match end
+// equals Machine::match's caps[1].
+class LazyDfa {
+ public:
+  explicit LazyDfa(const Prog& p) : p_(p) {
+    mark_.assign(p.inst.size(), 0);
+    for (uint32_t pc = 0; pc < p.inst.size(); ++pc) {
+      const IOp op = p.inst[pc].op;
+      if (op == IOp::Rune || op == IOp::Rune1 || op == IOp::RuneAny || op == IOp::RuneAnyNotNL) rinst_.push_back(pc);
+    }
+    for (int c = 0; c < 128; ++c) ascii_cls_[c] = class_of(c);
+    states_.push_back(State());                    // state 0: dead (no seeds)
+  }
+
+  // -1: no match; -2: state budget exceeded (caller falls back to the VM)
+  long match_end(const uint8_t* s, size_t len, size_t pos) {
+    const int32_t pr = pos == 0 ? -1 : rune_before(s, pos);
+    seeds_.assign(1, p_.start);
+    int st = intern(seeds_, cat(pr));
+    long end = -1;
+    size_t p = pos;
+    for (;;) {
+      if (st == 0) break;
+      if (p >= len) {
+        if (eot(st)) end = static_cast<long>(len);
+        break;
+      }
+      int k, w;
+      if (s[p] < 0x80) { k = ascii_cls_[s[p]]; w = 1; }
+      else { int32_t r; decode_rune(s + p, len - p, &r, &w); k = class_of(r); }
+      int32_t t = states_[st].next.size() > static_cast<size_t>(k) ? states_[st].next[k] : -1;
+      if (t < 0) {
+        t = transition(st, k);
+        if (t < 0) return -2;
+      }
+      if (t & 1) end = static_cast<long>(p);
+      st = t >> 1;
+      p += w;
+    }
+    return end;
+  }
+
+ private:
+  struct State {
+    std::vector<uint32_t> seeds;
+    uint8_t prev = 0;                // category of the previous rune
+    std::vector<int32_t> next;       // per class: (state << 1) | match-before-this-rune; -1 unknown
+    int8_t eot = -1;
+  };
+  static constexpr size_t kMaxStates = 4096;
+  const Prog& p_;
+  std::vector<uint32_t> rinst_;
+  int ascii_cls_[128];
+  std::vector<int32_t> cls_rep_;                 // class -> representative rune
+  std::unordered_map<std::string, int> cls_ids_;
+  std::unordered_map<int32_t, int> nonascii_cls_;
+  std::vector<State> states_;
+  std::unordered_map<std::string, int> state_ids_;
+  std::vector<uint32_t> mark_, seeds_, threads_, stack_;
+  uint32_t gen_ = 0;
+
+  // rune categories that decide empty-width contexts: 0 begin/end of text,
+  // 1 '\n', 2 word character, 3 anything else
+  static uint8_t cat(int32_t r) { return r < 0 ? 0 : r == '\n' ? 1 : is_word(r) ? 2 : 3; }
+  static int32_t rep_of_cat(uint8_t c) { static const int32_t k[4] = {-1, '\n', 'a', ' '}; return k[c]; }
+
+  bool consumes(uint32_t pc, int32_t c) const {
+    const Inst& in = p_.inst[pc];
+    switch (in.op) {
+      case IOp::Rune: return rune_match(p_, in, c);
+      case IOp::Rune1: return c == static_cast<int32_t>(in.arg);
+      case IOp::RuneAny: return c >= 0;
+      case IOp::RuneAnyNotNL: return c >= 0 && c != '\n';
+      default: return false;
+    }
+  }
+
+  int class_of(int32_t r) {
+    if (r >= 0x80) {
+      auto it = nonascii_cls_.find(r);
+      if (it != nonascii_cls_.end()) return it->second;
+    }
+    std::string sig(1, static_cast<char>(cat(r)));
+    sig.resize(1 + (rinst_.size() + 7) / 8, 0);
+    for (size_t i = 0; i < rinst_.size(); ++i)
+      if (consumes(rinst_[i], r)) sig[1 + i / 8] = static_cast<char>(sig[1 + i / 8] | (1 << (i & 7)));
+    auto ins = cls_ids_.emplace(sig, static_cast<int>(cls_rep_.size()));
+    if (ins.second) cls_rep_.push_back(r);
+    if (r >= 0x80) nonascii_cls_.emplace(r, ins.first->second);
+    return ins.first->second;
+  }
+
+  int intern(const std::vector<uint32_t>& seeds, uint8_t prev) {
+    if (seeds.empty()) return 0;
+    std::string key(1, static_cast<char>(prev));
+    key.append(reinterpret_cast<const char*>(seeds.data()), seeds.size() * sizeof(uint32_t));
+    auto it = state_ids_.find(key);
+    if (it != state_ids_.end()) return it->second;
+    if (states_.size() >= kMaxStates) return -1;
+    State st;
+    st.seeds = seeds;
+    st.prev = prev;
+    states_.push_back(std::move(st));
+    const int id = static_cast<int>(states_.size()) - 1;
+    state_ids_.emplace(std::move(key), id);
+    return id;
+  }
+
+  // Machine::add over every seed in order (shared visited set): the thread
+  // pcs (Match / Rune*) in priority order
+  void closure(const std::vector<uint32_t>& seeds, uint8_t cond) {
+    if (++gen_ == 0) { std::fill(mark_.begin(), mark_.end(), 0); gen_ = 1; }
+    threads_.clear();
+    for (uint32_t s0 : seeds) {
+      stack_.assign(1, s0);
+      while (!stack_.empty()) {
+        const uint32_t pc = stack_.back();
+        stack_.pop_back();
+        if (pc == 0 || mark_[pc] == gen_) continue;
+        mark_[pc] = gen_;
+        const Inst& in = p_.inst[pc];
+        switch (in.op) {
+          case IOp::Fail: break;
+          case IOp::Alt: case IOp::AltMatch: stack_.push_back(in.arg); stack_.push_back(in.out); break;
+          case IOp::Empty: if ((in.arg & ~cond) == 0) stack_.push_back(in.out); break;
+          case IOp::Nop: case IOp::Capture: stack_.push_back(in.out); break;
+          default: threads_.push_back(pc); break;
+        }
+      }
+    }
+  }
+
+  int32_t transition(int st, int k) {
+    const int32_t c = cls_rep_[k];
+    const uint8_t cond = empty_context(rep_of_cat(states_[st].prev), c);
+    closure(states_[st].seeds, cond);
+    bool matched = false;
+    std::vector<uint32_t> nseeds;
+    const uint32_t g = gen_;
+    (void)g;
+    for (uint32_t pc : threads_) {
+      const Inst& in = p_.inst[pc];
+      if (in.op == IOp::Match) { matched = true; break; }   // lower-priority threads are cut
+      if (consumes(pc, c) && std::find(nseeds.begin(), nseeds.end(), in.out) == nseeds.end()) nseeds.push_back(in.out);
+    }
+    const int to = intern(nseeds, cat(c));
+    if (to < 0) return -1;
+    const int32_t t = (to << 1) | (matched ? 1 : 0);
+    State& S = states_[st];
+    if (S.next.size() < cls_rep_.size()) S.next.resize(cls_rep_.size(), -1);
+    S.next[k] = t;
+    return t;
+  }
+
+  bool eot(int st) {
+    State& S = states_[st];
+    if (S.eot < 0) {
+      closure(S.seeds, empty_context(rep_of_cat(S.prev), -1));
+      bool m = false;
+      for (uint32_t pc : threads_) if (p_.inst[pc].op == IOp::Match) { m = true; break; }
+      S.eot = m ? 1 : 0;
+    }
+    return S.eot == 1;
+  }
+};
+
 // First-byte set of a program: follow non-consuming instructions from start
 // (assertions treated as passable); a reachable Match means no filter.
 void compute_first(Prog* p) {
@@ -1052,6 +1227,27 @@ bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored
     cache.emplace_back(id_, std::move(own));
   }
   return m->match(text, len, pos, anchored, caps);
+}
+
+long Regexp::match_end(const uint8_t* text, size_t len, size_t pos) const {
+  if (prog_.start == 0) return -1;
+  thread_local std::vector<std::pair<uint64_t, std::unique_ptr<LazyDfa>>> cache;
+  LazyDfa* d = nullptr;
+  for (auto& e : cache) {
+    if (e.first == id_) { d = e.second.get(); break; }
+  }
+  if (!d) {
+    if (cache.size() > 4096) cache.clear();
+    cache.emplace_back(id_, std::unique_ptr<LazyDfa>(new LazyDfa(prog_)));
+    d = cache.back().second.get();
+  }
+  long e = d->match_end(text, len, pos);
+  if (e == -2) {                        // state budget exceeded: start a fresh DFA next time, use the VM now
+    for (auto& c : cache) if (c.first == id_) c.second.reset(new LazyDfa(prog_));
+    std::vector<int> caps(2 * (prog_.num_cap + 1));
+    e = match_at(text, len, pos, true, 0, caps.data()) ? caps[1] : -1;
+  }
+  return e;
 }
 
 bool Regexp::match_string(const uint8_t* text, size_t len) const {

@@ -121,6 +121,9 @@ class Regexp {
   // caps receives 2*(num_subexp+1) offsets (-1 for non-participating groups).
   bool match_at(const uint8_t* text, size_t len, size_t pos, bool anchored, int ncap_wanted,
                 int* caps) const;
+  // End offset of the leftmost-first match anchored at `pos` (-1: none),
+  // from a lazily built DFA (no captures); equals match_at(.., true, ..)'s caps[1].
+  long match_end(const uint8_t* text, size_t len, size_t pos) const;
   // Regexp.MatchString
   bool match_string(const uint8_t* text, size_t len) const;
   // Regexp.FindAll(Submatch)Index(text, -1): flattened vectors of 2 (or 2*(ncap+1)) ints.

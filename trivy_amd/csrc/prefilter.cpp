@@ -548,12 +548,15 @@ struct AnchorChoice {
   uint32_t dmin = 0, dmax = 0;
 };
 
-AnchorChoice choose_anchor(const std::vector<const Node*>& items) {
+// bounded: the literal's offset from the match start must be bounded (a
+// candidate-start anchor); otherwise any literal set every match contains
+// will do (a presence gate for a rule evaluated in full on the host).
+AnchorChoice choose_anchor(const std::vector<const Node*>& items, bool bounded = true) {
   AnchorChoice best;
   double best_score = -1;
   uint32_t plo = 0, phi = 0;
   for (size_t k = 0; k < items.size(); ++k) {
-    if (phi <= kMaxPrefixBytes) {
+    if (!bounded || phi <= kMaxPrefixBytes) {
       SeqSet raw = prefix_of_items(items, k);
       SeqSet lits;
       for (const auto& s : raw) lits.insert(scan_form(s));
@@ -701,6 +704,10 @@ void two_pass(const Prefilter& pf, const ScanDfa* dfas, size_t ndfa, const std::
     const AnchorInfo& a = anchors[h.anchor];
     if (!(*gate)[a.rule] && pf.rules[a.rule].gate_on_gpu) continue;
     const RuleGpuInfo& gi = pf.rules[a.rule];
+    if (gi.mode == 3) {                                 // presence gate: the hit itself
+      (*cand)[a.rule].push_back(h.end);
+      continue;
+    }
     const DfaTable& v = pf.verify[gi.verify_dfa];
     long hi = static_cast<long>(h.end) + 1 - a.min_len - a.dmin;
     long lo = static_cast<long>(h.end) + 1 - a.max_len - a.dmax;
@@ -857,8 +864,16 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
   *pf = Prefilter();
   // --- keywords: distinct ASCII lowered keywords get a GPU pattern id
   std::map<std::string, uint32_t> kw_ids;
-  pf->rules.resize(rs.rules.size());
-  for (size_t r = 0; r < rs.rules.size(); ++r) {
+  // rules, then one keyword-less pseudo-rule per exclude-block regex
+  const size_t nr = rs.rules.size();
+  pf->rules.resize(nr + rs.excludes.size());
+  for (size_t k = 0; k < rs.excludes.size(); ++k) {
+    RuleGpuInfo& gi = pf->rules[nr + k];
+    gi.kw_begin = gi.kw_count = 0;
+    gi.always_gate = 1;
+    gi.gate_on_gpu = 1;
+  }
+  for (size_t r = 0; r < nr; ++r) {
     const Rule& rule = rs.rules[r];
     RuleGpuInfo& gi = pf->rules[r];
     gi.kw_begin = static_cast<uint32_t>(pf->rule_kw.size());
@@ -890,19 +905,51 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
     hmaxb = std::max(hmaxb, add_seq(&host, h0, keyword_seq(pf->kw_text[k], true), static_cast<int>(k)));
   }
   std::string rep;
-  for (size_t r = 0; r < rs.rules.size(); ++r) {
-    const Rule& rule = rs.rules[r];
+  for (size_t r = 0; r < pf->rules.size(); ++r) {
+    const re::Regexp* rx = r < nr ? rs.rules[r].regex.get() : rs.excludes[r - nr];
+    const std::string name = r < nr ? rs.rules[r].id : "exclude-block #" + std::to_string(r - nr);
     RuleGpuInfo& gi = pf->rules[r];
     gi.mode = 1;
-    if (!rule.regex) { gi.mode = 2; continue; }      // no regex: never any location
+    if (!rx) { gi.mode = 2; continue; }              // no regex: never any location
     std::vector<const Node*> items;
-    flatten(*rule.regex->ast(), &items);
-    AnchorChoice ch = rule.regex->nullable() ? AnchorChoice() : choose_anchor(items);
-    if (!ch.ok) { rep += rule.id + ": FULL (no bounded anchor)\n"; continue; }
+    flatten(*rx->ast(), &items);
+    AnchorChoice ch = rx->nullable() ? AnchorChoice() : choose_anchor(items);
     std::string note;
     DfaTable vt;
     uint32_t limit = 0;
-    if (!build_verify(items, ch.k + 1, &vt, &limit, &note)) { rep += rule.id + ": FULL (verify DFA too large)\n"; continue; }
+    const char* why = !ch.ok ? "no bounded anchor" : nullptr;
+    if (!why && !build_verify(items, ch.k + 1, &vt, &limit, &note)) why = "verify DFA too large";
+    if (why) {
+      // FULL on the host -- but only in files that contain one of a literal
+      // set every match contains (mode 3: K2 turns such a hit straight into
+      // a presence candidate, no verify)
+      AnchorChoice req = rx->nullable() ? AnchorChoice() : choose_anchor(items, false);
+      if (!req.ok) { rep += name + ": FULL (" + why + ")\n"; continue; }
+      gi.mode = 3;
+      gi.verify_dfa = 0;
+      gi.verify_limit = 0;
+      for (const auto& s : req.lits) {
+        AnchorInfo a{static_cast<uint32_t>(r), seq_min_len(s), seq_max_len(s), 0, 0};
+        uint32_t id = pf->nkw + static_cast<uint32_t>(pf->anchors.size());
+        pf->anchors.push_back(a);
+        pats.push_back({s, id});
+        maxb = std::max(maxb, seq_max_len(s));
+        AnchorInfo ha = a;
+        ha.min_len = 0xffffffffu;
+        ha.max_len = 0;
+        SeqSet vforms;
+        for (const auto& rawlit : req.raw) if (scan_form(rawlit) == s) vforms.insert(scan_form(rawlit, true));
+        for (const auto& v : vforms) {
+          ha.min_len = std::min(ha.min_len, seq_min_len(v));
+          ha.max_len = std::max(ha.max_len, seq_max_len(v));
+          hmaxb = std::max(hmaxb, add_seq(&host, h0, v, static_cast<int>(id)));
+        }
+        pf->host_anchors.push_back(ha);
+      }
+      rep += name + ": FULL (" + why + ") where present: item " + std::to_string(req.k) + ", " +
+             std::to_string(req.lits.size()) + " literal(s)\n";
+      continue;
+    }
     gi.mode = 0;
     gi.verify_dfa = static_cast<uint32_t>(pf->verify.size());
     gi.verify_limit = std::max<uint32_t>(limit, 1);
@@ -931,7 +978,7 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
       }
       pf->host_anchors.push_back(ha);
     }
-    rep += rule.id + ": anchored item " + std::to_string(ch.k) + ", " + std::to_string(ch.lits.size()) +
+    rep += name + ": anchored item " + std::to_string(ch.k) + ", " + std::to_string(ch.lits.size()) +
            " literal(s), offset [" + std::to_string(ch.dmin) + "," + std::to_string(ch.dmax) + "], verify " +
            std::to_string(pf->verify.back().nstates) + " states x " + std::to_string(pf->verify.back().nclasses) +
            " classes, limit " + std::to_string(gi.verify_limit) + note + "\n";
@@ -973,7 +1020,7 @@ void plan_from_candidates(const Prefilter& pf, std::vector<std::vector<uint64_t>
   plan->cands.clear();
   for (size_t k = 0; k < nr; ++k) {
     const RuleGpuInfo& gi = pf.rules[k];
-    if (gi.mode == 1) plan->kind[k] = kPlanFull;
+    if (gi.mode == 1 || (gi.mode == 3 && !(*cands)[k].empty())) plan->kind[k] = kPlanFull;
     else if (gi.mode == 0 && !(*cands)[k].empty()) {
       plan->kind[k] = gi.gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
       plan->cands.push_back({static_cast<uint32_t>(k), std::move((*cands)[k])});

@@ -61,7 +61,8 @@ struct AnchorInfo {                    // one literal of one rule
 };
 
 struct RuleGpuInfo {
-  uint8_t mode;                        // 0 = anchored (GPU candidates), 1 = FULL (host)
+  uint8_t mode;                        // 0 = anchored (GPU candidates), 1 = FULL (host), 2 = no regex,
+                                       // 3 = FULL in files containing a required literal (presence anchors)
   uint8_t gate_on_gpu;                 // keyword gate exact on GPU (ASCII keywords)
   uint8_t always_gate;                 // no keywords (or an empty keyword): gate always true
   uint32_t kw_begin, kw_count;         // keyword ids in Prefilter::rule_kw

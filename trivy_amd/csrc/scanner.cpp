@@ -118,6 +118,15 @@ bool contains(const std::vector<std::string>& v, const std::string& s) {
   return std::find(v.begin(), v.end(), s) != v.end();
 }
 
+void index_excludes(Ruleset* rs) {
+  rs->excludes.clear();
+  for (const auto& r : rs->exclude_block) rs->excludes.push_back(r.get());
+  for (auto& rule : rs->rules) {
+    rule.exclude_base = static_cast<uint32_t>(rs->excludes.size());
+    for (const auto& r : rule.exclude_block) rs->excludes.push_back(r.get());
+  }
+}
+
 }  // namespace
 
 bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
@@ -128,6 +137,7 @@ bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
     out->rules = std::move(b_rules);
     out->allow_rules = std::move(b_allow);
     out->exclude_block.clear();
+    index_excludes(out);
     return true;
   }
   std::vector<std::string> enable = str_list(cfg->get("enable-builtin-rules"));
@@ -172,6 +182,7 @@ bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
   for (auto& a : b_allow) if (!contains(disable_allow, a.id)) out->allow_rules.push_back(a);
   for (auto& a : custom_allow) if (!contains(disable_allow, a.id)) out->allow_rules.push_back(a);
   out->exclude_block = std::move(excl);
+  index_excludes(out);
   return true;
 }
 
@@ -295,9 +306,20 @@ void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t 
       size_t s = starts[idx];
       if (s < pos) { ++idx; continue; }
       if (s > len) { idx = starts.size(); break; }
-      if (chain_boundary(text, len, pos, s) && re.match_at(text, len, s, true, ncap, caps.data())) {
-        found = true;
-        break;
+      if (chain_boundary(text, len, pos, s)) {
+        // the lazy DFA decides whether (and where) an anchored match ends; the
+        // VM runs only for a match whose submatches are wanted
+        const long e = re.match_end(text, len, s);
+        if (e >= 0) {
+          if (submatch) {
+            if (!re.match_at(text, len, s, true, ncap, caps.data())) { ++idx; continue; }
+          } else {
+            caps[0] = static_cast<int>(s);
+            caps[1] = static_cast<int>(e);
+          }
+          found = true;
+          break;
+        }
       }
       ++idx;
     }
@@ -338,17 +360,31 @@ bool allow_match(const std::vector<AllowRule>& rules, const uint8_t* m, size_t n
 
 struct Loc { long start, end; };
 
-class Blocks {                                        // scanner.go:237-275
+// ExcludeBlock (scanner.go:237-275): on first use, every exclude regex's
+// find-all over the whole file.  With a plan, exclude regex k (pseudo-rule
+// plan_base + k) is evaluated like a rule: from its GPU candidate starts, not
+// at all when it has none, or in full when it has no bounded anchor.
+class Blocks {
  public:
-  Blocks(const uint8_t* c, size_t n, const std::vector<RegexpPtr>& rx) : c_(c), n_(n), rx_(rx) {}
+  Blocks(const uint8_t* c, size_t n, const std::vector<RegexpPtr>& rx, const FilePlan* plan, size_t plan_base)
+      : c_(c), n_(n), rx_(rx), plan_(plan), base_(plan_base) {}
   bool match(const Loc& l) {
     if (!done_) {
       done_ = true;
       std::vector<int> m;
-      for (const auto& r : rx_) {
+      for (size_t j = 0; j < rx_.size(); ++j) {
+        const auto& r = rx_[j];
         if (!r) continue;
         m.clear();
-        r->find_all(c_, n_, false, &m);
+        const size_t id = base_ + j;
+        const uint8_t kind = plan_ && id < plan_->kind.size() ? plan_->kind[id] : static_cast<uint8_t>(kPlanFull);
+        if (kind == kPlanFull) {
+          r->find_all(c_, n_, false, &m);
+        } else if (kind == kPlanCandidates || kind == kPlanCandHostGate) {
+          auto it = std::lower_bound(plan_->cands.begin(), plan_->cands.end(), id,
+                                     [](const RuleCandidates& a, size_t v) { return a.rule < v; });
+          if (it != plan_->cands.end() && it->rule == id) find_all_from_candidates(*r, c_, n_, it->starts, false, &m);
+        }
         for (size_t k = 0; k + 1 < m.size(); k += 2) locs_.push_back({m[k], m[k + 1]});
       }
     }
@@ -360,6 +396,8 @@ class Blocks {                                        // scanner.go:237-275
   const uint8_t* c_;
   size_t n_;
   const std::vector<RegexpPtr>& rx_;
+  const FilePlan* plan_;
+  size_t base_;
   bool done_ = false;
   std::vector<Loc> locs_;
 };
@@ -760,7 +798,7 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
     if (!have_lower) { lower = go_bytes_to_lower(content, len); have_lower = true; }
     return lower;
   };
-  Blocks gblocks(content, len, rs.exclude_block);
+  Blocks gblocks(content, len, rs.exclude_block, plan, rs.rules.size());
   struct M { const Rule* rule; Loc loc; };
   std::vector<M> matched;
   size_t cand_i = 0;
@@ -784,7 +822,7 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
     if (kind == kPlanCandidates || kind == kPlanCandHostGate) use = starts ? starts : &kEmpty;
     find_locations(rs, rule, content, len, use, &locs, &out.error);
     if (locs.empty()) continue;
-    Blocks lblocks(content, len, rule.exclude_block);
+    Blocks lblocks(content, len, rule.exclude_block, plan, rs.rules.size() + rule.exclude_base);
     for (const Loc& l : locs) {
       if (l.start < 0) continue;                      // reference panics here (error flagged)
       if (gblocks.match(l) || lblocks.match(l)) continue;

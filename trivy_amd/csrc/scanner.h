@@ -28,6 +28,7 @@ struct Rule {                            // scanner.go:89-100
   RegexpPtr path;
   std::vector<AllowRule> allow_rules;
   std::vector<RegexpPtr> exclude_block;
+  uint32_t exclude_base = 0;             // exclude_block[j] has exclude id exclude_base + j
   std::string secret_group_name;
   std::vector<int> secret_groups;        // i with SubexpNames()[i] == SecretGroupName
 };
@@ -35,7 +36,11 @@ struct Rule {                            // scanner.go:89-100
 struct Ruleset {                         // scanner.go:45-49 (Global)
   std::vector<Rule> rules;
   std::vector<AllowRule> allow_rules;
-  std::vector<RegexpPtr> exclude_block;
+  std::vector<RegexpPtr> exclude_block;  // exclude ids [0, size)
+  // Every exclude-block regex (global ones, then each rule's in rule order)
+  // by exclude id.  The prefilter treats exclude id k as pseudo-rule
+  // rules.size() + k, so block locations come from GPU candidates too.
+  std::vector<const re::Regexp*> excludes;
 };
 
 // ParseConfig (already decoded from YAML to JSON) + NewScanner: builtin rules
@@ -89,8 +94,8 @@ struct RuleCandidates {
 };
 
 struct FilePlan {
-  std::vector<uint8_t> kind;             // one PlanKind per rule
-  std::vector<RuleCandidates> cands;     // sorted by rule
+  std::vector<uint8_t> kind;             // one PlanKind per rule, then one per exclude regex
+  std::vector<RuleCandidates> cands;     // sorted by rule (exclude regexes after the rules)
 };
 
 // Newline counts for findLocation without rescanning a file: K1's per-chunk
