@@ -83,6 +83,7 @@ typedef struct tsg_stats {
   uint32_t k1_blocks, k1_threads, chunk_bytes;
   int32_t table_in_lds;
   double gpu_wall_ms;   /* wall time of the GPU phase incl. launches, syncs and copies */
+  uint32_t pieces;      /* pipeline pieces the batch was cut into (GPU of piece i+1 || host of piece i) */
 } tsg_stats;
 
 const char* tsg_last_error(void);

@@ -64,3 +64,41 @@ def test_synthetic_parity_on_gpu(seed):
     assert sum(len(w["Findings"]) for w in want) > 20
     for a, g, w in zip(args, got, want):
         assert g == w, a.FilePath
+
+
+def test_pipelined_pieces_on_gpu(monkeypatch):
+    # a batch cut into pieces (GPU passes of piece i+1 overlapping the host
+    # confirmation of piece i) gives the one-piece result, through both the
+    # upload entry point and the HBM-resident one
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from oracle import secret_oracle as so
+    from trivy_amd import _lib, synth
+    c = synth.generate(3_000_000, seed=13, sizes="lognormal", plant_rate=3e-3, base_bytes=1 << 20)
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    ref = so.Scanner(None)
+    want = [ref.scan(a.FilePath, a.Content) for a in args]
+    monkeypatch.setenv("TSG_PIECES", "5")
+    monkeypatch.setenv("TSG_MIN_PIECE_BYTES", "1")
+    sc = S.Scanner(None)
+    got, stats = sc.ScanBatch(args, with_stats=True)
+    assert stats["pieces"] > 1
+    for a, g, w in zip(args, got, want):
+        assert g == w, a.FilePath
+    # resident: the corpus in HBM, piece starts 16-byte aligned inside it
+    L = _lib.lib()
+    d = torch.from_numpy(np.ascontiguousarray(c.data)).to("cuda:0")
+    paths, lens, _keep = _lib.pack_paths(c.paths)
+    res = ctypes.c_void_p()
+    _lib.check(L.tsg_scan_batch_resident(sc.engine(), ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
+                                         c.offsets.ctypes.data, len(c.paths), paths, lens, None, ctypes.byref(res)))
+    try:
+        got2 = _lib.result_json(res)
+    finally:
+        L.tsg_result_free(res)
+    for a, g, w in zip(args, got2, want):
+        g.pop("Error", None)
+        assert g == w, a.FilePath

@@ -20,7 +20,8 @@ class TsgStats(ctypes.Structure):
                 ("bytes", ctypes.c_uint64), ("files", ctypes.c_uint64), ("hits", ctypes.c_uint64),
                 ("candidates", ctypes.c_uint64), ("confirm_files", ctypes.c_uint64), ("findings", ctypes.c_uint64),
                 ("k1_blocks", ctypes.c_uint32), ("k1_threads", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
-                ("table_in_lds", ctypes.c_int32), ("gpu_wall_ms", ctypes.c_double)]
+                ("table_in_lds", ctypes.c_int32), ("gpu_wall_ms", ctypes.c_double),
+                ("pieces", ctypes.c_uint32)]
 
 
 # (name, restype, argtypes) for every entry point declared in include/trivy_secret.h

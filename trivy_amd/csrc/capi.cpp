@@ -295,6 +295,7 @@ int tsg_result_stats(const tsg_result* r, tsg_stats* out) {
   out->k1_blocks = s.k1_blocks; out->k1_threads = s.k1_threads; out->chunk_bytes = s.chunk_bytes;
   out->table_in_lds = s.table_in_lds;
   out->gpu_wall_ms = s.gpu_wall_ms;
+  out->pieces = s.pieces;
   return TSG_OK;
 }
 

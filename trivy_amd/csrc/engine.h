@@ -15,7 +15,7 @@ struct ScanStats {
   double k1_ms = 0, k2_ms = 0, h2d_ms = 0, d2h_ms = 0, host_ms = 0, total_ms = 0;
   double gpu_wall_ms = 0;               // run_gpu() wall time (launches + syncs + copies)
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, confirm_files = 0, findings = 0;
-  uint32_t k1_blocks = 0, k1_threads = 0, chunk_bytes = 0;
+  uint32_t k1_blocks = 0, k1_threads = 0, chunk_bytes = 0, pieces = 1;
   int table_in_lds = 0;
 };
 
@@ -51,10 +51,12 @@ class Engine {
   void set_threads(int n) { threads_ = n; }
 
   struct Impl;
+  struct GpuOut;
 
  private:
   Engine() = default;
-  bool run_gpu(const BatchInput& in, ScanStats* stats, std::string* err);
+  bool run_gpu(const BatchInput& in, ScanStats* stats, GpuOut* out, std::string* err);
+  void confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf, uint64_t* nfind);
   std::shared_ptr<const Ruleset> rs_;
   Prefilter pf_;
   int device_ = 0;

@@ -540,6 +540,12 @@ struct K1Group {
   bool in_lds = false;
 };
 
+struct Engine::GpuOut {
+  std::vector<CandDev> cands;   // (file, rule, start) candidates, unsorted
+  std::vector<uint32_t> nl;     // '\n' count per K1 chunk
+  std::vector<uint32_t> ff;     // per-file flags (fold-special content)
+};
+
 struct Engine::Impl {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
@@ -565,16 +571,17 @@ struct Engine::Impl {
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   unsigned int* d_cnt = nullptr;
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18;
-  // last batch results (host)
-  std::vector<CandDev> h_cands;
-  std::vector<uint32_t> h_nl;
+  // host copies of a piece's GPU results: two slots, so the GPU passes of
+  // piece i+1 overlap the host confirmation of piece i (Engine::scan)
   std::vector<uint32_t> h_kw;
-  std::vector<uint32_t> h_ff;
+  GpuOut out[2];
   std::unique_ptr<ThreadPool> pool;
   int sms = 256;
   int k1_streams = 1;                 // interleaved DFA streams per K1 lane  } TSG_K1_CFG="threads,streams"
   uint32_t k1_threads = 1024;         // K1 workgroup size                  }
   uint32_t chunk = 4096;              // bytes per K1 stream chunk (multiple of 128; TSG_K1_CHUNK)
+  uint32_t pieces = 4;                // pipeline pieces per batch (TSG_PIECES)
+  uint64_t min_piece = 256ull << 20;  // smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
 };
 
 int device_count() {
@@ -599,6 +606,14 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
     const long v = std::atol(c);
     if (v >= 256 && v % 128 == 0) m.chunk = static_cast<uint32_t>(v);
+  }
+  if (const char* c = std::getenv("TSG_PIECES")) {
+    const long v = std::atol(c);
+    if (v >= 1 && v <= 64) m.pieces = static_cast<uint32_t>(v);
+  }
+  if (const char* c = std::getenv("TSG_MIN_PIECE_BYTES")) {
+    const long long v = std::atoll(c);
+    if (v >= 1) m.min_piece = static_cast<uint64_t>(v);
   }
   if (const char* cfg = std::getenv("TSG_K1_CFG")) {
     unsigned t = 0, k = 0;
@@ -712,7 +727,7 @@ Engine::~Engine() {
   if (m.stream) hipStreamDestroy(m.stream);
 }
 
-bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
+bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::string* err) {
   Impl& m = *impl_;
   HIP_OK(hipSetDevice(device_));
   const uint64_t total = in.offsets[in.nfiles] - in.offsets[0];
@@ -834,12 +849,12 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, std::string* err) {
       st->k2_ms += k2;
       if (c2 > m.cand_cap) { m.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
       auto t_d2h = std::chrono::steady_clock::now();
-      m.h_cands.resize(c2);
-      if (c2) HIP_OK(hipMemcpyAsync(m.h_cands.data(), m.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, m.stream));
-      m.h_ff.resize(in.nfiles);
-      if (in.nfiles) HIP_OK(hipMemcpyAsync(m.h_ff.data(), m.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
-      m.h_nl.resize(nchunks);
-      if (nchunks) HIP_OK(hipMemcpyAsync(m.h_nl.data(), m.d_nl, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+      out->cands.resize(c2);
+      if (c2) HIP_OK(hipMemcpyAsync(out->cands.data(), m.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, m.stream));
+      out->ff.resize(in.nfiles);
+      if (in.nfiles) HIP_OK(hipMemcpyAsync(out->ff.data(), m.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+      out->nl.resize(nchunks);
+      if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), m.d_nl, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
       HIP_OK(hipStreamSynchronize(m.stream));
       st->d2h_ms += ms_since(t_d2h);
       st->candidates = c2;
@@ -857,8 +872,8 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
                             std::string* err) {
   ScanStats local;
   if (!st) st = &local;
-  if (!run_gpu(in, st, err)) return false;
   Impl& m = *impl_;
+  if (!run_gpu(in, st, &m.out[0], err)) return false;
   const size_t nr = rs_->rules.size();   // real rules only (exclude pseudo-rules follow)
   if (kw_gate) {
     m.h_kw.resize(static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * m.kw_words);
@@ -878,7 +893,7 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
   }
   if (cands) {
     cands->assign(in.nfiles, std::vector<std::vector<uint64_t>>(nr));
-    for (const CandDev& c : m.h_cands)
+    for (const CandDev& c : m.out[0].cands)
       if (c.rule < nr) (*cands)[c.file][c.rule].push_back(c.start);
     for (auto& f : *cands)
       for (auto& v : f) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); }
@@ -886,29 +901,25 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
   return true;
 }
 
-bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* st, std::string* err) {
-  ScanStats local;
-  if (!st) st = &local;
-  auto t0 = std::chrono::steady_clock::now();
-  if (!run_gpu(in, st, err)) return false;
-  auto t_host = std::chrono::steady_clock::now();
-  st->gpu_wall_ms = ms_since(t0);
+// Host confirmation of one piece (files [0, in.nfiles) of `in`, results into
+// results[0..nfiles)) from that piece's GPU output `g`.
+void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf_out,
+                           uint64_t* nfind_out) {
   Impl& m = *impl_;
   const Ruleset& rs = *rs_;
   const size_t nr = rs.rules.size();
   const size_t nplan = pf_.rules.size();   // rules + exclude-block pseudo-rules
   // group candidates per file (counting sort by file, then sort each file's list)
   std::vector<uint32_t> per_file(in.nfiles + 1, 0);
-  for (const CandDev& c : m.h_cands) per_file[c.file + 1]++;
+  for (const CandDev& c : g.cands) per_file[c.file + 1]++;
   for (uint32_t f = 0; f < in.nfiles; ++f) per_file[f + 1] += per_file[f];
-  std::vector<CandDev> sorted(m.h_cands.size());
+  std::vector<CandDev> sorted(g.cands.size());
   {
     std::vector<uint32_t> pos(per_file.begin(), per_file.end() - 1);
-    for (const CandDev& c : m.h_cands) sorted[pos[c.file]++] = c;
+    for (const CandDev& c : g.cands) sorted[pos[c.file]++] = c;
   }
   bool any_full = false;
   for (size_t r = 0; r < nr; ++r) if (pf_.rules[r].mode == 1) any_full = true;
-  results->assign(in.nfiles, Secret());
   // largest files first (LPT): the per-file confirm cost grows with size
   std::vector<uint32_t> work(in.nfiles);
   for (uint32_t f = 0; f < in.nfiles; ++f) work[f] = f;
@@ -929,7 +940,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       const size_t len = in.offsets[f + 1] - in.offsets[f];
       const bool binary = in.binary ? in.binary[f] != 0 : false;
       const uint32_t cb = per_file[f], ce = per_file[f + 1];
-      if (m.h_ff[f]) {
+      if (g.ff[f]) {
         // fold-special file (U+0130/U+212A/U+017F present): the two passes run
         // on the host with the variant scan DFA, then the exact confirmer
         nconf.fetch_add(1);
@@ -939,7 +950,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         plan_from_candidates(pf_, &vc, &plan);
         Secret s = scan_file(rs, path, content, len, binary, &plan);
         nfind.fetch_add(s.findings.size());
-        (*results)[f] = std::move(s);
+        results[f] = std::move(s);
         continue;
       }
       if (cb == ce && !any_full) {
@@ -948,7 +959,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         for (const auto& a : rs.allow_rules) {
           if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) { s.file_path = path; break; }
         }
-        (*results)[f] = std::move(s);
+        results[f] = std::move(s);
         continue;
       }
       nconf.fetch_add(1);
@@ -974,21 +985,105 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         plan.cands.push_back(std::move(rc));
       }
       NlSource nls;
-      nls.chunk_nl = m.h_nl.data();
+      nls.chunk_nl = g.nl.data();
       nls.data = in.h_data;
       nls.file_off = in.offsets[f];
       nls.chunk = m.chunk;
       Secret s = scan_file(rs, path, content, len, binary, &plan, &nls);
       nfind.fetch_add(s.findings.size());
-      (*results)[f] = std::move(s);
+      results[f] = std::move(s);
     }
   };
   int nt = threads_ > 0 ? threads_ : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
   if (!m.pool || m.pool->size() != nt) m.pool.reset(new ThreadPool(nt));
   m.pool->run([&](int) { worker(); });
-  st->host_ms = ms_since(t_host);
-  st->confirm_files = nconf.load();
-  st->findings = nfind.load();
+  *nconf_out += nconf.load();
+  *nfind_out += nfind.load();
+}
+
+// A batch is cut into pieces at file boundaries (about equal bytes each).  The
+// GPU passes of piece i+1 run on a driver thread while the host pool confirms
+// piece i: the step costs ~max(GPU, host) + one piece of the other, instead of
+// their sum.  Each piece is a self-contained batch (offsets rebased to 0, its
+// device data a 16-byte aligned sub-range of the batch), so the kernels are
+// unchanged and the result equals the one-piece scan.
+bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* st, std::string* err) {
+  ScanStats local;
+  if (!st) st = &local;
+  auto t0 = std::chrono::steady_clock::now();
+  Impl& m = *impl_;
+  const uint64_t total = in.nfiles ? in.offsets[in.nfiles] - in.offsets[0] : 0;
+  if (in.offsets && in.offsets[0] != 0) { *err = "offsets[0] must be 0"; return false; }
+  uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(m.pieces, std::max<uint64_t>(1, total / m.min_piece)));
+  // piece boundaries: file indices, each piece start 16-byte aligned within the batch
+  std::vector<uint32_t> cut{0};
+  for (uint32_t p = 1; p < want; ++p) {
+    const uint64_t target = total / want * p;
+    uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
+    while (in.d_data && f < in.nfiles && (in.offsets[f] & 15) != 0) ++f;   // resident data: aligned piece starts
+    if (f > cut.back() && f < in.nfiles) cut.push_back(f);
+  }
+  cut.push_back(in.nfiles);
+  const size_t np = cut.size() - 1;
+  results->assign(in.nfiles, Secret());
+  std::vector<BatchInput> piece(np);
+  std::vector<std::vector<uint64_t>> poff(np);
+  std::vector<ScanStats> pst(np);
+  for (size_t p = 0; p < np; ++p) {
+    const uint32_t a = cut[p], b = cut[p + 1];
+    BatchInput& q = piece[p];
+    q = in;
+    const uint64_t base = in.offsets[a];
+    if (np > 1) {
+      poff[p].resize(b - a + 1);
+      for (uint32_t f = a; f <= b; ++f) poff[p][f - a] = in.offsets[f] - base;
+      q.offsets = poff[p].data();
+    }
+    q.nfiles = b - a;
+    q.h_data = in.h_data ? in.h_data + base : nullptr;
+    q.d_data = in.d_data ? static_cast<const uint8_t*>(in.d_data) + base : nullptr;
+    q.paths = in.paths ? in.paths + a : nullptr;
+    q.path_lens = in.path_lens ? in.path_lens + a : nullptr;
+    q.binary = in.binary ? in.binary + a : nullptr;
+  }
+  uint64_t nconf = 0, nfind = 0;
+  double gpu_ms = 0, host_ms = 0;
+  auto tg = std::chrono::steady_clock::now();
+  if (!run_gpu(piece[0], &pst[0], &m.out[0], err)) return false;
+  gpu_ms += ms_since(tg);
+  for (size_t p = 0; p < np; ++p) {
+    std::thread gpu;
+    bool ok_next = true;
+    std::string err_next;
+    double next_ms = 0;
+    if (p + 1 < np) {
+      gpu = std::thread([&, p]() {
+        auto t = std::chrono::steady_clock::now();
+        ok_next = run_gpu(piece[p + 1], &pst[p + 1], &m.out[(p + 1) & 1], &err_next);
+        next_ms = ms_since(t);
+      });
+    }
+    auto th = std::chrono::steady_clock::now();
+    confirm_piece(piece[p], m.out[p & 1], results->data() + cut[p], &nconf, &nfind);
+    host_ms += ms_since(th);
+    if (gpu.joinable()) gpu.join();
+    gpu_ms += next_ms;
+    if (!ok_next) { *err = err_next; return false; }
+  }
+  *st = ScanStats();
+  for (const ScanStats& s : pst) {
+    st->k1_ms += s.k1_ms; st->k2_ms += s.k2_ms; st->h2d_ms += s.h2d_ms; st->d2h_ms += s.d2h_ms;
+    st->hits += s.hits; st->candidates += s.candidates;
+    st->k1_blocks = s.k1_blocks; st->k1_threads = s.k1_threads; st->chunk_bytes = s.chunk_bytes;
+    st->table_in_lds = s.table_in_lds;
+  }
+  st->bytes = total;
+  st->files = in.nfiles;
+  st->pieces = static_cast<uint32_t>(np);
+  st->gpu_wall_ms = gpu_ms;
+  st->host_ms = host_ms;
+  st->confirm_files = nconf;
+  st->findings = nfind;
   st->total_ms = ms_since(t0);
   return true;
 }
