@@ -172,6 +172,12 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out);
 int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
                     int64_t* dfa_end, int64_t* vm_end);
 
+/* Test hook: Regexp.MatchString(text) for `pattern` with the required-literal
+ * gate the ruleset compiler sets on path / allow regexes (*gated) and without
+ * it (*plain); *has_gate = 1 if a gate was found (2: bounded). */
+int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, int* gated, int* plain,
+                          int* has_gate);
+
 #ifdef __cplusplus
 }
 #endif

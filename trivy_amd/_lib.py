@@ -70,6 +70,9 @@ SIGNATURES = [
                                              c_char_pp, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_prefilter_report", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_regex_match_probe", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_int)]),
     ("tsg_regex_probe", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                         ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
 ]

@@ -387,6 +387,25 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
 
 const char* tsg_builtin_rules_json(void) { return tsg_builtin_json_ptr(); }
 
+int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, int* gated, int* plain,
+                          int* has_gate) {
+  if (!pattern || (len && !text) || !gated || !plain || !has_gate) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string err;
+  auto rx = re::Regexp::compile(pattern, &err);
+  if (!rx) return fail(TSG_ERR_CONFIG, err);
+  *plain = rx->match_string(text, len) ? 1 : 0;
+  re::LitGate g;
+  bool bounded = false;
+  uint32_t dmin = 0, dmax = 0;
+  *has_gate = 0;
+  if (literal_gate(*rx->ast(), &g, &bounded, &dmin, &dmax)) {
+    rx->set_gate(std::move(g), bounded, dmin, dmax);
+    *has_gate = bounded ? 2 : 1;
+  }
+  *gated = rx->match_string(text, len) ? 1 : 0;
+  return TSG_OK;
+}
+
 int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
                     int64_t* dfa_end, int64_t* vm_end) {
   if (!pattern || (len && !text) || (n && (!pos || !dfa_end || !vm_end))) return fail(TSG_ERR_INVALID, "NULL argument");

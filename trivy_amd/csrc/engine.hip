@@ -580,7 +580,9 @@ struct Engine::Impl {
   int k1_streams = 1;                 // interleaved DFA streams per K1 lane  } TSG_K1_CFG="threads,streams"
   uint32_t k1_threads = 1024;         // K1 workgroup size                  }
   uint32_t chunk = 4096;              // bytes per K1 stream chunk (multiple of 128; TSG_K1_CHUNK)
-  uint32_t pieces = 4;                // pipeline pieces per batch (TSG_PIECES)
+  uint32_t pieces = 2;                // pipeline pieces per batch (TSG_PIECES)
+  double first_piece = 0.6;           // share of the first piece (TSG_FIRST_PIECE): the host idles
+                                      // through piece 0's GPU passes, the GPU through the last confirm
   uint64_t min_piece = 256ull << 20;  // smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
 };
 
@@ -610,6 +612,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   if (const char* c = std::getenv("TSG_PIECES")) {
     const long v = std::atol(c);
     if (v >= 1 && v <= 64) m.pieces = static_cast<uint32_t>(v);
+  }
+  if (const char* c = std::getenv("TSG_FIRST_PIECE")) {
+    const double v = std::atof(c);
+    if (v > 0.0 && v < 1.0) m.first_piece = v;
   }
   if (const char* c = std::getenv("TSG_MIN_PIECE_BYTES")) {
     const long long v = std::atoll(c);
@@ -1018,7 +1024,9 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   // piece boundaries: file indices, each piece start 16-byte aligned within the batch
   std::vector<uint32_t> cut{0};
   for (uint32_t p = 1; p < want; ++p) {
-    const uint64_t target = total / want * p;
+    // piece 0 takes first_piece of the bytes, the others share the rest
+    const double share = p == 0 ? 0.0 : m.first_piece + (1.0 - m.first_piece) * (p - 1) / (want - 1);
+    const uint64_t target = static_cast<uint64_t>(share * static_cast<double>(total));
     uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
     while (in.d_data && f < in.nfiles && (in.offsets[f] & 15) != 0) ++f;   // resident data: aligned piece starts
     if (f > cut.back() && f < in.nfiles) cut.push_back(f);

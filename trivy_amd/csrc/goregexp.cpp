@@ -1250,9 +1250,58 @@ long Regexp::match_end(const uint8_t* text, size_t len, size_t pos) const {
   return e;
 }
 
+// Length of the gate sequence `seq` occurring at text[i..] (0: none there).
+static size_t seq_at(const std::vector<std::vector<std::string>>& seq, const uint8_t* text, size_t len, size_t i) {
+  size_t p = i;
+  for (const auto& unit : seq) {
+    bool any = false;
+    for (const auto& alt : unit) {
+      // alternatives of a unit are whole runes (1-byte ASCII or a complete
+      // UTF-8 sequence): none is a proper prefix of another
+      if (p + alt.size() <= len && std::memcmp(text + p, alt.data(), alt.size()) == 0) {
+        p += alt.size();
+        any = true;
+        break;
+      }
+    }
+    if (!any) return 0;
+  }
+  return p - i;
+}
+
 bool Regexp::match_string(const uint8_t* text, size_t len) const {
-  std::vector<int> caps(2 * (prog_.num_cap + 1));
-  return match_at(text, len, 0, false, 0, caps.data());
+  if (gate_.empty()) {
+    std::vector<int> caps(2 * (prog_.num_cap + 1));
+    return match_at(text, len, 0, false, 0, caps.data());
+  }
+  auto hit_at = [&](size_t i) {
+    if (!gate_first_[text[i]]) return false;
+    for (const auto& seq : gate_) if (seq_at(seq, text, len, i)) return true;
+    return false;
+  };
+  if (!gate_bounded_) {
+    for (size_t i = 0; i < len; ++i) {
+      if (hit_at(i)) {
+        std::vector<int> caps(2 * (prog_.num_cap + 1));
+        return match_at(text, len, 0, false, 0, caps.data());
+      }
+    }
+    return false;                                  // no gate literal: no match can exist
+  }
+  // every match starts gate_dmin_..gate_dmax_ bytes before a gate literal
+  std::vector<uint8_t> tried;
+  std::vector<int> caps;
+  for (size_t i = gate_dmin_; i < len; ++i) {
+    if (!hit_at(i)) continue;
+    if (tried.empty()) { tried.assign(len + 1, 0); caps.resize(2 * (prog_.num_cap + 1)); }
+    const size_t lo = i >= gate_dmax_ ? i - gate_dmax_ : 0, hi = i - gate_dmin_;
+    for (size_t s0 = lo; s0 <= hi; ++s0) {
+      if (tried[s0]) continue;
+      tried[s0] = 1;
+      if (match_at(text, len, s0, true, 0, caps.data())) return true;
+    }
+  }
+  return false;
 }
 
 void Regexp::find_all(const uint8_t* text, size_t len, bool submatch, std::vector<int>* out) const {

@@ -104,6 +104,10 @@ bool is_print(uint32_t r);
 // Append UTF-8 encoding of rune r.
 void append_utf8(std::string* out, uint32_t r);
 
+// Required-literal gate: alternatives of literal sequences (each unit a set of
+// alternative byte strings); every match of the regexp contains at least one.
+using LitGate = std::vector<std::vector<std::vector<std::string>>>;
+
 class Regexp {
  public:
   // Returns nullptr and sets *err on a syntax error (Go: "error parsing regexp: ...").
@@ -124,8 +128,18 @@ class Regexp {
   // End offset of the leftmost-first match anchored at `pos` (-1: none),
   // from a lazily built DFA (no captures); equals match_at(.., true, ..)'s caps[1].
   long match_end(const uint8_t* text, size_t len, size_t pos) const;
-  // Regexp.MatchString
+  // Regexp.MatchString (with a gate set: false without running the VM when
+  // no gate literal occurs in the text -- no match can exist then)
   bool match_string(const uint8_t* text, size_t len) const;
+  // bounded gate: every match starts dmin..dmax bytes before a gate literal,
+  // so only those starts are tried (anchored)
+  void set_gate(LitGate g, bool bounded = false, uint32_t dmin = 0, uint32_t dmax = 0) {
+    gate_ = std::move(g); gate_bounded_ = bounded; gate_dmin_ = dmin; gate_dmax_ = dmax;
+    for (auto& f : gate_first_) f = 0;
+    for (const auto& seq : gate_)
+      for (const auto& alt : seq[0]) gate_first_[static_cast<uint8_t>(alt[0])] = 1;
+  }
+  const LitGate& gate() const { return gate_; }
   // Regexp.FindAll(Submatch)Index(text, -1): flattened vectors of 2 (or 2*(ncap+1)) ints.
   void find_all(const uint8_t* text, size_t len, bool submatch, std::vector<int>* out) const;
   // Minimal byte length of a match (used by the prefilter to reject nullable rules).
@@ -138,6 +152,10 @@ class Regexp {
   std::vector<std::string> names_;
   bool nullable_ = false;
   uint64_t id_ = 0;
+  LitGate gate_;
+  uint8_t gate_first_[256] = {};    // first bytes of the gate literals
+  bool gate_bounded_ = false;
+  uint32_t gate_dmin_ = 0, gate_dmax_ = 0;
 };
 
 }  // namespace re

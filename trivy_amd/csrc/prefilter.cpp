@@ -860,6 +860,27 @@ bool k1_fits(const ScanDfa& d) {
          kK1HitLdsBytes + k1_lds_table_bytes(d) <= kK1LdsBytes;
 }
 
+bool literal_gate(const re::Node& ast, re::LitGate* out, bool* bounded, uint32_t* dmin, uint32_t* dmax) {
+  std::vector<const Node*> items;
+  flatten(ast, &items);
+  for (bool b : {true, false}) {
+    out->clear();
+    AnchorChoice a = choose_anchor(items, b);
+    if (!a.ok) continue;
+    for (const Seq& raw : a.raw) {
+      Seq f = scan_form(raw, /*keep_special=*/true);   // ASCII case-folded superset, fold runes kept
+      if (f.empty()) { out->clear(); break; }
+      out->push_back(f);
+    }
+    if (out->empty()) continue;
+    *bounded = b;
+    *dmin = a.dmin;
+    *dmax = a.dmax;
+    return true;
+  }
+  return false;
+}
+
 bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
   *pf = Prefilter();
   // --- keywords: distinct ASCII lowered keywords get a GPU pattern id

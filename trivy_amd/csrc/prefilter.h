@@ -90,6 +90,12 @@ struct Prefilter {
 
 bool build_prefilter(const Ruleset& rs, Prefilter* out, std::string* err);
 
+// Required-literal gate of a regexp (false: none found): every match contains
+// one of the sequences.  Set on path / allow regexes so MatchString skips the
+// VM on texts that contain none (scanner.go's per-file AllowPath/MatchPath).
+// Bounded (*bounded): every match starts *dmin..*dmax bytes before one.
+bool literal_gate(const re::Node& ast, re::LitGate* out, bool* bounded, uint32_t* dmin, uint32_t* dmax);
+
 // CPU model of the two GPU passes (used by unit tests to check the compiled
 // tables without a GPU, never by the product path): returns per-rule sorted
 // candidate starts and keyword-gate bits for one file.

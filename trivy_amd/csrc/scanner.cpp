@@ -1,5 +1,6 @@
 // Exact restatement of pkg/fanal/secret/scanner.go on the host (see scanner.h).
 #include "scanner.h"
+#include "prefilter.h"
 
 #include <algorithm>
 #include <cstring>
@@ -21,6 +22,10 @@ RegexpPtr compile_or_err(const JValue* v, std::string* err) {
     if (err->empty()) *err = "regexp compile error: " + e;
     return nullptr;
   }
+  re::LitGate g;
+  bool bounded = false;
+  uint32_t dmin = 0, dmax = 0;
+  if (literal_gate(*re->ast(), &g, &bounded, &dmin, &dmax)) re->set_gate(std::move(g), bounded, dmin, dmax);
   return RegexpPtr(re.release());
 }
 
