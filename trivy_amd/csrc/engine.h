@@ -56,7 +56,8 @@ class Engine {
  private:
   Engine() = default;
   bool run_gpu(const BatchInput& in, ScanStats* stats, GpuOut* out, std::string* err);
-  void confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf, uint64_t* nfind);
+  void confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf, uint64_t* nfind,
+                     bool gpu_in_flight);
   std::shared_ptr<const Ruleset> rs_;
   Prefilter pf_;
   int device_ = 0;

@@ -544,6 +544,7 @@ struct Engine::GpuOut {
   std::vector<CandDev> cands;   // (file, rule, start) candidates, unsorted
   std::vector<uint32_t> nl;     // '\n' count per K1 chunk
   std::vector<uint32_t> ff;     // per-file flags (fold-special content)
+  uint32_t chunk = 0;           // K1 chunk bytes of this piece (nl[] granularity)
 };
 
 struct Engine::Impl {
@@ -579,9 +580,11 @@ struct Engine::Impl {
   int sms = 256;
   int k1_streams = 1;                 // interleaved DFA streams per K1 lane  } TSG_K1_CFG="threads,streams"
   uint32_t k1_threads = 1024;         // K1 workgroup size                  }
-  uint32_t chunk = 4096;              // bytes per K1 stream chunk (multiple of 128; TSG_K1_CHUNK)
+  uint32_t chunk = 4096;              // max bytes per K1 stream chunk (multiple of 128; TSG_K1_CHUNK)
+  bool adaptive_chunk = false;        // shrink the chunk to balance the last round (TSG_K1_ADAPTIVE=1; measured
+                                      // slower on MI355X: 3840-B chunks ran K1 at 1.6 vs 2.07 TB/s)
   uint32_t pieces = 2;                // pipeline pieces per batch (TSG_PIECES)
-  double first_piece = 0.6;           // share of the first piece (TSG_FIRST_PIECE): the host idles
+  double first_piece = 0.7;           // share of the first piece (TSG_FIRST_PIECE): the host idles
                                       // through piece 0's GPU passes, the GPU through the last confirm
   uint64_t min_piece = 256ull << 20;  // smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
 };
@@ -613,6 +616,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
     const long v = std::atol(c);
     if (v >= 1 && v <= 64) m.pieces = static_cast<uint32_t>(v);
   }
+  if (const char* c = std::getenv("TSG_K1_ADAPTIVE")) m.adaptive_chunk = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_FIRST_PIECE")) {
     const double v = std::atof(c);
     if (v > 0.0 && v < 1.0) m.first_piece = v;
@@ -743,8 +747,19 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
   }
   st->bytes = total;
   st->files = in.nfiles;
-  const uint32_t kChunk = m.chunk;
+  // chunk size: at most m.chunk, shrunk so that every lane of the one-
+  // workgroup-per-CU grid gets the same whole number R of chunks (a launch
+  // lasts R chunk-times; a fixed chunk leaves the last round part-empty)
+  uint32_t kChunk = m.chunk;
+  if (m.adaptive_chunk) {
+    const uint64_t lanes = static_cast<uint64_t>(m.sms) * m.k1_threads * static_cast<uint64_t>(m.k1_streams);
+    const uint64_t per_lane = (total + lanes - 1) / std::max<uint64_t>(lanes, 1);
+    const uint64_t rounds = std::max<uint64_t>(1, (per_lane + m.chunk - 1) / m.chunk);
+    const uint64_t c = ((per_lane + rounds - 1) / rounds + 127) / 128 * 128;
+    kChunk = static_cast<uint32_t>(std::min<uint64_t>(m.chunk, std::max<uint64_t>(1024, c)));
+  }
   st->chunk_bytes = kChunk;
+  out->chunk = kChunk;
   const uint8_t* d_data = static_cast<const uint8_t*>(in.d_data);
   auto t_h2d = std::chrono::steady_clock::now();
   if (!d_data) {
@@ -791,13 +806,21 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
     const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
     uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(m.hit_cap / nregions, 0xffffffffu));
     HIP_OK(hipMemsetAsync(m.d_bh, 0, nregions * sizeof(uint32_t), m.stream));
+    auto k1_lds = [&](const K1Group& g) {
+      return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
+             (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
+    };
+    for (uint32_t gi = 0; gi < ngroups; ++gi) {
+      const K1Group& g = m.k1g[gi];
+      const void* kfn = k1_kernel(g.in_lds, nthr, ks);
+      if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
+      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(k1_lds(g))));
+    }
     HIP_OK(hipEventRecord(m.ev[0], m.stream));
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = m.k1g[gi];
-      const size_t lds = (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 + (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
+      const size_t lds = k1_lds(g);
       const void* kfn = k1_kernel(g.in_lds, nthr, ks);
-      if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
-      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
       uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
@@ -910,7 +933,7 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
 // Host confirmation of one piece (files [0, in.nfiles) of `in`, results into
 // results[0..nfiles)) from that piece's GPU output `g`.
 void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf_out,
-                           uint64_t* nfind_out) {
+                           uint64_t* nfind_out, bool gpu_in_flight) {
   Impl& m = *impl_;
   const Ruleset& rs = *rs_;
   const size_t nr = rs.rules.size();
@@ -926,15 +949,44 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
   }
   bool any_full = false;
   for (size_t r = 0; r < nr; ++r) if (pf_.rules[r].mode == 1) any_full = true;
-  // largest files first (LPT): the per-file confirm cost grows with size
-  std::vector<uint32_t> work(in.nfiles);
-  for (uint32_t f = 0; f < in.nfiles; ++f) work[f] = f;
+  // files to confirm (candidates, fold-special content, or host-evaluated
+  // rules), largest first (LPT: the per-file confirm cost grows with size);
+  // every other file only needs the global allow-path outcome and is handled
+  // in blocks after them (image layers: hundreds of thousands of such files)
+  std::vector<uint32_t> work, light;
+  work.reserve(in.nfiles / 4 + 16);
+  for (uint32_t f = 0; f < in.nfiles; ++f) {
+    if (any_full || g.ff[f] || per_file[f] != per_file[f + 1]) work.push_back(f);
+    else light.push_back(f);
+  }
   std::sort(work.begin(), work.end(), [&](uint32_t a, uint32_t b) {
     const uint64_t sa = in.offsets[a + 1] - in.offsets[a], sb = in.offsets[b + 1] - in.offsets[b];
     return sa != sb ? sa > sb : a < b;
   });
+  constexpr uint32_t kLightBlock = 512;
+  const uint32_t nlight_blocks = static_cast<uint32_t>((light.size() + kLightBlock - 1) / kLightBlock);
+  std::atomic<uint32_t> next_light{0};
   std::atomic<uint32_t> next{0};
   std::atomic<uint64_t> nfind{0}, nconf{0};
+  auto light_files = [&]() {
+    std::string path;
+    for (;;) {
+      const uint32_t b = next_light.fetch_add(1);
+      if (b >= nlight_blocks) break;
+      const size_t e = std::min<size_t>(light.size(), (static_cast<size_t>(b) + 1) * kLightBlock);
+      for (size_t k = static_cast<size_t>(b) * kLightBlock; k < e; ++k) {
+        const uint32_t f = light[k];
+        // no candidates, no host-evaluated rule: only the global allow-path outcome remains
+        if (in.path_lens) path.assign(in.paths[f], in.path_lens[f]); else path.assign(in.paths[f]);
+        for (const auto& a : rs.allow_rules) {
+          if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) {
+            results[f].file_path = path;
+            break;
+          }
+        }
+      }
+    }
+  };
   auto worker = [&]() {
     FilePlan plan;
     for (;;) {
@@ -956,15 +1008,6 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
         plan_from_candidates(pf_, &vc, &plan);
         Secret s = scan_file(rs, path, content, len, binary, &plan);
         nfind.fetch_add(s.findings.size());
-        results[f] = std::move(s);
-        continue;
-      }
-      if (cb == ce && !any_full) {
-        // no candidates, no host-evaluated rule: only the global allow-path outcome remains
-        Secret s;
-        for (const auto& a : rs.allow_rules) {
-          if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) { s.file_path = path; break; }
-        }
         results[f] = std::move(s);
         continue;
       }
@@ -994,7 +1037,7 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
       nls.chunk_nl = g.nl.data();
       nls.data = in.h_data;
       nls.file_off = in.offsets[f];
-      nls.chunk = m.chunk;
+      nls.chunk = g.chunk;
       Secret s = scan_file(rs, path, content, len, binary, &plan, &nls);
       nfind.fetch_add(s.findings.size());
       results[f] = std::move(s);
@@ -1002,7 +1045,14 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
   };
   int nt = threads_ > 0 ? threads_ : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
   if (!m.pool || m.pool->size() != nt) m.pool.reset(new ThreadPool(nt));
-  m.pool->run([&](int) { worker(); });
+  // while the next piece's GPU passes are in flight one core stays with the
+  // thread driving them (a preempted driver thread stalls the GPU)
+  const int active = gpu_in_flight && nt > 1 ? nt - 1 : nt;
+  m.pool->run([&](int idx) {
+    if (idx >= active) return;
+    worker();
+    light_files();
+  });
   *nconf_out += nconf.load();
   *nfind_out += nfind.load();
 }
@@ -1072,7 +1122,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       });
     }
     auto th = std::chrono::steady_clock::now();
-    confirm_piece(piece[p], m.out[p & 1], results->data() + cut[p], &nconf, &nfind);
+    confirm_piece(piece[p], m.out[p & 1], results->data() + cut[p], &nconf, &nfind, gpu.joinable());
     host_ms += ms_since(th);
     if (gpu.joinable()) gpu.join();
     gpu_ms += next_ms;
