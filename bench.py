@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=16)
     ap.add_argument("--cpu-sample-mb", type=float, default=1200.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host batch) measurement")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -265,6 +266,29 @@ def main():
         "cpu_baseline": None,
         "parity": None,
     }
+
+    if rank == 0 and world == 1 and not args.no_pcie:
+        # PCIe-inclusive rate (reported, never `value`): the same batch handed
+        # over in pinned host memory through tsg_scan_batch, which uploads each
+        # pipeline piece while the host confirms the previous one
+        hp = ctypes.c_void_p()
+        _lib.check(L.tsg_alloc_pinned(corpus.nbytes + 64, ctypes.byref(hp)))
+        try:
+            ctypes.memmove(hp, h_ptr, corpus.nbytes)
+            times = []
+            for k in range(2):
+                t0 = time.perf_counter()
+                res = ctypes.c_void_p()
+                _lib.check(L.tsg_scan_batch(eng, hp, off_ptr, nfiles, paths, lens, None, ctypes.byref(res)))
+                times.append(time.perf_counter() - t0)
+                if k == 1:
+                    pc = _lib.result_json(res)
+                    out["host_feed"]["pcie_inclusive_same_findings"] = pc == gpu_results
+                L.tsg_result_free(res)
+            out["host_feed"]["pcie_inclusive_gbps"] = round(corpus.nbytes / times[-1] / 1e9, 2)
+            log("PCIe-inclusive (pinned host batch -> tsg_scan_batch): %.1f GB/s" % (corpus.nbytes / times[-1] / 1e9))
+        finally:
+            L.tsg_free_pinned(hp)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # config 5's exclude blocks make the oracle's backtracking engine
