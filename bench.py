@@ -262,7 +262,8 @@ def main():
                          "candidates": stats[-1]["candidates"], "confirm_files": stats[-1]["confirm_files"],
                          "findings": findings, "rules_with_findings": len(rules_hit)},
         "host_feed": {"h2d_pinned_gbps": round(h2d_gbps, 2),
-                      "note": "PCIe-inclusive path (tsg_scan_batch from host buffers) is bounded by this rate"},
+                      "note": "h2d_pinned_gbps: one torch copy of a <= 4 GB pinned slice; pcie_inclusive_gbps: the "
+                              "whole batch from pinned host memory through tsg_scan_batch (uploads overlap confirmation)"},
         "cpu_baseline": None,
         "parity": None,
     }

@@ -14,5 +14,5 @@ cat $OUT/smoke.log
 timeout -k 10 400 python bench.py --json-out $OUT/bench.json > $OUT/bench.out 2> $OUT/bench.log || exit $?
 cat $OUT/bench.log
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof -o run -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $ROOT/$OUT/prof.log 2>&1 || exit $?
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof -o run -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pcie > $ROOT/$OUT/prof.log 2>&1 || exit $?
 cd $ROOT && find $OUT/prof -name '*.db' -o -name '*stats*' | head
