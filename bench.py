@@ -268,6 +268,23 @@ def main():
         "parity": None,
     }
 
+    if rank == 0:
+        # host feed: batched Required + IsBinary + CR strip (tsg_prepare_batch)
+        # over the same files as read (reported beside the scan, never `value`)
+        hpb = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        _lib.check(L.tsg_prepare_batch(sc._rs, None, h_ptr, off_ptr, nfiles, paths, lens, args.threads,
+                                       ctypes.byref(hpb)))
+        tprep = time.perf_counter() - t0
+        d_, o_, i_, b_, nk = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint32()
+        _lib.check(L.tsg_prepared_view(hpb, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_), ctypes.byref(b_),
+                                       ctypes.byref(nk)))
+        L.tsg_prepared_free(hpb)
+        out["host_feed"]["prepare_gbps"] = round(corpus.nbytes / tprep / 1e9, 2)
+        out["host_feed"]["prepare_kept_files"] = nk.value
+        log("host feed prepare (Required + IsBinary + CR strip, %d threads): %.1f GB/s, %d of %d files kept" % (
+            args.threads, corpus.nbytes / tprep / 1e9, nk.value, nfiles))
+
     if rank == 0 and world == 1 and not args.no_pcie:
         # PCIe-inclusive rate (reported, never `value`): the same batch handed
         # over in pinned host memory through tsg_scan_batch, which uploads each

@@ -172,6 +172,25 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out);
 int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
                     int64_t* dfa_end, int64_t* vm_end);
 
+/* ---- host feed ----
+ * Batched SecretAnalyzer.Required + Analyze content preparation, replacing the
+ * per-file analyzer calls of pkg/fanal/analyzer/secret/secret.go:103-190
+ * (Required: size >= 10, skip dirs/files/exts, the config file itself,
+ * global AllowPath; Analyze: utils.IsBinary on the first 300 bytes
+ * (utils.go:68-86), binaries other than .pyc dropped, CR stripped from text,
+ * ExtractPrintableBytes for .pyc (utils.go:111-143)).  raw/raw_offsets: the
+ * files as read; paths: input.FilePath as the analyzer sees it (no "/" prefix
+ * for image files: the caller adds it to the scan path, secret.go:133-135).
+ * The result packs the kept files back to back (+64 B pad) ready for
+ * tsg_scan_batch; index[k] = source file of kept file k. */
+typedef struct tsg_prepared tsg_prepared;
+int tsg_prepare_batch(const tsg_ruleset* rs, const char* config_path, const uint8_t* raw, const uint64_t* raw_offsets,
+                      uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
+                      tsg_prepared** out);
+int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_t** offsets, const uint32_t** index,
+                      const uint8_t** binary, uint32_t* nkept);
+void tsg_prepared_free(tsg_prepared* p);
+
 /* Test hook: Regexp.MatchString(text) for `pattern` with the required-literal
  * gate the ruleset compiler sets on path / allow regexes (*gated) and without
  * it (*plain); *has_gate = 1 if a gate was found (2: bounded). */

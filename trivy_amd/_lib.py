@@ -70,6 +70,13 @@ SIGNATURES = [
                                              c_char_pp, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_prefilter_report", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prepare_batch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prepared_view", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32)]),
+    ("tsg_prepared_free", None, [ctypes.c_void_p]),
     ("tsg_regex_match_probe", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                              ctypes.POINTER(ctypes.c_int)]),

@@ -9,6 +9,7 @@
 #include <thread>
 
 #include "engine.h"
+#include "feed.h"
 #include "prefilter.h"
 #include "scanner.h"
 
@@ -29,6 +30,10 @@ struct tsg_engine {
   std::unique_ptr<Engine> eng;
   std::mutex mu;
   std::string report;
+};
+
+struct tsg_prepared {
+  PreparedBatch b;
 };
 
 struct tsg_result {
@@ -422,3 +427,32 @@ int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const 
 }
 
 }  // extern "C"
+
+int tsg_prepare_batch(const tsg_ruleset* rs, const char* config_path, const uint8_t* raw, const uint64_t* raw_offsets,
+                      uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
+                      tsg_prepared** out) {
+  if (!rs || !out || !raw_offsets || (nfiles && (!raw || !paths))) return fail(TSG_ERR_INVALID, "NULL argument");
+  auto* p = new tsg_prepared();
+  std::string err;
+  const int nt = threads > 0 ? threads : static_cast<int>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (!prepare_batch(*rs->rs, config_path ? config_path : "", raw, raw_offsets, nfiles, paths, path_lens, nt,
+                     &p->b, &err)) {
+    delete p;
+    return fail(TSG_ERR_INVALID, err);
+  }
+  *out = p;
+  return TSG_OK;
+}
+
+int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_t** offsets, const uint32_t** index,
+                      const uint8_t** binary, uint32_t* nkept) {
+  if (!p || !data || !offsets || !index || !binary || !nkept) return fail(TSG_ERR_INVALID, "NULL argument");
+  *data = p->b.data.data();
+  *offsets = p->b.offsets.data();
+  *index = p->b.index.data();
+  *binary = p->b.binary.data();
+  *nkept = static_cast<uint32_t>(p->b.index.size());
+  return TSG_OK;
+}
+
+void tsg_prepared_free(tsg_prepared* p) { delete p; }

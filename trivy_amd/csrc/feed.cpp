@@ -1,0 +1,134 @@
+// Host feed: SecretAnalyzer.Required + Analyze's content preparation for a
+// whole batch (pkg/fanal/analyzer/secret/secret.go:103-190,
+// pkg/fanal/utils/utils.go:68-86,111-143), producing the packed ScanArgs
+// contents the engine scans.  Two parallel passes (decide + size, then copy)
+// around a prefix sum, so a batch of many small files (image layers) is
+// prepared at memory speed instead of one Go goroutine per file.
+#include "feed.h"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace tsg {
+namespace {
+
+const char* const kSkipFiles[] = {"go.mod", "go.sum", "package-lock.json", "yarn.lock", "pnpm-lock.yaml",
+                                  "Pipfile.lock", "Gemfile.lock"};                         // secret.go:28-36
+const char* const kSkipDirs[] = {".git", "node_modules"};                                 // secret.go:37-40
+const char* const kSkipExts[] = {".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg", ".socket", ".deb",
+                                 ".rpm", ".zip", ".gz", ".gzip", ".tar"};                  // secret.go:41-62
+
+// filepath.Base (Unix)
+std::string go_base(std::string p) {
+  if (p.empty()) return ".";
+  while (p.size() > 1 && p.back() == '/') p.pop_back();
+  if (p == "/") return "/";
+  const size_t i = p.rfind('/');
+  return i == std::string::npos ? p : p.substr(i + 1);
+}
+
+// filepath.Ext of a final path element
+std::string go_ext(const std::string& name) {
+  for (size_t i = name.size(); i-- > 0;) {
+    if (name[i] == '/') break;
+    if (name[i] == '.') return name.substr(i);
+  }
+  return "";
+}
+
+bool required(const Ruleset& rs, const std::string& path, uint64_t size, const std::string& cfg_base) {
+  if (size < 10) return false;                                     // secret.go:154-156
+  const size_t slash = path.rfind('/');                            // filepath.Split
+  const std::string dir = slash == std::string::npos ? "" : path.substr(0, slash + 1);
+  const std::string name = slash == std::string::npos ? path : path.substr(slash + 1);
+  size_t b = 0;                                                    // strings.Split(dir, "/")
+  for (;;) {
+    const size_t e = dir.find('/', b);
+    const std::string part = dir.substr(b, e == std::string::npos ? std::string::npos : e - b);
+    for (const char* sd : kSkipDirs) if (part == sd) return false;
+    if (e == std::string::npos) break;
+    b = e + 1;
+  }
+  for (const char* sf : kSkipFiles) if (name == sf) return false;
+  if (cfg_base == path) return false;                              // secret.go:178-180
+  const std::string ext = go_ext(name);
+  for (const char* se : kSkipExts) if (ext == se) return false;
+  for (const auto& a : rs.allow_rules)                             // scanner.AllowPath (scanner.go:205-212)
+    if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) return false;
+  return true;
+}
+
+template <typename F>
+void parallel_for(uint32_t n, int threads, F&& fn) {
+  const int nt = std::max(1, std::min<int>(threads, static_cast<int>((n + 255) / 256)));
+  if (nt == 1) { for (uint32_t i = 0; i < n; ++i) fn(i); return; }
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nt; ++t) {
+    ts.emplace_back([&, t]() {
+      for (uint32_t i = static_cast<uint32_t>(static_cast<uint64_t>(n) * t / nt),
+                    e = static_cast<uint32_t>(static_cast<uint64_t>(n) * (t + 1) / nt); i < e; ++i) fn(i);
+    });
+  }
+  for (auto& th : ts) th.join();
+}
+
+}  // namespace
+
+bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,
+                   uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
+                   PreparedBatch* out, std::string* err) {
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    if (raw_off[i + 1] < raw_off[i]) { *err = "offsets must be non-decreasing"; return false; }
+  }
+  const std::string cfg_base = go_base(config_path);
+  // pass 1: keep decision, binary flag and prepared size per file
+  std::vector<uint8_t> keep(nfiles), bin(nfiles);
+  std::vector<uint64_t> size(nfiles);
+  parallel_for(nfiles, threads, [&](uint32_t i) {
+    const std::string path = path_lens ? std::string(paths[i], path_lens[i]) : std::string(paths[i]);
+    const uint8_t* c = raw + raw_off[i];
+    const uint64_t n = raw_off[i + 1] - raw_off[i];
+    keep[i] = 0;
+    if (!required(rs, path, n, cfg_base)) return;
+    const bool binary = go_is_binary(c, n);                        // secret.go:104-108
+    if (binary && go_ext(path) != ".pyc") return;                  // allowedBinary
+    bin[i] = binary;
+    keep[i] = 1;
+    if (binary) {
+      size[i] = go_extract_printable(c, n).size();
+    } else {
+      uint64_t cr = 0;
+      for (uint64_t k = 0; k < n; ++k) cr += c[k] == '\r';
+      size[i] = n - cr;
+    }
+  });
+  out->index.clear();
+  for (uint32_t i = 0; i < nfiles; ++i) if (keep[i]) out->index.push_back(i);
+  const uint32_t nk = static_cast<uint32_t>(out->index.size());
+  out->offsets.assign(nk + 1, 0);
+  out->binary.assign(nk, 0);
+  for (uint32_t k = 0; k < nk; ++k) {
+    out->offsets[k + 1] = out->offsets[k] + size[out->index[k]];
+    out->binary[k] = bin[out->index[k]];
+  }
+  out->data.assign(out->offsets[nk] + 64, 0);                      // K1 reads 16-byte vectors past the end
+  // pass 2: write ScanArgs.Content (CR stripped, or the printable runs of a .pyc)
+  parallel_for(nk, threads, [&](uint32_t k) {
+    const uint32_t i = out->index[k];
+    const uint8_t* c = raw + raw_off[i];
+    const uint64_t n = raw_off[i + 1] - raw_off[i];
+    uint8_t* d = out->data.data() + out->offsets[k];
+    if (out->binary[k]) {
+      const std::string p = go_extract_printable(c, n);
+      std::memcpy(d, p.data(), p.size());
+      return;
+    }
+    for (uint64_t x = 0; x < n; ++x) if (c[x] != '\r') *d++ = c[x];
+  });
+  return true;
+}
+
+}  // namespace tsg

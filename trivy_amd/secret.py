@@ -167,6 +167,37 @@ def pack(args_list):
     return data, offsets
 
 
+def PrepareBatch(scanner, files, config_path="", image=False, threads=0):
+    """Batched SecretAnalyzer.Required + Analyze content prep (tsg_prepare_batch;
+    pkg/fanal/analyzer/secret/secret.go:103-190).  files: [(input.FilePath, raw
+    bytes)].  Returns (ScanArgs list, source index list) for the kept files;
+    image=True adds the "/" prefix image files get (secret.go:133-135)."""
+    L = _lib.lib()
+    raw, offsets = pack([ScanArgs(p, c) for p, c in files])
+    paths, lens, _keep = _lib.pack_paths([p for p, _ in files])
+    h = ctypes.c_void_p()
+    _lib.check(L.tsg_prepare_batch(scanner._rs, (config_path or "").encode(), raw.ctypes.data, offsets.ctypes.data,
+                                   len(files), paths, lens, threads, ctypes.byref(h)))
+    try:
+        d, o, ix, b = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        nk = ctypes.c_uint32()
+        _lib.check(L.tsg_prepared_view(h, ctypes.byref(d), ctypes.byref(o), ctypes.byref(ix), ctypes.byref(b),
+                                       ctypes.byref(nk)))
+        n = nk.value
+        offs = np.ctypeslib.as_array(ctypes.cast(o, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy() \
+            if n else np.zeros(1, np.uint64)
+        idx = np.ctypeslib.as_array(ctypes.cast(ix, ctypes.POINTER(ctypes.c_uint32)), shape=(n,)).tolist() if n else []
+        binf = np.ctypeslib.as_array(ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)), shape=(n,)).tolist() if n else []
+        data = ctypes.string_at(d, int(offs[-1])) if n else b""
+    finally:
+        L.tsg_prepared_free(h)
+    out = []
+    for k, i in enumerate(idx):
+        p = files[i][0]
+        out.append(ScanArgs("/" + p if image else p, data[int(offs[k]):int(offs[k + 1])], bool(binf[k])))
+    return out, idx
+
+
 # ---------------------------------------------------------------- test hooks
 def scan_host_reference(scanner, args_list, threads=1):
     """The C++ confirmer on every (file, rule) pair, no prefilter (tests only)."""
