@@ -447,7 +447,7 @@ int tsg_prepare_batch(const tsg_ruleset* rs, const char* config_path, const uint
 int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_t** offsets, const uint32_t** index,
                       const uint8_t** binary, uint32_t* nkept) {
   if (!p || !data || !offsets || !index || !binary || !nkept) return fail(TSG_ERR_INVALID, "NULL argument");
-  *data = p->b.data.data();
+  *data = p->b.data.get();
   *offsets = p->b.offsets.data();
   *index = p->b.index.data();
   *binary = p->b.binary.data();

@@ -7,6 +7,7 @@
 #include "feed.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -61,17 +62,24 @@ bool required(const Ruleset& rs, const std::string& path, uint64_t size, const s
   return true;
 }
 
+// fn(i) for i in [0, n) on `threads` threads, files handed out dynamically
+// (one at a time for batches of few, large files; in blocks of 64 otherwise)
 template <typename F>
 void parallel_for(uint32_t n, int threads, F&& fn) {
-  const int nt = std::max(1, std::min<int>(threads, static_cast<int>((n + 255) / 256)));
+  const int nt = std::max(1, std::min<int>(threads, static_cast<int>(n)));
   if (nt == 1) { for (uint32_t i = 0; i < n; ++i) fn(i); return; }
+  std::atomic<uint32_t> next{0};
+  const uint32_t blk = n >= 256u * static_cast<uint32_t>(nt) ? 64 : 1;
+  auto run = [&]() {
+    for (;;) {
+      const uint32_t b = next.fetch_add(blk);
+      if (b >= n) break;
+      for (uint32_t i = b, e = std::min(n, b + blk); i < e; ++i) fn(i);
+    }
+  };
   std::vector<std::thread> ts;
-  for (int t = 0; t < nt; ++t) {
-    ts.emplace_back([&, t]() {
-      for (uint32_t i = static_cast<uint32_t>(static_cast<uint64_t>(n) * t / nt),
-                    e = static_cast<uint32_t>(static_cast<uint64_t>(n) * (t + 1) / nt); i < e; ++i) fn(i);
-    });
-  }
+  for (int t = 1; t < nt; ++t) ts.emplace_back(run);
+  run();
   for (auto& th : ts) th.join();
 }
 
@@ -100,9 +108,7 @@ bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint
     if (binary) {
       size[i] = go_extract_printable(c, n).size();
     } else {
-      uint64_t cr = 0;
-      for (uint64_t k = 0; k < n; ++k) cr += c[k] == '\r';
-      size[i] = n - cr;
+      size[i] = n - static_cast<uint64_t>(std::count(c, c + n, static_cast<uint8_t>('\r')));
     }
   });
   out->index.clear();
@@ -114,18 +120,22 @@ bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint
     out->offsets[k + 1] = out->offsets[k] + size[out->index[k]];
     out->binary[k] = bin[out->index[k]];
   }
-  out->data.assign(out->offsets[nk] + 64, 0);                      // K1 reads 16-byte vectors past the end
+  // not zero-filled (every byte below offsets[nk] is written in pass 2); only
+  // the pad K1 may read past the last file is cleared
+  out->data.reset(new uint8_t[out->offsets[nk] + 64]);
+  std::memset(out->data.get() + out->offsets[nk], 0, 64);
   // pass 2: write ScanArgs.Content (CR stripped, or the printable runs of a .pyc)
   parallel_for(nk, threads, [&](uint32_t k) {
     const uint32_t i = out->index[k];
     const uint8_t* c = raw + raw_off[i];
     const uint64_t n = raw_off[i + 1] - raw_off[i];
-    uint8_t* d = out->data.data() + out->offsets[k];
+    uint8_t* d = out->data.get() + out->offsets[k];
     if (out->binary[k]) {
       const std::string p = go_extract_printable(c, n);
       std::memcpy(d, p.data(), p.size());
       return;
     }
+    if (out->offsets[k + 1] - out->offsets[k] == n) { std::memcpy(d, c, n); return; }   // no CR
     for (uint64_t x = 0; x < n; ++x) if (c[x] != '\r') *d++ = c[x];
   });
   return true;

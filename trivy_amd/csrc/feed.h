@@ -1,6 +1,7 @@
 // Host feed: batched SecretAnalyzer.Required + content preparation.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -9,7 +10,7 @@
 namespace tsg {
 
 struct PreparedBatch {
-  std::vector<uint8_t> data;       // kept files' ScanArgs.Content, back to back (+64 B pad)
+  std::unique_ptr<uint8_t[]> data; // kept files' ScanArgs.Content, back to back (+64 B pad)
   std::vector<uint64_t> offsets;   // nkept + 1
   std::vector<uint32_t> index;     // source file index of each kept file
   std::vector<uint8_t> binary;     // ScanArgs.Binary (a .pyc scanned as printable runs)
