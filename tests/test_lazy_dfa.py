@@ -89,3 +89,21 @@ def test_lazy_dfa_planted_rule_samples():
             assert (d == v).all(), r["id"]
             hits += int((d >= 0).sum())
     assert hits > 50
+
+
+SPAN_PATTERNS = [r"--- ignore block start ---(.|\s)*--- ignore block stop ---",
+                 r"(?s)BEGIN NOSCAN.*?END NOSCAN", r"(?s)<x-ignore>.*?</x-ignore>", r"AB(?s:.)*CD",
+                 r"AB(.|\n)*?CD", r"AB.*CD", r"AB[^z]*CD"]     # last two: not every rune -> the DFA path
+
+
+@pytest.mark.parametrize("pattern", SPAN_PATTERNS)
+def test_span_shape_end_matches_vm(pattern):
+    # L1 (any rune)* L2: the fast anchored end (last / first L2 after L1) equals the VM
+    rng = random.Random(99)
+    parts = [b"--- ignore block start ---", b"--- ignore block stop ---", b"BEGIN NOSCAN", b"END NOSCAN",
+             b"<x-ignore>", b"</x-ignore>", b"AB", b"CD", b"C", b"\n", b"\xe2\x84\xaa", b"\xff", b"\xc3", b"z",
+             b"x", b" ", b"--- ignore block st"]
+    for _ in range(40):
+        t = b"".join(rng.choice(parts) for _ in range(rng.randint(0, 30)))
+        d, v = _probe(pattern, t)
+        assert (d == v).all(), (pattern, t, d, v)

@@ -1188,6 +1188,58 @@ void append_utf8(std::string* out, uint32_t r) {
   out->push_back(static_cast<char>(0x80 | (r & 0x3F)));
 }
 
+namespace {
+
+// Rune ranges a one-rune node matches (false: not a one-rune node).
+bool rune_cover(const Node& n, std::vector<Range>* out) {
+  switch (n.op) {
+    case Op::AnyChar: out->push_back({0, 0x10FFFF}); return true;
+    case Op::AnyCharNotNL: out->push_back({0, 9}); out->push_back({11, 0x10FFFF}); return true;
+    case Op::CharClass: out->insert(out->end(), n.ranges.begin(), n.ranges.end()); return true;
+    case Op::Literal: out->push_back({n.rune, n.rune}); return true;
+    case Op::Capture: return rune_cover(*n.sub[0], out);
+    case Op::Alternate:
+      for (const auto& c : n.sub) if (!rune_cover(*c, out)) return false;
+      return true;
+    default: return false;
+  }
+}
+
+bool matches_every_rune(const Node& n) {
+  std::vector<Range> r;
+  if (!rune_cover(n, &r)) return false;
+  std::sort(r.begin(), r.end(), [](const Range& a, const Range& b) { return a.lo < b.lo; });
+  uint32_t next = 0;                     // every rune below `next` is covered
+  for (const Range& x : r) {
+    if (x.lo > next) return false;
+    if (x.hi >= next) next = x.hi + 1;
+  }
+  return next > 0x10FFFF;
+}
+
+void flatten_concat(const Node& n, std::vector<const Node*>* items) {
+  if (n.op == Op::Concat) { for (const auto& c : n.sub) flatten_concat(*c, items); return; }
+  items->push_back(&n);
+}
+
+// L1 X* L2 (X matches every rune; L1, L2 non-empty ASCII literal runs)
+int span_shape(const Node& ast, std::string* l1, std::string* l2) {
+  std::vector<const Node*> items;
+  flatten_concat(ast, &items);
+  size_t k = 0;
+  l1->clear();
+  l2->clear();
+  while (k < items.size() && items[k]->op == Op::Literal && items[k]->rune < 0x80) l1->push_back(static_cast<char>(items[k++]->rune));
+  if (l1->empty() || k >= items.size() || items[k]->op != Op::Star || !matches_every_rune(*items[k]->sub[0])) return 0;
+  const int shape = items[k]->nongreedy ? 2 : 1;
+  ++k;
+  while (k < items.size() && items[k]->op == Op::Literal && items[k]->rune < 0x80) l2->push_back(static_cast<char>(items[k++]->rune));
+  if (l2->empty() || k != items.size()) return 0;
+  return shape;
+}
+
+}  // namespace
+
 std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string* err) {
   static std::atomic<uint64_t> next_id{1};
   auto re = std::unique_ptr<Regexp>(new Regexp());
@@ -1205,6 +1257,7 @@ std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string*
   re->prog_.start = f.i;
   re->nullable_ = f.nullable;
   compute_first(&re->prog_);
+  re->span_shape_ = span_shape(*re->ast_, &re->span_l1_, &re->span_l2_);
   return re;
 }
 
@@ -1231,6 +1284,26 @@ bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored
 
 long Regexp::match_end(const uint8_t* text, size_t len, size_t pos) const {
   if (prog_.start == 0) return -1;
+  if (span_shape_) {
+    // L1 X* L2: X* takes any run of runes, and L2 (ASCII) starts on a rune
+    // boundary wherever it occurs, so the match ends after the last (greedy)
+    // or first (lazy) occurrence of L2 at or after pos + |L1|
+    const size_t n1 = span_l1_.size(), n2 = span_l2_.size();
+    if (pos + n1 + n2 > len || std::memcmp(text + pos, span_l1_.data(), n1) != 0) return -1;
+    const size_t lo = pos + n1;
+    if (span_shape_ == 2) {
+      const void* q = memmem(text + lo, len - lo, span_l2_.data(), n2);
+      return q ? static_cast<long>(static_cast<const uint8_t*>(q) - text + n2) : -1;
+    }
+    for (size_t hi = len - n2 + 1; hi > lo;) {       // candidate starts in [lo, hi)
+      const void* q = memrchr(text + lo, span_l2_[0], hi - lo);
+      if (!q) break;
+      const size_t at = static_cast<const uint8_t*>(q) - text;
+      if (std::memcmp(text + at, span_l2_.data(), n2) == 0) return static_cast<long>(at + n2);
+      hi = at;
+    }
+    return -1;
+  }
   thread_local std::vector<std::pair<uint64_t, std::unique_ptr<LazyDfa>>> cache;
   LazyDfa* d = nullptr;
   for (auto& e : cache) {

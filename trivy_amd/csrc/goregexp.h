@@ -156,6 +156,11 @@ class Regexp {
   uint8_t gate_first_[256] = {};    // first bytes of the gate literals
   bool gate_bounded_ = false;
   uint32_t gate_dmin_ = 0, gate_dmax_ = 0;
+  // L1 (any-rune)* L2 with ASCII literals (e.g. the exclude-block idiom
+  // `--- ignore block start ---(.|\s)*--- ignore block stop ---`): the
+  // anchored leftmost-first end is the last (greedy) / first (lazy) L2 after L1
+  int span_shape_ = 0;               // 0 none, 1 greedy star, 2 lazy star
+  std::string span_l1_, span_l2_;
 };
 
 }  // namespace re
