@@ -61,8 +61,12 @@ def main():
         "calib_k1pattern": {"bytes": calib_bytes, "fetch_size_kb": cal, "scale": scale},
         "calib_coalesced_fetch_size_kb": coal,
     }
-    f = min(k1["tsg_k1_scan"]) * 1024.0 * scale
-    w = min(k1w.get("tsg_k1_scan", [0.0])) * 1024.0
+    # mean over the K1 launches (a pipelined step launches K1 once per piece,
+    # pieces of unequal size; bytes_per_launch is the mean too)
+    kf = k1["tsg_k1_scan"]
+    kw = k1w.get("tsg_k1_scan", [0.0])
+    f = sum(kf) / len(kf) * 1024.0 * scale
+    w = sum(kw) / len(kw) * 1024.0
     out["traffic_bytes_per_launch"] = f + w
     out["read_bytes_per_launch"] = f
     out["write_bytes_per_launch"] = w
