@@ -1083,7 +1083,6 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   }
   cut.push_back(in.nfiles);
   const size_t np = cut.size() - 1;
-  results->assign(in.nfiles, Secret());
   std::vector<BatchInput> piece(np);
   std::vector<std::vector<uint64_t>> poff(np);
   std::vector<ScanStats> pst(np);
@@ -1106,9 +1105,20 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   }
   uint64_t nconf = 0, nfind = 0;
   double gpu_ms = 0, host_ms = 0;
-  auto tg = std::chrono::steady_clock::now();
-  if (!run_gpu(piece[0], &pst[0], &m.out[0], err)) return false;
-  gpu_ms += ms_since(tg);
+  {
+    // piece 0's GPU passes on the driver thread while this thread sets up the
+    // per-file result slots (hundreds of thousands for image layers)
+    bool ok0 = true;
+    std::thread gpu0([&]() {
+      auto tg = std::chrono::steady_clock::now();
+      ok0 = run_gpu(piece[0], &pst[0], &m.out[0], err);
+      gpu_ms += ms_since(tg);
+    });
+    results->clear();
+    results->resize(in.nfiles);
+    gpu0.join();
+    if (!ok0) return false;
+  }
   for (size_t p = 0; p < np; ++p) {
     std::thread gpu;
     bool ok_next = true;
