@@ -1064,6 +1064,7 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
 // device data a 16-byte aligned sub-range of the batch), so the kernels are
 // unchanged and the result equals the one-piece scan.
 bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* st, std::string* err) {
+  constexpr uint32_t kManyFiles = 1u << 16;
   ScanStats local;
   if (!st) st = &local;
   auto t0 = std::chrono::steady_clock::now();
@@ -1105,9 +1106,10 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   }
   uint64_t nconf = 0, nfind = 0;
   double gpu_ms = 0, host_ms = 0;
-  {
-    // piece 0's GPU passes on the driver thread while this thread sets up the
-    // per-file result slots (hundreds of thousands for image layers)
+  if (in.nfiles >= kManyFiles) {
+    // piece 0's GPU passes on a driver thread while this thread sets up the
+    // per-file result slots (hundreds of thousands for image layers; with few
+    // files the extra thread hand-off measured slower, so they run in line)
     bool ok0 = true;
     std::thread gpu0([&]() {
       auto tg = std::chrono::steady_clock::now();
@@ -1118,6 +1120,11 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     results->resize(in.nfiles);
     gpu0.join();
     if (!ok0) return false;
+  } else {
+    results->assign(in.nfiles, Secret());
+    auto tg = std::chrono::steady_clock::now();
+    if (!run_gpu(piece[0], &pst[0], &m.out[0], err)) return false;
+    gpu_ms += ms_since(tg);
   }
   for (size_t p = 0; p < np; ++p) {
     std::thread gpu;
