@@ -107,7 +107,8 @@ def main():
         dist.init_process_group("gloo")
 
     import torch
-    from trivy_amd import _lib, synth
+    from trivy_amd import _lib
+    from workload import synth
     from trivy_amd import secret as S
 
     def log(*a):

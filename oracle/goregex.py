@@ -18,6 +18,19 @@ two libraries' flag-scoping differences can leak in:
     (Go \\s = [\\t\\n\\f\\r ], no \\v)
   * named groups (?P<n>..) / (?<n>..) -> plain groups; names kept in
     `subexp_names` (Go allows duplicate names, scanner.go:155-168 relies on it)
+  * an alternation whose alternatives each match exactly one char and hold no
+    capture (e.g. `(.|\\s)` of the exclude-block idiom) -> one char class, the
+    union of the alternatives' char sets (computed by running each over every
+    code point).  Each alternative consumes the same single char, so the union
+    matches exactly what the alternation matches; without the rewrite the
+    `regex` module backtracks per char and exhausts memory on MB-sized inputs.
+    `_Translator(pattern, merge=False)` keeps the literal alternation
+    (tests/test_oracle_regex.py checks both translations agree).
+
+Matches that need no submatches (MatchString, FindAllIndex) run on a second
+translation with every group non-capturing: the `regex` module records every
+iteration of a repeated capturing group, which is what made config 5's
+`(.|\\s)*` block scan run out of memory.
 
 Matching runs on `bytes.decode('utf-8', 'surrogateescape')`, so each invalid
 byte is one char, like Go's utf8.DecodeRune (RuneError, width 1).  Offsets are
@@ -53,12 +66,69 @@ def _cls_lit(cp):
     return "\\U%08x" % cp
 
 
+_ALL_CHARS = None
+
+
+def _all_chars():
+    """Every char a scanned text can hold: all code points except surrogates,
+    plus U+DC80..U+DCFF (invalid bytes under 'surrogateescape')."""
+    global _ALL_CHARS
+    if _ALL_CHARS is None:
+        cps = list(range(0xD800)) + list(range(0xDC80, 0xDD00)) + list(range(0xE000, 0x110000))
+        _ALL_CHARS = "".join(map(chr, cps))
+    return _ALL_CHARS
+
+
+_UNION_CACHE = {}
+
+
+def _char_set(pat):
+    """Code points matched by a one-char pattern, or None if it can match
+    anything but exactly one char."""
+    if pat not in _UNION_CACHE:
+        rx = regex.compile(pat, regex.VERSION0)
+        if rx.match("") is not None:
+            _UNION_CACHE[pat] = None
+        else:
+            text = _all_chars()
+            pts = []
+            ok = True
+            for m in rx.finditer(text):
+                if m.end() - m.start() != 1:
+                    ok = False
+                    break
+                pts.append(ord(text[m.start()]))
+            _UNION_CACHE[pat] = set(pts) if ok else None
+    return _UNION_CACHE[pat]
+
+
+def _union_class(alts):
+    sets = [_char_set(a) for a in alts]
+    if any(x is None for x in sets):
+        return None
+    cps = sorted(set().union(*sets))
+    if not cps:
+        return "[^\\x00-\\U0010ffff]"
+    ranges = []
+    lo = prev = cps[0]
+    for c in cps[1:]:
+        if c != prev + 1:
+            ranges.append((lo, prev))
+            lo = c
+        prev = c
+    ranges.append((lo, prev))
+    return "[%s]" % "".join(_cls_lit(a) if a == b else "%s-%s" % (_cls_lit(a), _cls_lit(b)) for a, b in ranges)
+
+
 class _Translator:
-    def __init__(self, pat):
+    def __init__(self, pat, merge=True, capture=True):
         self.p = pat
         self.i = 0
         self.names = [""]   # index 0 = whole match
         self.depth = 0
+        self.merge = merge       # single-char alternations -> one class
+        self.capture = capture   # False: every group non-capturing
+        self._single = False     # the last atom / concat / alternation matches exactly one char, no capture
 
     # ------------------------------------------------------------------ lexing
     def peek(self, k=0):
@@ -80,19 +150,33 @@ class _Translator:
         # Flags set by (?x) persist to the end of the enclosing group,
         # across '|' (Go regexp/syntax parse.go semantics).
         alts = [self.concat(flags)]
+        singles = [self._single]
         while self.peek() == "|":
             self.i += 1
             alts.append(self.concat(flags))
+            singles.append(self._single)
+        if self.merge and len(alts) > 1 and all(singles):
+            u = _union_class(alts)
+            if u is not None:
+                self._single = True
+                return u
+        self._single = len(alts) == 1 and singles[0]
         return "|".join(alts)
 
     def concat(self, flags):
         items = []
+        single = False
         while not self.eof() and self.peek() not in "|)":
+            self._single = False
             atom = self.atom(flags)
             if atom is None:
                 continue
-            atom = self.repeat(atom, flags)
-            items.append(atom)
+            single = self._single
+            rep = self.repeat(atom, flags)
+            if rep is not atom:
+                single = False
+            items.append(rep)
+        self._single = len(items) == 1 and single
         return "".join(items)
 
     def repeat(self, atom, flags):
@@ -153,6 +237,7 @@ class _Translator:
         if c == "(":
             return self.group(flags)
         if c == "[":
+            self._single = True
             return self.char_class(flags)
         if c in ("*", "+", "?"):
             raise GoSyntaxError("missing argument to repetition operator in %r" % self.p)
@@ -161,8 +246,10 @@ class _Translator:
             if self.try_brace() is not None:
                 raise GoSyntaxError("missing argument to repetition operator in %r" % self.p)
             self.i = save + 1
+            self._single = True
             return self.fold_wrap(_lit(ord("{")), flags)
         self.i += 1
+        self._single = c not in "^$"
         if c == ".":
             return "(?s:.)" if flags["s"] else "[^\\n]"
         if c == "^":
@@ -213,7 +300,7 @@ class _Translator:
                         if self.peek() != ")":
                             raise GoSyntaxError("missing closing ) in %r" % self.p)
                         self.i += 1
-                        return "(?:%s)" % inner
+                        return "(?:%s)" % inner     # keeps self._single of `inner`
                     else:
                         raise GoSyntaxError("invalid or unsupported Perl syntax in %r" % self.p)
         # capturing group
@@ -222,6 +309,9 @@ class _Translator:
         if self.peek() != ")":
             raise GoSyntaxError("missing closing ) in %r" % self.p)
         self.i += 1
+        if not self.capture:
+            return "(?:%s)" % inner         # keeps self._single of `inner`
+        self._single = False
         return "(%s)" % inner
 
     # ---------------------------------------------------------------- escapes
@@ -280,6 +370,7 @@ class _Translator:
 
     def escape(self, flags):
         c = self.peek()
+        self._single = c not in "AzbBQ"
         if c in "dswDSW":
             self.i += 1
             body = PERL[c.lower()]
@@ -306,6 +397,7 @@ class _Translator:
             end = self.p.find("\\E", self.i)
             lit = self.p[self.i:] if end < 0 else self.p[self.i:end]
             self.i = len(self.p) if end < 0 else end + 2
+            self._single = len(lit) == 1
             return "".join(self.fold_wrap(_lit(ord(ch)), flags) for ch in lit)
         if c == "C":
             raise GoSyntaxError("invalid escape \\C in %r" % self.p)
@@ -391,12 +483,15 @@ class _Translator:
 class GoRegexp:
     """A compiled Go regexp (oracle restatement)."""
 
-    def __init__(self, pattern):
+    def __init__(self, pattern, merge=True):
         self.pattern = pattern
-        t = _Translator(pattern)
+        t = _Translator(pattern, merge=merge)
         self.py_pattern = t.parse()
         self.subexp_names = t.names
         self.rx = regex.compile(self.py_pattern, regex.VERSION0)
+        # no-capture translation for matches whose submatches are not wanted
+        self.py_pattern_nocap = _Translator(pattern, merge=merge, capture=False).parse()
+        self.rx_nocap = regex.compile(self.py_pattern_nocap, regex.VERSION0)
 
     # -- helpers on (text, byte-offset map)
     @staticmethod
@@ -417,7 +512,7 @@ class GoRegexp:
     def match_string(self, s):
         if isinstance(s, bytes):
             s = s.decode("utf-8", "surrogateescape")
-        return self.rx.search(s) is not None
+        return self.rx_nocap.search(s) is not None
 
     def find_all(self, content, prepared=None, submatch=False):
         """Go Regexp.FindAll(Submatch)Index(content, -1) (regexp.go allMatches)."""
@@ -425,8 +520,9 @@ class GoRegexp:
         end = len(text)
         out = []
         pos, prev_end = 0, -1
+        rx = self.rx if submatch else self.rx_nocap
         while pos <= end:
-            m = self.rx.search(text, pos)
+            m = rx.search(text, pos)
             if m is None:
                 break
             accept = True

@@ -155,7 +155,11 @@ def parse_config(path):
     if not path or not os.path.exists(path):
         return None
     with open(path, "rb") as f:
-        doc = yaml.safe_load(f) or {}
+        docs = yaml.safe_load_all(f.read())
+        try:
+            doc = next(docs) or {}    # yaml.v3 Decoder.Decode: the first document
+        except StopIteration:         # no document: io.EOF (scanner.go:296-298)
+            raise ConfigError("secrets config decode error: EOF") from None
     cfg = {
         "enable_builtin_rule_ids": [str(x) for x in (doc.get("enable-builtin-rules") or [])],
         "disable_rule_ids": [str(x) for x in (doc.get("disable-rules") or [])],
@@ -283,27 +287,42 @@ def _go_str_less(a, b):
     return a.encode("utf-8", "surrogateescape") < b.encode("utf-8", "surrogateescape")
 
 
+_GO_QUOTE_NAMED = {7: "\\a", 8: "\\b", 12: "\\f", 10: "\\n", 13: "\\r", 9: "\\t", 11: "\\v"}
+
+
+def go_is_print(cp):
+    """unicode.IsPrint: categories L, M, N, P, S plus U+0020 (not other spaces)."""
+    if cp == 0x20:
+        return True
+    if 0xD800 <= cp <= 0xDFFF:
+        return False
+    return unicodedata.category(chr(cp))[0] in "LMNPS"
+
+
 def go_quote(s):
-    """fmt %q of a Go string (strconv.Quote), enough for file paths/titles."""
+    """fmt %q of a Go string = strconv.Quote (go1.23 strconv/quote.go
+    appendQuotedWith + appendEscapedRune, ASCIIonly = graphicOnly = false):
+    an invalid byte (a surrogateescape'd char here) -> \\xHH; '"' and '\\'
+    backslashed; printable runes raw; \\a \\b \\f \\n \\r \\t \\v named; other
+    runes < 0x20 and 0x7f -> \\xHH; other non-printable runes -> \\uHHHH or
+    \\UHHHHHHHH."""
     out = ['"']
     for ch in s:
         o = ord(ch)
-        if ch == '"':
-            out.append('\\"')
-        elif ch == "\\":
-            out.append("\\\\")
-        elif 0xDC80 <= o <= 0xDCFF:
+        if 0xDC80 <= o <= 0xDCFF:
             out.append("\\x%02x" % (o - 0xDC00))
-        elif ch == "\n":
-            out.append("\\n")
-        elif ch == "\t":
-            out.append("\\t")
-        elif ch == "\r":
-            out.append("\\r")
-        elif o < 0x20 or o == 0x7f:
-            out.append("\\x%02x" % o)
-        else:
+        elif ch == '"' or ch == "\\":
+            out.append("\\" + ch)
+        elif go_is_print(o):
             out.append(ch)
+        elif o in _GO_QUOTE_NAMED:
+            out.append(_GO_QUOTE_NAMED[o])
+        elif o < 0x20 or o == 0x7F:
+            out.append("\\x%02x" % o)
+        elif o < 0x10000:
+            out.append("\\u%04x" % o)
+        else:
+            out.append("\\U%08x" % o)
     out.append('"')
     return "".join(out)
 

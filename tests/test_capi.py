@@ -52,3 +52,29 @@ def test_engine_create_without_gpu_fails_loudly():
     assert rc == -3
     assert b"no HIP device" in L.tsg_last_error()
     L.tsg_ruleset_free(rs)
+
+
+def test_parse_config_document_rules(tmp_path):
+    # yaml.v3 Decoder.Decode (scanner.go:296-298): no document -> io.EOF error;
+    # an explicit null document -> the zero Config; only the first document counts
+    import pytest
+
+    from oracle import secret_oracle as so
+    from trivy_amd import secret as S
+    cases = {"empty.yaml": b"", "comments.yaml": b"# nothing here\n\n", "null.yaml": b"---\n",
+             "tilde.yaml": b"~\n", "two.yaml": b"disable-rules: [aws-access-key-id]\n---\nrules: 3\n"}
+    for name, body in cases.items():
+        p = tmp_path / name
+        p.write_bytes(body)
+        if name in ("empty.yaml", "comments.yaml"):
+            with pytest.raises(S.ConfigError, match="secrets config decode error: EOF"):
+                S.ParseConfig(str(p))
+            with pytest.raises(so.ConfigError, match="secrets config decode error: EOF"):
+                so.parse_config(str(p))
+        else:
+            cfg = S.ParseConfig(str(p))
+            assert isinstance(cfg, dict)
+            ids = S.Scanner(cfg).rule_ids
+            want = [r.id for r in so.Scanner(so.parse_config(str(p))).rules]
+            assert ids == want
+    assert "aws-access-key-id" not in S.Scanner(S.ParseConfig(str(tmp_path / "two.yaml"))).rule_ids

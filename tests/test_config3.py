@@ -13,7 +13,7 @@ import pytest
 
 from oracle import secret_oracle as so
 from trivy_amd import secret as S
-from trivy_amd import synth
+from workload import synth
 
 
 def _args(nbytes, seed, sizes):

@@ -55,7 +55,7 @@ def test_synthetic_parity_on_gpu(seed):
     # every builtin rule planted densely, near misses, CRLF-stripped, fold-special
     # runes and invalid UTF-8: the HIP path equals the oracle file by file
     from oracle import secret_oracle as so
-    from trivy_amd import synth
+    from workload import synth
     c = synth.generate(1_500_000, seed=seed, sizes="lognormal", plant_rate=3e-3, base_bytes=1 << 20)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     ref = so.Scanner(None)
@@ -76,7 +76,8 @@ def test_pipelined_pieces_on_gpu(monkeypatch):
     import torch
 
     from oracle import secret_oracle as so
-    from trivy_amd import _lib, synth
+    from trivy_amd import _lib
+    from workload import synth
     c = synth.generate(3_000_000, seed=13, sizes="lognormal", plant_rate=3e-3, base_bytes=1 << 20)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     ref = so.Scanner(None)

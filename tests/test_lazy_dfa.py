@@ -11,7 +11,8 @@ import random
 import numpy as np
 import pytest
 
-from trivy_amd import _lib, synth
+from trivy_amd import _lib
+from workload import synth
 from trivy_amd import secret as S
 
 EDGE = [

@@ -12,7 +12,8 @@ import os
 import numpy as np
 import pytest
 
-from trivy_amd import _lib, synth
+from trivy_amd import _lib
+from workload import synth
 
 DATA = os.path.join(os.path.dirname(__file__), "..", "trivy_amd", "data", "builtin_rules.json")
 

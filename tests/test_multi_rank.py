@@ -24,7 +24,8 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from trivy_amd import secret as S, synth
+    from trivy_amd import secret as S
+    from workload import synth
     c = synth.generate(300_000, seed=11, sizes="lognormal", plant_rate=2e-3, base_bytes=1 << 20)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     sc = S.Scanner(None)
@@ -55,7 +56,8 @@ def test_two_gloo_ranks_match_single_process():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from trivy_amd import secret as S, synth
+    from trivy_amd import secret as S
+    from workload import synth
     c = synth.generate(300_000, seed=11, sizes="lognormal", plant_rate=2e-3, base_bytes=1 << 20)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     want = S.scan_table_model(S.Scanner(None), args)

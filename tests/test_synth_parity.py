@@ -5,7 +5,7 @@ import pytest
 
 from oracle import secret_oracle as so
 from trivy_amd import secret as S
-from trivy_amd import synth
+from workload import synth
 
 
 def _corpus(seed, nbytes, plant_rate):

@@ -9,7 +9,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from trivy_amd import secret as S, synth  # noqa: E402
+from trivy_amd import secret as S
+from workload import synth  # noqa: E402
 
 
 def main():

@@ -357,7 +357,7 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   // per-chunk newline counts over the packed batch, as K1 produces them
   const uint32_t ch = 2048;
   const uint64_t total = nfiles ? offsets[nfiles] : 0;
-  std::vector<uint32_t> chunk_nl(total / ch + 2, 0);
+  std::vector<uint32_t> chunk_nl((total + ch - 1) / ch, 0);   // exactly K1's chunk count
   for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += data[x] == '\n';
   for (uint32_t f = 0; f < nfiles; ++f) {
     const uint8_t* c = data + offsets[f];
@@ -417,7 +417,7 @@ int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const 
   std::string err;
   auto rx = re::Regexp::compile(pattern, &err);
   if (!rx) return fail(TSG_ERR_CONFIG, err);
-  std::vector<int> caps(2 * (rx->num_subexp() + 1));
+  std::vector<re::Cap> caps(2 * (rx->num_subexp() + 1));
   for (size_t i = 0; i < n; ++i) {
     if (pos[i] > len) return fail(TSG_ERR_INVALID, "position out of range");
     dfa_end[i] = rx->match_end(text, len, pos[i]);

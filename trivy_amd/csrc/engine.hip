@@ -66,6 +66,12 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
 constexpr uint32_t kWaveHits = 1024;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
+
+// Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
+// record's 32 - kAnchorBits offset bits.
+constexpr uint32_t k1_max_chunk(int ks) {
+  return ((1u << (32 - kAnchorBits)) / (64u * static_cast<uint32_t>(ks))) & ~127u;
+}
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 // Keyword ids < 128 accumulate in two per-stream 64-bit masks, flushed with
@@ -135,6 +141,9 @@ struct K1Ctx {
   bool primary;                   // first scan group: also counts newlines and flags fold-special files
   unsigned long long* __restrict__ hits;   // this workgroup's region of the hit list
   uint32_t region_cap;
+  unsigned long long* __restrict__ over;   // shared overflow pool for hits past a full region
+  uint32_t* over_cnt;
+  uint32_t over_cap;
   uint32_t* b_hitcnt;           // LDS: fill count of the workgroup's region
   uint32_t* w_hits;             // this wave's LDS hit buffer
   unsigned long long item_base; // first byte of the wave's current item
@@ -168,7 +177,12 @@ __device__ __forceinline__ void k1_out(const K1Ctx& x, K1Stream& t, uint32_t st,
         x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
       } else {                                           // buffer full: straight to the region
         const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
-        if (gi < x.region_cap) x.hits[gi] = (q << 24) | (id - x.nkw);
+        if (gi < x.region_cap) {
+          x.hits[gi] = (q << 24) | (id - x.nkw);
+        } else {                                         // region full: the shared overflow pool
+          const uint32_t oi = atomicAdd(x.over_cnt, 1u);
+          if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
+        }
       }
     }
   }
@@ -260,6 +274,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
+    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
     uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | (scan table | class map |
@@ -279,6 +294,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
   x.meta = g_meta; x.list = g_list; x.nkw = nkw;
   x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
   x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
+  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
   x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
   if (kLds) {
     uint16_t* s_next = reinterpret_cast<uint16_t*>(s_tab);
@@ -406,12 +422,24 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const uint32_t n = min(*x.w_hitcnt, kWaveHits);
-    uint32_t b0 = 0;
-    if (lane == 0 && n) b0 = atomicAdd(x.b_hitcnt, n);
+    uint32_t b0 = 0, o0 = 0;
+    if (lane == 0 && n) {
+      b0 = atomicAdd(x.b_hitcnt, n);
+      // entries past the region's capacity go to the shared overflow pool
+      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
+    }
     b0 = __shfl(b0, 0);
+    o0 = __shfl(o0, 0);
+    const uint32_t spill_from = max(b0, region_cap);
     for (uint32_t i = lane; i < n; i += 64) {
       const uint32_t h = x.w_hits[i];
-      if (b0 + i < region_cap) x.hits[b0 + i] = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
+      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
+      if (b0 + i < region_cap) {
+        x.hits[b0 + i] = v;
+      } else {
+        const uint32_t oi = o0 + (b0 + i - spill_from);
+        if (oi < x.over_cap) x.over[oi] = v;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -565,13 +593,14 @@ struct Engine::Impl {
   uint64_t* d_off = nullptr; size_t d_off_cap = 0;
   uint32_t* d_kw = nullptr; size_t d_kw_cap = 0;
   unsigned long long* d_hits = nullptr; size_t d_hits_cap = 0;
+  unsigned long long* d_over = nullptr; size_t d_over_cap = 0;   // hits past a full region (any workgroup)
   uint32_t* d_bh = nullptr; size_t d_bh_cap = 0;    // hits written per K1 workgroup (its region of d_hits)
   std::vector<uint32_t> h_bh;
   CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
   uint32_t* d_nl = nullptr; size_t d_nl_cap = 0;
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   unsigned int* d_cnt = nullptr;
-  size_t hit_cap = 1 << 20, cand_cap = 1 << 18;
+  size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
   // host copies of a piece's GPU results: two slots, so the GPU passes of
   // piece i+1 overlap the host confirmation of piece i (Engine::scan)
   std::vector<uint32_t> h_kw;
@@ -608,10 +637,6 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
   if (hipSetDevice(device) != hipSuccess) { *err = "hipSetDevice failed"; return nullptr; }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) m.sms = prop.multiProcessorCount;
-  if (const char* c = std::getenv("TSG_K1_CHUNK")) {
-    const long v = std::atol(c);
-    if (v >= 256 && v % 128 == 0) m.chunk = static_cast<uint32_t>(v);
-  }
   if (const char* c = std::getenv("TSG_PIECES")) {
     const long v = std::atol(c);
     if (v >= 1 && v <= 64) m.pieces = static_cast<uint32_t>(v);
@@ -631,6 +656,13 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
       m.k1_threads = t;
       m.k1_streams = static_cast<int>(k);
     }
+  }
+  if (const char* c = std::getenv("TSG_K1_CHUNK")) {
+    // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
+    // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
+    // chunks are clamped so the offset cannot wrap
+    const long v = std::atol(c);
+    if (v >= 256 && v % 128 == 0) m.chunk = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(m.k1_streams)));
   }
   if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess) { *err = "hipStreamCreate failed"; return nullptr; }
   for (auto& ev : m.ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
@@ -727,7 +759,7 @@ Engine::~Engine() {
   Impl& m = *impl_;
   hipSetDevice(device_);
   void* ps[] = {m.anchors, m.rules, m.rule_kw, m.vdfa, m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw,
-                m.d_hits, m.d_bh, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
+                m.d_hits, m.d_over, m.d_bh, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
   for (void* p : ps) if (p) hipFree(p);
   for (K1Group& g : m.k1g) {
     void* gs[] = {g.next, g.cls, g.meta, g.list};
@@ -758,6 +790,7 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
     const uint64_t c = ((per_lane + rounds - 1) / rounds + 127) / 128 * 128;
     kChunk = static_cast<uint32_t>(std::min<uint64_t>(m.chunk, std::max<uint64_t>(1024, c)));
   }
+  if (kChunk > k1_max_chunk(m.k1_streams) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
   const uint8_t* d_data = static_cast<const uint8_t*>(in.d_data);
@@ -779,6 +812,8 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
   if (!ensure(&m.d_nl, &m.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
   m.hit_cap = std::max<size_t>(m.hit_cap, total / 256);   // ~1 hit per 670 B on source text
   if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
+  m.over_cap = std::max<size_t>(m.over_cap, total / 2048);
+  if (!ensure(&m.d_over, &m.d_over_cap, m.over_cap, err)) return false;
   const uint32_t ngroups = static_cast<uint32_t>(m.k1g.size());
   if (!ensure(&m.d_bh, &m.d_bh_cap, 2ull * std::max(m.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
   if (!ensure(&m.d_ff, &m.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
@@ -835,24 +870,32 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
       uint8_t* a_cls = g.cls;
       OutMeta* a_meta = g.meta;
       uint32_t* a_list = g.list;
+      uint32_t* a_ocnt = m.d_cnt + 2;
+      uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(m.over_cap, 0xffffffffu));
       void* args[] = {&a_data, &a_total, &m.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
-                      &m.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &region_cap, &m.d_nl, &m.d_ff};
+                      &m.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &region_cap,
+                      &m.d_over, &a_ocnt, &a_ocap, &m.d_nl, &m.d_ff};
       HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, m.stream));
     }
     HIP_OK(hipEventRecord(m.ev[1], m.stream));
-    m.h_bh.resize(nregions);
+    m.h_bh.resize(nregions + 1);
     HIP_OK(hipMemcpyAsync(m.h_bh.data(), m.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+    HIP_OK(hipMemcpyAsync(m.h_bh.data() + nregions, m.d_cnt + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
     HIP_OK(hipStreamSynchronize(m.stream));
     float k1 = 0;
     HIP_OK(hipEventElapsedTime(&k1, m.ev[0], m.ev[1]));
     st->k1_ms += k1;
     uint64_t nhits = 0;
     uint32_t maxr = 0;
-    for (uint32_t b : m.h_bh) { nhits += b; maxr = std::max(maxr, b); }
-    if (maxr > region_cap) {                           // a workgroup's region overflowed: grow, rerun K1
-      m.hit_cap = static_cast<size_t>(maxr) * 5 / 4 * nregions + 1024;
-      if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
+    for (uint32_t r = 0; r < nregions; ++r) { nhits += m.h_bh[r]; maxr = std::max(maxr, std::min(m.h_bh[r], region_cap)); }
+    const uint32_t nover = m.h_bh[nregions];
+    if (nover > m.over_cap) {
+      // the overflow pool (shared by every workgroup) was too small: grow it
+      // to the exact need and run K1 again.  Growth follows the batch's total
+      // hit count, not the fullest region times the region count.
+      m.over_cap = static_cast<size_t>(nover) * 5 / 4 + 1024;
+      if (!ensure(&m.d_over, &m.d_over_cap, m.over_cap, err)) return false;
       continue;
     }
     st->hits = nhits;
@@ -868,6 +911,14 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
                            m.d_hits, m.d_bh, region_cap, nregions, m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
                            m.v_cls, m.d_cands, m.d_cnt, static_cast<uint32_t>(m.cand_cap));
         HIP_OK(hipGetLastError());
+        if (nover > 0) {                               // the overflow pool as one more region
+          const uint32_t osub = static_cast<uint32_t>(std::min<uint64_t>(4096, (nover + 1023) / 1024));
+          hipLaunchKernelGGL(tsg_k2_verify, dim3(osub), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles,
+                             m.d_over, m.d_cnt + 2, static_cast<uint32_t>(m.over_cap), 1u, m.anchors, m.rules, m.rule_kw, m.d_kw,
+                             m.kw_words, m.vdfa, m.v_next, m.v_acc, m.v_cls, m.d_cands, m.d_cnt,
+                             static_cast<uint32_t>(m.cand_cap));
+          HIP_OK(hipGetLastError());
+        }
       }
       HIP_OK(hipEventRecord(m.ev[3], m.stream));
       unsigned int c2 = 0;

@@ -784,7 +784,7 @@ class Machine {
     stack_.reserve(64);
   }
 
-  bool match(const uint8_t* s, size_t len, size_t pos0, bool anchored, int* caps_out) {
+  bool match(const uint8_t* s, size_t len, size_t pos0, bool anchored, Cap* caps_out) {
     matched_ = false;
     std::fill(matchcap_.begin(), matchcap_.end(), -1);
     int rq = 0, nq = 1;
@@ -813,7 +813,7 @@ class Machine {
       if (!matched_ && (!anchored || pos == pos0)) {
         if (ncap_ > 0) {
           std::fill(scratch_.begin(), scratch_.end(), -1);
-          scratch_[0] = static_cast<int>(pos);
+          scratch_[0] = static_cast<Cap>(pos);
         }
         add(rq, p_.start, pos, scratch_.data(), flag);
       }
@@ -838,12 +838,12 @@ class Machine {
   int ncap_;
   std::vector<uint32_t> sparse_[2], dense_pc_[2];
   std::vector<uint8_t> dense_has_[2];
-  std::vector<int> caps_[2];
+  std::vector<Cap> caps_[2];
   uint32_t size_[2];
-  std::vector<int> matchcap_, scratch_;
+  std::vector<Cap> matchcap_, scratch_;
   bool matched_ = false;
   uint8_t first_[256] = {0};
-  struct Frame { uint32_t pc; int slot; int old; };
+  struct Frame { uint32_t pc; int slot; Cap old; };
   std::vector<Frame> stack_;
 
   bool contains(int q, uint32_t pc) const {
@@ -852,7 +852,7 @@ class Machine {
   }
 
   // Go machine.add: DFS in priority order; capture slots restored on unwind.
-  void add(int q, uint32_t pc0, size_t pos, int* cap, uint8_t cond) {
+  void add(int q, uint32_t pc0, size_t pos, Cap* cap, uint8_t cond) {
     // explicit stack: entries are either (pc) to visit or a capture-restore
     stack_.clear();
     stack_.push_back({pc0, -1, 0});
@@ -883,7 +883,7 @@ class Machine {
         case IOp::Capture:
           if (static_cast<int>(in.arg) < ncap_) {
             stack_.push_back({0, static_cast<int>(in.arg), cap[in.arg]});   // restore after subtree
-            cap[in.arg] = static_cast<int>(pos);
+            cap[in.arg] = static_cast<Cap>(pos);
             stack_.push_back({in.out, -1, 0});
           } else {
             stack_.push_back({in.out, -1, 0});
@@ -901,12 +901,12 @@ class Machine {
     for (uint32_t j = 0; j < size_[rq]; ++j) {
       if (!dense_has_[rq][j]) continue;
       const Inst& in = p_.inst[dense_pc_[rq][j]];
-      int* tcap = ncap_ > 0 ? &caps_[rq][static_cast<size_t>(j) * ncap_] : nullptr;
+      Cap* tcap = ncap_ > 0 ? &caps_[rq][static_cast<size_t>(j) * ncap_] : nullptr;
       bool addit = false;
       switch (in.op) {
         case IOp::Match:
           if (ncap_ > 0) {
-            tcap[1] = static_cast<int>(pos);
+            tcap[1] = static_cast<Cap>(pos);
             std::copy(tcap, tcap + ncap_, matchcap_.begin());
           }
           matched_ = true;
@@ -1262,7 +1262,7 @@ std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string*
 }
 
 bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored, int ncap_wanted,
-                      int* caps) const {
+                      Cap* caps) const {
   if (prog_.start == 0) return false;
   // one Machine per (thread, Regexp): keyed by the Regexp's unique id
   thread_local std::vector<std::pair<uint64_t, std::unique_ptr<Machine>>> cache;
@@ -1317,7 +1317,7 @@ long Regexp::match_end(const uint8_t* text, size_t len, size_t pos) const {
   long e = d->match_end(text, len, pos);
   if (e == -2) {                        // state budget exceeded: start a fresh DFA next time, use the VM now
     for (auto& c : cache) if (c.first == id_) c.second.reset(new LazyDfa(prog_));
-    std::vector<int> caps(2 * (prog_.num_cap + 1));
+    std::vector<Cap> caps(2 * (prog_.num_cap + 1));
     e = match_at(text, len, pos, true, 0, caps.data()) ? caps[1] : -1;
   }
   return e;
@@ -1344,7 +1344,7 @@ static size_t seq_at(const std::vector<std::vector<std::string>>& seq, const uin
 
 bool Regexp::match_string(const uint8_t* text, size_t len) const {
   if (gate_.empty()) {
-    std::vector<int> caps(2 * (prog_.num_cap + 1));
+    std::vector<Cap> caps(2 * (prog_.num_cap + 1));
     return match_at(text, len, 0, false, 0, caps.data());
   }
   auto hit_at = [&](size_t i) {
@@ -1355,7 +1355,7 @@ bool Regexp::match_string(const uint8_t* text, size_t len) const {
   if (!gate_bounded_) {
     for (size_t i = 0; i < len; ++i) {
       if (hit_at(i)) {
-        std::vector<int> caps(2 * (prog_.num_cap + 1));
+        std::vector<Cap> caps(2 * (prog_.num_cap + 1));
         return match_at(text, len, 0, false, 0, caps.data());
       }
     }
@@ -1363,7 +1363,7 @@ bool Regexp::match_string(const uint8_t* text, size_t len) const {
   }
   // every match starts gate_dmin_..gate_dmax_ bytes before a gate literal
   std::vector<uint8_t> tried;
-  std::vector<int> caps;
+  std::vector<Cap> caps;
   for (size_t i = gate_dmin_; i < len; ++i) {
     if (!hit_at(i)) continue;
     if (tried.empty()) { tried.assign(len + 1, 0); caps.resize(2 * (prog_.num_cap + 1)); }
@@ -1377,9 +1377,9 @@ bool Regexp::match_string(const uint8_t* text, size_t len) const {
   return false;
 }
 
-void Regexp::find_all(const uint8_t* text, size_t len, bool submatch, std::vector<int>* out) const {
+void Regexp::find_all(const uint8_t* text, size_t len, bool submatch, std::vector<Cap>* out) const {
   const int ncap = 2 * (prog_.num_cap + 1);
-  std::vector<int> caps(ncap);
+  std::vector<Cap> caps(ncap);
   size_t pos = 0;
   long prev_end = -1;
   while (pos <= len) {

@@ -30,6 +30,9 @@ enum class Op : uint8_t {
 
 struct Range { uint32_t lo, hi; };
 
+// Match offsets (64-bit: files of 2 GiB and more are valid Go []byte inputs).
+using Cap = int64_t;
+
 struct Node {
   Op op = Op::EmptyMatch;
   bool nongreedy = false;
@@ -124,7 +127,7 @@ class Regexp {
   // If `anchored`, only a match starting exactly at `pos` is considered.
   // caps receives 2*(num_subexp+1) offsets (-1 for non-participating groups).
   bool match_at(const uint8_t* text, size_t len, size_t pos, bool anchored, int ncap_wanted,
-                int* caps) const;
+                Cap* caps) const;
   // End offset of the leftmost-first match anchored at `pos` (-1: none),
   // from a lazily built DFA (no captures); equals match_at(.., true, ..)'s caps[1].
   long match_end(const uint8_t* text, size_t len, size_t pos) const;
@@ -141,7 +144,7 @@ class Regexp {
   }
   const LitGate& gate() const { return gate_; }
   // Regexp.FindAll(Submatch)Index(text, -1): flattened vectors of 2 (or 2*(ncap+1)) ints.
-  void find_all(const uint8_t* text, size_t len, bool submatch, std::vector<int>* out) const;
+  void find_all(const uint8_t* text, size_t len, bool submatch, std::vector<Cap>* out) const;
   // Minimal byte length of a match (used by the prefilter to reject nullable rules).
   bool nullable() const { return nullable_; }
 

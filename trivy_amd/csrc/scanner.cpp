@@ -298,9 +298,9 @@ bool chain_boundary(const uint8_t* t, size_t len, size_t pos, size_t s) {
 
 void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t len,
                               const std::vector<uint64_t>& starts, bool submatch,
-                              std::vector<int>* out) {
+                              std::vector<re::Cap>* out) {
   const int ncap = 2 * (re.num_subexp() + 1);
-  std::vector<int> caps(ncap);
+  std::vector<re::Cap> caps(ncap);
   size_t pos = 0;
   long prev_end = -1;
   size_t idx = 0;
@@ -319,8 +319,8 @@ void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t 
           if (submatch) {
             if (!re.match_at(text, len, s, true, ncap, caps.data())) { ++idx; continue; }
           } else {
-            caps[0] = static_cast<int>(s);
-            caps[1] = static_cast<int>(e);
+            caps[0] = static_cast<re::Cap>(s);
+            caps[1] = static_cast<re::Cap>(e);
           }
           found = true;
           break;
@@ -376,7 +376,7 @@ class Blocks {
   bool match(const Loc& l) {
     if (!done_) {
       done_ = true;
-      std::vector<int> m;
+      std::vector<re::Cap> m;
       for (size_t j = 0; j < rx_.size(); ++j) {
         const auto& r = rx_[j];
         if (!r) continue;
@@ -412,12 +412,12 @@ void find_locations(const Ruleset& rs, const Rule& rule, const uint8_t* c, size_
                     const std::vector<uint64_t>* starts, std::vector<Loc>* locs, int* error) {
   if (!rule.regex) return;
   const bool sub = !rule.secret_group_name.empty();
-  std::vector<int> m;
+  std::vector<re::Cap> m;
   if (starts) find_all_from_candidates(*rule.regex, c, n, *starts, sub, &m);
   else rule.regex->find_all(c, n, sub, &m);
   const size_t stride = sub ? 2 * (rule.regex->num_subexp() + 1) : 2;
   for (size_t k = 0; k + stride <= m.size(); k += stride) {
-    const int s = m[k], e = m[k + 1];
+    const long s = m[k], e = m[k + 1];
     // AllowLocation (scanner.go:150-153): global then rule allow regexes on the whole match
     if (allow_match(rs.allow_rules, c + s, e - s) || allow_match(rule.allow_rules, c + s, e - s)) continue;
     if (!sub) { locs->push_back({s, e}); continue; }
@@ -610,9 +610,12 @@ class CensoredView {
       data_ = nl->data;
       off_ = nl->file_off;
       first_ = off_ / ch_;
+      // prefix_at(g) reads local_[g / ch_ - first_] for g <= off_ + n: only
+      // chunks strictly below (off_ + n) / ch_ are summed, so a file ending
+      // exactly on the batch's last chunk boundary reads no count past the end
       const uint64_t last = (off_ + n) / ch_;
-      local_.assign(last - first_ + 2, 0);
-      for (uint64_t k = first_; k <= last; ++k) local_[k - first_ + 1] = local_[k - first_] + nl->chunk_nl[k];
+      local_.assign(last - first_ + 1, 0);
+      for (uint64_t k = first_; k < last; ++k) local_[k - first_ + 1] = local_[k - first_] + nl->chunk_nl[k];
     } else {
       // local prefix over this file (reference / host-only paths)
       ch_ = 4096;

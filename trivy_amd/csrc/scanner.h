@@ -122,7 +122,7 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
 // match can start; the result equals re.find_all(text).
 void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t len,
                               const std::vector<uint64_t>& starts, bool submatch,
-                              std::vector<int>* out);
+                              std::vector<re::Cap>* out);
 
 // SecretAnalyzer helpers (pkg/fanal/analyzer/secret/secret.go:103-190, utils.go:68-143)
 bool go_is_binary(const uint8_t* head, size_t n);

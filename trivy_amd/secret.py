@@ -42,8 +42,17 @@ _GoStringLoader.yaml_implicit_resolvers = {
 
 
 def load_yaml(path):
+    """yaml.v3 Decoder.Decode of the file's FIRST document.  An input with no
+    document at all (empty, or only comments) is io.EOF, which ParseConfig
+    reports as "secrets config decode error: EOF" (scanner.go:296-298); an
+    explicit null document decodes to the zero Config."""
     with open(path, "rb") as f:
-        return yaml.load(f, Loader=_GoStringLoader)  # noqa: S506 (SafeLoader subclass)
+        text = f.read()
+    docs = yaml.load_all(text, Loader=_GoStringLoader)  # noqa: S506 (SafeLoader subclass)
+    try:
+        return next(docs)
+    except StopIteration:
+        raise ConfigError("secrets config decode error: EOF") from None
 
 
 @dataclass
@@ -63,7 +72,7 @@ def ParseConfig(config_path):
         doc = load_yaml(config_path)
     except yaml.YAMLError as e:
         raise ConfigError("secrets config decode error: %s" % e)
-    if doc is None:
+    if doc is None:                    # explicit null document: zero Config
         doc = {}
     if not isinstance(doc, dict):
         raise ConfigError("secrets config decode error: not a mapping")

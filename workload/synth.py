@@ -260,15 +260,16 @@ def rule_samples(rules, rng, per_rule=24):
     return out
 
 
-_SAMPLES_CACHE = os.path.join(_HERE, "data", "rule_samples.json")
+_SAMPLES_CACHE = os.path.join(_HERE, "rule_samples.json")
+_BUILTIN_JSON = os.path.join(_HERE, "..", "trivy_amd", "data", "builtin_rules.json")
 
 
 def load_samples(seed=DEFAULT_SEED):
-    """Cached plant strings (trivy_amd/data/rule_samples.json, generated here
+    """Cached plant strings (workload/rule_samples.json, generated here
     once with the oracle so the GPU box needs no oracle import to build a corpus)."""
     if os.path.exists(_SAMPLES_CACHE):
         return json.load(open(_SAMPLES_CACHE))
-    rules = json.load(open(os.path.join(_HERE, "data", "builtin_rules.json")))["rules"]
+    rules = json.load(open(_BUILTIN_JSON))["rules"]
     s = rule_samples(rules, random.Random(seed))
     with open(_SAMPLES_CACHE, "w") as f:
         json.dump(s, f, indent=0, ensure_ascii=False)
