@@ -98,13 +98,19 @@ def test_table(src, marker):
     return golit.parse_expr_at(src, j + len("\n\t}"))
 
 
+def stored(name):
+    """Fixture file name in the repo: *.pyc inputs are kept as *.pyc.data
+    (repo snapshots sent to the GPU box drop Python caches, *.pyc included)."""
+    return name + ".data" if name.endswith(".pyc") else name
+
+
 def copy_data(names, srcdir, dstdir):
     os.makedirs(dstdir, exist_ok=True)
     for n in sorted(set(names)):
         if not n:
             continue
         s = os.path.join(srcdir, n)
-        d = os.path.join(dstdir, n)
+        d = os.path.join(dstdir, stored(n))
         os.makedirs(os.path.dirname(d), exist_ok=True)
         shutil.copyfile(s, d)
 
@@ -141,7 +147,7 @@ def analyzer_cases(env):
         if want is not None:
             secrets = [ctx.secret(s) for s in want.get("Secrets").items]
         cases.append({"name": k["name"], "config": k.get("configPath", ""),
-                      "input": k["filePath"], "path": k["filePath"], "dir": k.get("dir", ""),
+                      "input": stored(k["filePath"]), "path": k["filePath"], "dir": k.get("dir", ""),
                       "want": secrets, "ref": "pkg/fanal/analyzer/secret/secret_test.go:16-214"})
         files += [k.get("configPath", ""), k["filePath"]]
     # TestSecretRequire (:216-258)

@@ -42,13 +42,17 @@ def test_config3_parity_cpu(seed, sizes):
 
 
 @pytest.mark.gpu
-def test_config3_many_files_gpu():
-    args = _args(30_000_000, 33, "tiny")
-    assert len(args) > 50_000
+@pytest.mark.parametrize("nbytes,many", [(30_000_000, True), (6_000_000, False)])
+def test_config3_many_files_gpu(nbytes, many):
+    # Engine::scan sets up the per-file result slots on a separate driver
+    # thread for batches of >= 65536 files (kManyFiles) and in line below
+    # that: both branches are pinned to the host confirmer
+    args = _args(nbytes, 33, "tiny")
+    assert (len(args) >= 1 << 16) == many, len(args)
     sc = S.Scanner(None)
     got = sc.ScanBatch(args)
     host = S.scan_host_reference(sc, args, threads=16)
-    assert sum(len(h["Findings"]) for h in host) > 100
+    assert sum(len(h["Findings"]) for h in host) > (100 if many else 10)
     for a, g, h in zip(args, got, host):
         assert g == h, a.FilePath
     ref = so.Scanner(None)
