@@ -27,8 +27,11 @@
  *     not necessarily valid UTF-8, not NUL-terminated unless stated.
  *   - ownership: the caller owns every input buffer until the call returns;
  *     the library owns every tsg_* object until its *_free/_destroy call.
- *   - threading: a tsg_ruleset is immutable and may be shared; a tsg_engine
- *     serialises calls internally (one HIP stream per engine).
+ *   - threading: a tsg_ruleset is immutable and may be shared.  A tsg_engine
+ *     may be shared too: concurrent tsg_scan_batch calls each take their own
+ *     lane (compute + copy HIP streams and scratch buffers) on every device
+ *     and their own host confirm pool, as the reference's Scan is called
+ *     concurrently from --parallel goroutines (analyzer.go:434-451).
  *   - there is no CPU fallback: tsg_engine_create fails with
  *     TSG_ERR_NO_DEVICE when no MI355X (HIP device) is visible.
  */
@@ -82,8 +85,11 @@ typedef struct tsg_stats {
   uint64_t bytes, files, hits, candidates, confirm_files, findings;
   uint32_t k1_blocks, k1_threads, chunk_bytes;
   int32_t table_in_lds;
-  double gpu_wall_ms;   /* wall time of the GPU phase incl. launches, syncs and copies */
-  uint32_t pieces;      /* pipeline pieces the batch was cut into (GPU of piece i+1 || host of piece i) */
+  double gpu_wall_ms;   /* device driver threads' busy time (sum over devices) */
+  uint32_t pieces;      /* pipeline segments the batch was cut into */
+  uint32_t k1_launches; /* K1 launches (segments x scan-DFA groups) */
+  uint32_t devices;     /* devices that took part */
+  double feed_ms;       /* uploaded batches: wall time until the last segment's upload had landed */
 } tsg_stats;
 
 const char* tsg_last_error(void);
@@ -106,7 +112,11 @@ const char* tsg_engine_report(const tsg_engine* e);
 const char* tsg_builtin_rules_json(void);
 
 int tsg_device_count(void);
-int tsg_engine_create(const tsg_ruleset* rs, int device, tsg_engine** out);
+/* device_mask: bit d selects HIP device d (0 = every visible device).  With
+ * several devices one tsg_scan_batch call is spread over all of them: the
+ * batch is cut into segments (TSG_SEGMENT_BYTES, default 512 MB) that each
+ * device's driver thread pulls from a shared queue. */
+int tsg_engine_create(const tsg_ruleset* rs, uint64_t device_mask, tsg_engine** out);
 void tsg_engine_destroy(tsg_engine* e);
 /* host worker threads for exact confirmation (0 = min(16, hardware)) */
 void tsg_engine_set_threads(tsg_engine* e, int threads);
@@ -118,8 +128,11 @@ void tsg_free_pinned(void* p);
 /* Scan a batch of nfiles files packed back to back in `data`
  * (offsets[0] = 0, offsets[nfiles] = total bytes).  paths[i] has length
  * path_lens[i] (or is NUL-terminated when path_lens is NULL).  binary may be
- * NULL (all false).  The batch is copied to HBM, scanned by the GPU kernels,
- * and confirmed exactly on the host.  result[i] == Scanner.Scan(args[i]). */
+ * NULL (all false).  The batch is streamed to HBM in segments (upload of
+ * segment k+1 overlapping the kernels of segment k and the host confirmation
+ * of segment k-1), scanned by the GPU kernels, and confirmed exactly on the
+ * host.  result[i] == Scanner.Scan(args[i]).  `data` should be pinned
+ * (tsg_alloc_pinned) for full PCIe rate; pageable memory works, slower. */
 int tsg_scan_batch(tsg_engine* e, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                    const char* const* paths, const uint32_t* path_lens, const uint8_t* binary,
                    tsg_result** out);
@@ -133,6 +146,11 @@ int tsg_scan_batch_resident(tsg_engine* e, const void* d_data, const uint8_t* h_
  * findings (used to time the kernels in isolation). */
 int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data,
                            const uint64_t* offsets, uint32_t nfiles, tsg_result** out);
+
+/* Host-feed ceiling: stream `bytes` of host memory (pinned for full rate) to
+ * HBM through the engine's upload path in segments, with no kernels; *ms =
+ * wall time.  Reported beside scan rates, never used by a scan. */
+int tsg_feed_probe(tsg_engine* e, const uint8_t* data, uint64_t bytes, double* ms);
 
 uint32_t tsg_result_num_files(const tsg_result* r);
 /* types.Secret.FilePath of file i ("" for types.Secret{}) */

@@ -82,8 +82,9 @@ def test_pipelined_pieces_on_gpu(monkeypatch):
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     ref = so.Scanner(None)
     want = [ref.scan(a.FilePath, a.Content) for a in args]
-    monkeypatch.setenv("TSG_PIECES", "5")
+    monkeypatch.setenv("TSG_PIECES", "5")                 # resident entry point: pieces
     monkeypatch.setenv("TSG_MIN_PIECE_BYTES", "1")
+    monkeypatch.setenv("TSG_SEGMENT_BYTES", str(256 << 10))   # upload entry point: segments
     sc = S.Scanner(None)
     got, stats = sc.ScanBatch(args, with_stats=True)
     assert stats["pieces"] > 1

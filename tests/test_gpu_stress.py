@@ -1,7 +1,7 @@
 """GPU stress parity:
 
 * config 2's size model (log-uniform 64 B - 64 MB) with a whole 64 MB file in
-  the batch, the batch cut into several pipeline pieces: every file equals the
+  the batch, the batch cut into several pipeline segments: every file equals the
   C++ exact confirmer run without the GPU prefilter (tsg_scan_host_reference,
   itself pinned to the oracle by the CPU suite), and a sample equals the
   oracle;
@@ -34,8 +34,7 @@ def _config2_args():
 def test_config2_loguniform_pieces_gpu(monkeypatch):
     args = _config2_args()
     assert max(len(a.Content) for a in args) >= 64 << 20
-    monkeypatch.setenv("TSG_PIECES", "4")
-    monkeypatch.setenv("TSG_MIN_PIECE_BYTES", str(16 << 20))
+    monkeypatch.setenv("TSG_SEGMENT_BYTES", str(48 << 20))
     sc = S.Scanner(None)
     got, stats = sc.ScanBatch(args, with_stats=True)
     assert stats["pieces"] >= 3

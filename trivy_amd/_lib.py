@@ -21,7 +21,8 @@ class TsgStats(ctypes.Structure):
                 ("candidates", ctypes.c_uint64), ("confirm_files", ctypes.c_uint64), ("findings", ctypes.c_uint64),
                 ("k1_blocks", ctypes.c_uint32), ("k1_threads", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
                 ("table_in_lds", ctypes.c_int32), ("gpu_wall_ms", ctypes.c_double),
-                ("pieces", ctypes.c_uint32)]
+                ("pieces", ctypes.c_uint32), ("k1_launches", ctypes.c_uint32), ("devices", ctypes.c_uint32),
+                ("feed_ms", ctypes.c_double)]
 
 
 # (name, restype, argtypes) for every entry point declared in include/trivy_secret.h
@@ -36,7 +37,7 @@ SIGNATURES = [
     ("tsg_engine_report", ctypes.c_char_p, [ctypes.c_void_p]),
     ("tsg_builtin_rules_json", ctypes.c_char_p, []),
     ("tsg_device_count", ctypes.c_int, []),
-    ("tsg_engine_create", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_engine_create", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_engine_destroy", None, [ctypes.c_void_p]),
     ("tsg_engine_set_threads", None, [ctypes.c_void_p, ctypes.c_int]),
     ("tsg_alloc_pinned", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
@@ -48,6 +49,8 @@ SIGNATURES = [
                                                 ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_prefilter_resident", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_feed_probe", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.POINTER(ctypes.c_double)]),
     ("tsg_result_num_files", ctypes.c_uint32, [ctypes.c_void_p]),
     ("tsg_result_file_path", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
                                              ctypes.POINTER(ctypes.c_size_t)]),

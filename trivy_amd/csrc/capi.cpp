@@ -27,8 +27,7 @@ struct tsg_ruleset {
 };
 
 struct tsg_engine {
-  std::unique_ptr<Engine> eng;
-  std::mutex mu;
+  std::unique_ptr<Engine> eng;   // reentrant: every call takes its own lanes (streams + buffers)
   std::string report;
 };
 
@@ -83,10 +82,23 @@ int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len) 
 
 int tsg_device_count(void) { return device_count(); }
 
-int tsg_engine_create(const tsg_ruleset* rs, int device, tsg_engine** out) {
+int tsg_engine_create(const tsg_ruleset* rs, uint64_t device_mask, tsg_engine** out) {
   if (!rs || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string err;
-  auto eng = Engine::create(rs->rs, device, &err);
+  const int n = device_count();
+  if (n <= 0) return fail(TSG_ERR_NO_DEVICE, "no HIP device available (the GPU engine has no CPU fallback)");
+  std::vector<int> devs;
+  for (int d = 0; d < n && d < 64; ++d) if (device_mask == 0 || ((device_mask >> d) & 1u)) devs.push_back(d);
+  if (devs.empty()) return fail(TSG_ERR_INVALID, "device_mask selects no visible HIP device");
+  // TSG_ENGINE_REPLICAS=k: each selected device appears k times (several
+  // drivers share one device; exercises the multi-device queue on one GPU)
+  if (const char* r = std::getenv("TSG_ENGINE_REPLICAS")) {
+    const int k = std::atoi(r);
+    std::vector<int> rep;
+    for (int i = 0; i < std::max(1, std::min(k, 8)); ++i) rep.insert(rep.end(), devs.begin(), devs.end());
+    devs = rep;
+  }
+  auto eng = Engine::create(rs->rs, devs, &err);
   if (!eng) return fail(device_count() <= 0 ? TSG_ERR_NO_DEVICE : TSG_ERR_HIP, err);
   auto* e = new tsg_engine();
   e->report = eng->prefilter().report;
@@ -119,10 +131,7 @@ static int do_scan(tsg_engine* e, const void* d_data, const uint8_t* h_data, con
   auto* r = new tsg_result();
   r->rs = e->eng->ruleset();
   std::string err;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (!e->eng->scan(in, &r->files, &r->stats, &err)) { delete r; return fail(TSG_ERR_HIP, err); }
-  }
+  if (!e->eng->scan(in, &r->files, &r->stats, &err)) { delete r; return fail(TSG_ERR_HIP, err); }
   *out = r;
   return TSG_OK;
 }
@@ -149,12 +158,16 @@ int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_d
   in.nfiles = nfiles;
   auto* r = new tsg_result();
   std::string err;
-  {
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (!e->eng->prefilter_only(in, nullptr, &r->cands, &r->stats, &err)) { delete r; return fail(TSG_ERR_HIP, err); }
-  }
+  if (!e->eng->prefilter_only(in, &r->cands, &r->stats, &err)) { delete r; return fail(TSG_ERR_HIP, err); }
   r->files.resize(nfiles);
   *out = r;
+  return TSG_OK;
+}
+
+int tsg_feed_probe(tsg_engine* e, const uint8_t* data, uint64_t bytes, double* ms) {
+  if (!e || !ms || (bytes && !data)) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string err;
+  if (!e->eng->feed_probe(data, bytes, ms, &err)) return fail(TSG_ERR_HIP, err);
   return TSG_OK;
 }
 
@@ -301,6 +314,9 @@ int tsg_result_stats(const tsg_result* r, tsg_stats* out) {
   out->table_in_lds = s.table_in_lds;
   out->gpu_wall_ms = s.gpu_wall_ms;
   out->pieces = s.pieces;
+  out->k1_launches = s.k1_launches;
+  out->devices = s.devices;
+  out->feed_ms = s.feed_ms;
   return TSG_OK;
 }
 

@@ -1,8 +1,12 @@
-// GPU engine: device-resident rule tables + per-batch scan on one MI355X.
+// GPU engine: device-resident rule tables on one or more MI355X devices and
+// the batch pipeline (upload -> K1 -> K2 -> candidates -> exact host confirm).
 #pragma once
+#include <atomic>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -13,10 +17,13 @@ namespace tsg {
 
 struct ScanStats {
   double k1_ms = 0, k2_ms = 0, h2d_ms = 0, d2h_ms = 0, host_ms = 0, total_ms = 0;
-  double gpu_wall_ms = 0;               // run_gpu() wall time (launches + syncs + copies)
+  double gpu_wall_ms = 0;               // sum over devices of the driver threads' busy time
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, confirm_files = 0, findings = 0;
   uint32_t k1_blocks = 0, k1_threads = 0, chunk_bytes = 0, pieces = 1;
   int table_in_lds = 0;
+  uint32_t k1_launches = 0;             // K1 launches (segments x scan-DFA groups)
+  uint32_t devices = 1;                 // devices that took part
+  double feed_ms = 0;                   // wall time from the first upload to the last segment's upload done
 };
 
 struct BatchInput {
@@ -29,40 +36,71 @@ struct BatchInput {
   const uint8_t* binary = nullptr;     // optional ScanArgs.Binary flags
 };
 
+struct DeviceTables;
+struct Lane;
+struct GpuOut;
+struct CallCtx;
+
+// One engine = the compiled ruleset's device tables on every selected device.
+// scan() is reentrant: each call takes its own lane (HIP streams + scratch
+// buffers) on every device it uses and its own host confirm pool.
 class Engine {
  public:
-  // Fails (returns nullptr, *err set) when no HIP device is available: the
-  // product path has no CPU fallback.
-  static std::unique_ptr<Engine> create(std::shared_ptr<const Ruleset> rs, int device, std::string* err);
+  // devices: HIP device ordinals (may repeat one ordinal: replicas on one
+  // device, used to exercise the multi-device queue on a one-GPU machine).
+  // Fails (nullptr, *err set) when no HIP device is available: the product
+  // path has no CPU fallback.
+  static std::unique_ptr<Engine> create(std::shared_ptr<const Ruleset> rs, const std::vector<int>& devices,
+                                        std::string* err);
   ~Engine();
 
-  // Scan one batch; results[i] is Scanner.Scan(ScanArgs{paths[i], data[off[i]:off[i+1]], binary[i]}).
+  // results[i] is Scanner.Scan(ScanArgs{paths[i], data[off[i]:off[i+1]], binary[i]}).
   bool scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* stats, std::string* err);
 
-  // Only the two GPU passes (no host confirmation): used by bench.py to time
-  // the kernels in isolation and by tests to compare raw candidates.
-  bool prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate /*nfiles*nrules or null*/,
-                      std::vector<std::vector<std::vector<uint64_t>>>* cands /*[file][rule] or null*/,
+  // Only the two GPU passes (no host confirmation): used by tests to compare
+  // raw candidates.  Resident data on the engine's first device.
+  bool prefilter_only(const BatchInput& in, std::vector<std::vector<std::vector<uint64_t>>>* cands,
                       ScanStats* stats, std::string* err);
+
+  // Host-feed ceiling (no kernels): streams `bytes` of host memory through
+  // the first device's upload ring in segment_ pieces, as scan() does, and
+  // returns the wall time in ms.
+  bool feed_probe(const uint8_t* h_data, uint64_t bytes, double* ms, std::string* err);
 
   const Prefilter& prefilter() const { return pf_; }
   std::shared_ptr<const Ruleset> ruleset() const { return rs_; }
-  int device() const { return device_; }
+  const std::vector<int>& devices() const { return devices_; }
   void set_threads(int n) { threads_ = n; }
-
-  struct Impl;
-  struct GpuOut;
 
  private:
   Engine() = default;
-  bool run_gpu(const BatchInput& in, ScanStats* stats, GpuOut* out, std::string* err);
-  void confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf, uint64_t* nfind,
-                     bool gpu_in_flight);
+  struct Segment;
+  bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, ScanStats* st, GpuOut* out,
+                   std::string* err);
+  void confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Secret* results, uint64_t* nconf,
+                       uint64_t* nfind, bool gpu_in_flight);
+  Lane* acquire_lane(DeviceTables& dt, std::string* err);
+  void release_lane(DeviceTables& dt, Lane* ln);
+  CallCtx* acquire_call();
+  void release_call(CallCtx* cc);
+
   std::shared_ptr<const Ruleset> rs_;
   Prefilter pf_;
-  int device_ = 0;
+  std::vector<int> devices_;
+  std::vector<std::unique_ptr<DeviceTables>> dev_;
   int threads_ = 0;
-  std::unique_ptr<Impl> impl_;
+  std::mutex call_mu_;
+  std::vector<std::unique_ptr<CallCtx>> calls_;
+  std::vector<CallCtx*> free_calls_;
+  // tuning (TSG_* environment knobs, read once at create)
+  uint32_t chunk_ = 4096;               // K1 bytes per lane chunk (TSG_K1_CHUNK)
+  int k1_streams_ = 1;                  // TSG_K1_CFG="threads,streams"
+  uint32_t k1_threads_ = 1024;
+  uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)
+  double first_piece_ = 0.7;            // resident data: share of the first piece (TSG_FIRST_PIECE)
+  uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
+  uint64_t segment_ = 1ull << 30;       // uploaded data: bytes per pipeline segment (TSG_SEGMENT_BYTES);
+                                        // 1 GB = one full K1 round (256 CUs x 1024 lanes x 4 KiB chunks)
 };
 
 int device_count();

@@ -26,6 +26,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <thread>
 
 #include "engine.h"
@@ -568,17 +570,10 @@ struct K1Group {
   bool in_lds = false;
 };
 
-struct Engine::GpuOut {
-  std::vector<CandDev> cands;   // (file, rule, start) candidates, unsorted
-  std::vector<uint32_t> nl;     // '\n' count per K1 chunk
-  std::vector<uint32_t> ff;     // per-file flags (fold-special content)
-  uint32_t chunk = 0;           // K1 chunk bytes of this piece (nl[] granularity)
-};
-
-struct Engine::Impl {
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[6] = {};
-  // tables
+// The compiled rule tables on one device plus that device's pool of lanes.
+struct DeviceTables {
+  int device = 0;
+  int sms = 256;
   std::vector<K1Group> k1g;
   AnchorDev* anchors = nullptr;
   RuleDev* rules = nullptr;
@@ -588,35 +583,84 @@ struct Engine::Impl {
   uint8_t* v_acc = nullptr;
   uint8_t* v_cls = nullptr;
   uint32_t kw_words = 1;
-  // batch buffers
-  uint8_t* d_data = nullptr; size_t d_data_cap = 0;
+  std::mutex mu;                               // guards the lane pool
+  std::vector<std::unique_ptr<Lane>> lanes;
+  std::vector<Lane*> free_lanes;
+  ~DeviceTables();
+};
+
+// One in-flight call's resources on one device: its own streams (compute +
+// copy), timing events, the two-slot upload ring and every per-batch scratch
+// buffer, so concurrent calls never share mutable GPU state.
+struct Lane {
+  int device = 0;
+  hipStream_t compute = nullptr, copy = nullptr;
+  hipEvent_t ev[4] = {};                        // K1 start/end, K2 start/end (compute stream)
+  hipEvent_t up_begin[2] = {}, up_done[2] = {}; // upload ring slot: H2D start / done (copy stream)
+  uint8_t* ring[2] = {nullptr, nullptr};
+  size_t ring_cap[2] = {0, 0};
   uint64_t* d_off = nullptr; size_t d_off_cap = 0;
   uint32_t* d_kw = nullptr; size_t d_kw_cap = 0;
   unsigned long long* d_hits = nullptr; size_t d_hits_cap = 0;
   unsigned long long* d_over = nullptr; size_t d_over_cap = 0;   // hits past a full region (any workgroup)
   uint32_t* d_bh = nullptr; size_t d_bh_cap = 0;    // hits written per K1 workgroup (its region of d_hits)
-  std::vector<uint32_t> h_bh;
   CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
   uint32_t* d_nl = nullptr; size_t d_nl_cap = 0;
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   unsigned int* d_cnt = nullptr;
+  std::vector<uint32_t> h_bh;
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
-  // host copies of a piece's GPU results: two slots, so the GPU passes of
-  // piece i+1 overlap the host confirmation of piece i (Engine::scan)
-  std::vector<uint32_t> h_kw;
-  GpuOut out[2];
-  std::unique_ptr<ThreadPool> pool;
-  int sms = 256;
-  int k1_streams = 1;                 // interleaved DFA streams per K1 lane  } TSG_K1_CFG="threads,streams"
-  uint32_t k1_threads = 1024;         // K1 workgroup size                  }
-  uint32_t chunk = 4096;              // max bytes per K1 stream chunk (multiple of 128; TSG_K1_CHUNK)
-  bool adaptive_chunk = false;        // shrink the chunk to balance the last round (TSG_K1_ADAPTIVE=1; measured
-                                      // slower on MI355X: 3840-B chunks ran K1 at 1.6 vs 2.07 TB/s)
-  uint32_t pieces = 2;                // pipeline pieces per batch (TSG_PIECES)
-  double first_piece = 0.7;           // share of the first piece (TSG_FIRST_PIECE): the host idles
-                                      // through piece 0's GPU passes, the GPU through the last confirm
-  uint64_t min_piece = 256ull << 20;  // smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
+  ~Lane();
 };
+
+// GPU results of one segment, handed from a device driver thread to the
+// host confirmer.
+struct GpuOut {
+  std::vector<CandDev> cands;   // (file, rule, start) candidates, unsorted
+  std::vector<uint32_t> nl;     // '\n' count per K1 chunk
+  std::vector<uint32_t> ff;     // per-file flags (fold-special content)
+  uint32_t chunk = 0;           // K1 chunk bytes of this segment (nl[] granularity)
+};
+
+// One call's host confirm resources.
+struct CallCtx {
+  std::unique_ptr<ThreadPool> pool;
+};
+
+// A self-contained sub-batch: files [f0, f0 + in.nfiles) of the call's
+// batch, offsets rebased to 0, data pointers advanced to its first byte.
+struct Engine::Segment {
+  BatchInput in;
+  std::vector<uint64_t> off;
+  uint32_t f0 = 0;
+  uint64_t b0 = 0, bytes = 0;
+};
+
+DeviceTables::~DeviceTables() {
+  hipSetDevice(device);
+  lanes.clear();
+  void* ps[] = {anchors, rules, rule_kw, vdfa, v_next, v_acc, v_cls};
+  for (void* p : ps) if (p) hipFree(p);
+  for (K1Group& g : k1g) {
+    void* gs[] = {g.next, g.cls, g.meta, g.list};
+    for (void* p : gs) if (p) hipFree(p);
+  }
+}
+
+Lane::~Lane() {
+  hipSetDevice(device);
+  if (compute) hipStreamSynchronize(compute);
+  if (copy) hipStreamSynchronize(copy);
+  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_cnt};
+  for (void* p : ps) if (p) hipFree(p);
+  for (auto& e : ev) if (e) hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i) {
+    if (up_begin[i]) hipEventDestroy(up_begin[i]);
+    if (up_done[i]) hipEventDestroy(up_done[i]);
+  }
+  if (compute) hipStreamDestroy(compute);
+  if (copy) hipStreamDestroy(copy);
+}
 
 int device_count() {
   int n = 0;
@@ -624,51 +668,15 @@ int device_count() {
   return n;
 }
 
-std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int device, std::string* err) {
-  int n = device_count();
-  if (n <= 0) { *err = "no HIP device available (the GPU engine has no CPU fallback)"; return nullptr; }
-  if (device < 0 || device >= n) { *err = "HIP device index out of range"; return nullptr; }
-  std::unique_ptr<Engine> e(new Engine());
-  e->rs_ = std::move(rs);
-  e->device_ = device;
-  if (!build_prefilter(*e->rs_, &e->pf_, err)) return nullptr;
-  e->impl_.reset(new Impl());
-  Impl& m = *e->impl_;
-  if (hipSetDevice(device) != hipSuccess) { *err = "hipSetDevice failed"; return nullptr; }
+namespace {
+
+// Upload the prefilter's tables to one device.
+bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
+  HIP_OK(hipSetDevice(dt->device));
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess) m.sms = prop.multiProcessorCount;
-  if (const char* c = std::getenv("TSG_PIECES")) {
-    const long v = std::atol(c);
-    if (v >= 1 && v <= 64) m.pieces = static_cast<uint32_t>(v);
-  }
-  if (const char* c = std::getenv("TSG_K1_ADAPTIVE")) m.adaptive_chunk = std::atoi(c) != 0;
-  if (const char* c = std::getenv("TSG_FIRST_PIECE")) {
-    const double v = std::atof(c);
-    if (v > 0.0 && v < 1.0) m.first_piece = v;
-  }
-  if (const char* c = std::getenv("TSG_MIN_PIECE_BYTES")) {
-    const long long v = std::atoll(c);
-    if (v >= 1) m.min_piece = static_cast<uint64_t>(v);
-  }
-  if (const char* cfg = std::getenv("TSG_K1_CFG")) {
-    unsigned t = 0, k = 0;
-    if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k))) {
-      m.k1_threads = t;
-      m.k1_streams = static_cast<int>(k);
-    }
-  }
-  if (const char* c = std::getenv("TSG_K1_CHUNK")) {
-    // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
-    // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
-    // chunks are clamped so the offset cannot wrap
-    const long v = std::atol(c);
-    if (v >= 256 && v % 128 == 0) m.chunk = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(m.k1_streams)));
-  }
-  if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess) { *err = "hipStreamCreate failed"; return nullptr; }
-  for (auto& ev : m.ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
-  const Prefilter& pf = e->pf_;
-  if (pf.anchors.size() >= (1u << kAnchorBits)) { *err = "too many anchor literals for K1's hit encoding"; return nullptr; }
-  m.kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
+  if (hipGetDeviceProperties(&prop, dt->device) == hipSuccess) dt->sms = prop.multiProcessorCount;
+  if (pf.anchors.size() >= (1u << kAnchorBits)) { *err = "too many anchor literals for K1's hit encoding"; return false; }
+  dt->kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
   for (const ScanDfa& sd : pf.groups) {
     K1Group g;
     // scan table with an odd dword row stride: next[s*stride + c] then spreads
@@ -686,9 +694,9 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
     // is then one add + one LDS read per byte (no multiply)
     if (static_cast<uint64_t>(sd.t.nstates) * stride > 65535) {
       *err = "scan DFA group too large for 16-bit pre-multiplied offsets";
-      return nullptr;
+      return false;
     }
-    if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return nullptr; }
+    if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return false; }
     std::vector<uint16_t> sn(static_cast<size_t>(sd.t.nstates) * stride, 0);
     for (uint32_t st = 0; st < sd.t.nstates; ++st) {
       for (uint32_t c = 0; c < C; ++c)
@@ -721,10 +729,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
     for (int b = 0; b < 256; ++b) cls[b] = static_cast<uint8_t>(sd.t.byte_class[b] * 2);
     if (!dev_upload(sn, &g.next, err) || !dev_upload(cls, &g.cls, err) || !dev_upload(meta, &g.meta, err) ||
         !dev_upload(olist, &g.list, err)) {
-      return nullptr;
+      return false;
     }
-    m.kw_words = std::max<uint32_t>(m.kw_words, g.kw_base / 32 + 4);   // a group's masks span 4 words from kw_base
-    m.k1g.push_back(g);
+    dt->kw_words = std::max<uint32_t>(dt->kw_words, g.kw_base / 32 + 4);   // a group's masks span 4 words from kw_base
+    dt->k1g.push_back(g);
   }
   std::vector<AnchorDev> an;
   for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
@@ -745,115 +753,248 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, int de
     vc.insert(vc.end(), t.byte_class, t.byte_class + 256);
     vd.push_back(d);
   }
-  if (!dev_upload(an, &m.anchors, err) || !dev_upload(rd, &m.rules, err) ||
-      !dev_upload(pf.rule_kw, &m.rule_kw, err) || !dev_upload(vd, &m.vdfa, err) ||
-      !dev_upload(vn, &m.v_next, err) || !dev_upload(va, &m.v_acc, err) || !dev_upload(vc, &m.v_cls, err)) {
-    return nullptr;
+  return dev_upload(an, &dt->anchors, err) && dev_upload(rd, &dt->rules, err) &&
+         dev_upload(pf.rule_kw, &dt->rule_kw, err) && dev_upload(vd, &dt->vdfa, err) &&
+         dev_upload(vn, &dt->v_next, err) && dev_upload(va, &dt->v_acc, err) && dev_upload(vc, &dt->v_cls, err);
+}
+
+// Device of a device pointer (-1: not a device allocation).
+int device_of(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return -1; }
+  if (a.type != hipMemoryTypeDevice) return -1;
+  return a.device;
+}
+
+// Blocking hand-off of finished segments from the device drivers to the confirmer.
+template <typename T>
+class JobQueue {
+ public:
+  JobQueue(int producers, size_t cap) : producers_(producers), cap_(cap) {}
+  void push(std::unique_ptr<T> j) {
+    std::unique_lock<std::mutex> lk(mu_);
+    space_.wait(lk, [&] { return q_.size() < cap_ || aborted_; });
+    q_.push_back(std::move(j));
+    ready_.notify_one();
   }
-  if (hipMalloc(&m.d_cnt, 64) != hipSuccess) { *err = "hipMalloc counters failed"; return nullptr; }
+  void producer_done() {
+    std::lock_guard<std::mutex> lk(mu_);
+    --producers_;
+    ready_.notify_all();
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu_);
+    aborted_ = true;
+    space_.notify_all();
+    ready_.notify_all();
+  }
+  bool aborted() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return aborted_;
+  }
+  // nullptr once every producer is done and the queue is drained
+  std::unique_ptr<T> pop(int* producers_left) {
+    std::unique_lock<std::mutex> lk(mu_);
+    ready_.wait(lk, [&] { return !q_.empty() || producers_ == 0 || aborted_; });
+    *producers_left = producers_;
+    if (q_.empty()) return nullptr;
+    std::unique_ptr<T> j = std::move(q_.front());
+    q_.pop_front();
+    space_.notify_one();
+    return j;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable ready_, space_;
+  std::deque<std::unique_ptr<T>> q_;
+  int producers_;
+  size_t cap_;
+  bool aborted_ = false;
+};
+
+void add_stats(ScanStats* a, const ScanStats& s) {
+  a->k1_ms += s.k1_ms; a->k2_ms += s.k2_ms; a->h2d_ms += s.h2d_ms; a->d2h_ms += s.d2h_ms;
+  a->hits += s.hits; a->candidates += s.candidates; a->k1_launches += s.k1_launches;
+  a->k1_blocks = s.k1_blocks; a->k1_threads = s.k1_threads; a->chunk_bytes = s.chunk_bytes;
+  a->table_in_lds = s.table_in_lds;
+}
+
+}  // namespace
+
+std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const std::vector<int>& devices,
+                                       std::string* err) {
+  const int n = device_count();
+  if (n <= 0) { *err = "no HIP device available (the GPU engine has no CPU fallback)"; return nullptr; }
+  if (devices.empty()) { *err = "no device selected"; return nullptr; }
+  for (int d : devices) {
+    if (d < 0 || d >= n) { *err = "HIP device index out of range"; return nullptr; }
+  }
+  std::unique_ptr<Engine> e(new Engine());
+  e->rs_ = std::move(rs);
+  e->devices_ = devices;
+  if (!build_prefilter(*e->rs_, &e->pf_, err)) return nullptr;
+  if (const char* c = std::getenv("TSG_PIECES")) {
+    const long v = std::atol(c);
+    if (v >= 1 && v <= 64) e->pieces_ = static_cast<uint32_t>(v);
+  }
+  if (const char* c = std::getenv("TSG_FIRST_PIECE")) {
+    const double v = std::atof(c);
+    if (v > 0.0 && v < 1.0) e->first_piece_ = v;
+  }
+  if (const char* c = std::getenv("TSG_MIN_PIECE_BYTES")) {
+    const long long v = std::atoll(c);
+    if (v >= 1) e->min_piece_ = static_cast<uint64_t>(v);
+  }
+  if (const char* c = std::getenv("TSG_SEGMENT_BYTES")) {
+    const long long v = std::atoll(c);
+    if (v >= 4096) e->segment_ = static_cast<uint64_t>(v);
+  }
+  if (const char* cfg = std::getenv("TSG_K1_CFG")) {
+    unsigned t = 0, k = 0;
+    if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k))) {
+      e->k1_threads_ = t;
+      e->k1_streams_ = static_cast<int>(k);
+    }
+  }
+  if (const char* c = std::getenv("TSG_K1_CHUNK")) {
+    // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
+    // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
+    // chunks are clamped so the offset cannot wrap
+    const long v = std::atol(c);
+    if (v >= 256 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(e->k1_streams_)));
+  }
+  for (int d : devices) {
+    std::unique_ptr<DeviceTables> dt(new DeviceTables());
+    dt->device = d;
+    if (!build_tables(e->pf_, dt.get(), err)) return nullptr;
+    e->dev_.push_back(std::move(dt));
+  }
   return e;
 }
 
 Engine::~Engine() {
-  if (!impl_) return;
-  Impl& m = *impl_;
-  hipSetDevice(device_);
-  void* ps[] = {m.anchors, m.rules, m.rule_kw, m.vdfa, m.v_next, m.v_acc, m.v_cls, m.d_data, m.d_off, m.d_kw,
-                m.d_hits, m.d_over, m.d_bh, m.d_cands, m.d_nl, m.d_cnt, m.d_ff};
-  for (void* p : ps) if (p) hipFree(p);
-  for (K1Group& g : m.k1g) {
-    void* gs[] = {g.next, g.cls, g.meta, g.list};
-    for (void* p : gs) if (p) hipFree(p);
-  }
-  for (auto& ev : m.ev) if (ev) hipEventDestroy(ev);
-  if (m.stream) hipStreamDestroy(m.stream);
+  dev_.clear();
+  calls_.clear();
 }
 
-bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::string* err) {
-  Impl& m = *impl_;
-  HIP_OK(hipSetDevice(device_));
-  const uint64_t total = in.offsets[in.nfiles] - in.offsets[0];
-  if (in.offsets[0] != 0) { *err = "offsets[0] must be 0"; return false; }
-  for (uint32_t i = 0; i < in.nfiles; ++i) {
-    if (in.offsets[i + 1] < in.offsets[i]) { *err = "offsets must be non-decreasing"; return false; }
+Lane* Engine::acquire_lane(DeviceTables& dt, std::string* err) {
+  {
+    std::lock_guard<std::mutex> lk(dt.mu);
+    if (!dt.free_lanes.empty()) {
+      Lane* l = dt.free_lanes.back();
+      dt.free_lanes.pop_back();
+      return l;
+    }
   }
-  st->bytes = total;
-  st->files = in.nfiles;
-  // chunk size: at most m.chunk, shrunk so that every lane of the one-
-  // workgroup-per-CU grid gets the same whole number R of chunks (a launch
-  // lasts R chunk-times; a fixed chunk leaves the last round part-empty)
-  uint32_t kChunk = m.chunk;
-  if (m.adaptive_chunk) {
-    const uint64_t lanes = static_cast<uint64_t>(m.sms) * m.k1_threads * static_cast<uint64_t>(m.k1_streams);
-    const uint64_t per_lane = (total + lanes - 1) / std::max<uint64_t>(lanes, 1);
-    const uint64_t rounds = std::max<uint64_t>(1, (per_lane + m.chunk - 1) / m.chunk);
-    const uint64_t c = ((per_lane + rounds - 1) / rounds + 127) / 128 * 128;
-    kChunk = static_cast<uint32_t>(std::min<uint64_t>(m.chunk, std::max<uint64_t>(1024, c)));
+  std::unique_ptr<Lane> l(new Lane());
+  l->device = dt.device;
+  if (hipSetDevice(dt.device) != hipSuccess || hipStreamCreateWithFlags(&l->compute, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&l->copy, hipStreamNonBlocking) != hipSuccess || hipMalloc(&l->d_cnt, 64) != hipSuccess) {
+    *err = "lane setup (streams, counters) failed";
+    return nullptr;
   }
-  if (kChunk > k1_max_chunk(m.k1_streams) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
+  for (auto& ev : l->ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
+  for (int i = 0; i < 2; ++i) {
+    if (hipEventCreate(&l->up_begin[i]) != hipSuccess || hipEventCreate(&l->up_done[i]) != hipSuccess) {
+      *err = "hipEventCreate failed";
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> lk(dt.mu);
+  dt.lanes.push_back(std::move(l));
+  return dt.lanes.back().get();
+}
+
+void Engine::release_lane(DeviceTables& dt, Lane* ln) {
+  std::lock_guard<std::mutex> lk(dt.mu);
+  dt.free_lanes.push_back(ln);
+}
+
+CallCtx* Engine::acquire_call() {
+  std::lock_guard<std::mutex> lk(call_mu_);
+  const int nt = threads_ > 0 ? threads_ : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+  CallCtx* cc = nullptr;
+  if (!free_calls_.empty()) {
+    cc = free_calls_.back();
+    free_calls_.pop_back();
+  } else {
+    calls_.emplace_back(new CallCtx());
+    cc = calls_.back().get();
+  }
+  if (!cc->pool || cc->pool->size() != nt) cc->pool.reset(new ThreadPool(nt));
+  return cc;
+}
+
+void Engine::release_call(CallCtx* cc) {
+  std::lock_guard<std::mutex> lk(call_mu_);
+  free_calls_.push_back(cc);
+}
+
+// K1 + K2 + candidate D2H of one segment whose bytes are at d_data on the
+// lane's device (resident, or landed by the lane's upload), on the lane's
+// compute stream.  Returns when the segment's results are on the host.
+bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, ScanStats* st,
+                         GpuOut* out, std::string* err) {
+  const BatchInput& in = sg.in;
+  HIP_OK(hipSetDevice(dt.device));
+  const uint64_t total = in.offsets[in.nfiles];
+  const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
+  if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
+  const uint32_t kChunk = chunk_;
+  if (kChunk > k1_max_chunk(k1_streams_) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
-  const uint8_t* d_data = static_cast<const uint8_t*>(in.d_data);
-  auto t_h2d = std::chrono::steady_clock::now();
-  if (!d_data) {
-    if (!ensure(&m.d_data, &m.d_data_cap, total + 64, err)) return false;
-    if (total) HIP_OK(hipMemcpyAsync(m.d_data, in.h_data, total, hipMemcpyHostToDevice, m.stream));
-    HIP_OK(hipMemsetAsync(m.d_data + total, 0, 64, m.stream));
-    d_data = m.d_data;
-  } else if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) {
-    *err = "device data must be 16-byte aligned";
-    return false;
-  }
-  if (!ensure(&m.d_off, &m.d_off_cap, in.nfiles + 1, err)) return false;
-  HIP_OK(hipMemcpyAsync(m.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, m.stream));
-  const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * m.kw_words;
-  if (!ensure(&m.d_kw, &m.d_kw_cap, kw_n, err)) return false;
+  hipStream_t s = ln.compute;
+  if (!ensure(&ln.d_off, &ln.d_off_cap, in.nfiles + 1, err)) return false;
+  HIP_OK(hipMemcpyAsync(ln.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * dt.kw_words;
+  if (!ensure(&ln.d_kw, &ln.d_kw_cap, kw_n, err)) return false;
   const unsigned long long nchunks = (total + kChunk - 1) / kChunk;
-  if (!ensure(&m.d_nl, &m.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
-  m.hit_cap = std::max<size_t>(m.hit_cap, total / 256);   // ~1 hit per 670 B on source text
-  if (!ensure(&m.d_hits, &m.d_hits_cap, m.hit_cap, err)) return false;
-  m.over_cap = std::max<size_t>(m.over_cap, total / 2048);
-  if (!ensure(&m.d_over, &m.d_over_cap, m.over_cap, err)) return false;
-  const uint32_t ngroups = static_cast<uint32_t>(m.k1g.size());
-  if (!ensure(&m.d_bh, &m.d_bh_cap, 2ull * std::max(m.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
-  if (!ensure(&m.d_ff, &m.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
-  HIP_OK(hipStreamSynchronize(m.stream));
-  st->h2d_ms = in.d_data ? 0.0 : ms_since(t_h2d);
+  if (!ensure(&ln.d_nl, &ln.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
+  ln.hit_cap = std::max<size_t>(ln.hit_cap, total / 256);   // ~1 hit per 670 B on source text
+  if (!ensure(&ln.d_hits, &ln.d_hits_cap, ln.hit_cap, err)) return false;
+  ln.over_cap = std::max<size_t>(ln.over_cap, total / 2048);
+  if (!ensure(&ln.d_over, &ln.d_over_cap, ln.over_cap, err)) return false;
+  const uint32_t ngroups = static_cast<uint32_t>(dt.k1g.size());
+  if (!ensure(&ln.d_bh, &ln.d_bh_cap, 2ull * std::max(dt.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
+  if (!ensure(&ln.d_ff, &ln.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
 
-  const uint32_t sms = static_cast<uint32_t>(m.sms);
+  const uint32_t sms = static_cast<uint32_t>(dt.sms);
   const Prefilter& pf = pf_;
   for (int attempt = 0; attempt < 3; ++attempt) {
-    HIP_OK(hipMemsetAsync(m.d_kw, 0, kw_n * sizeof(uint32_t), m.stream));
-    HIP_OK(hipMemsetAsync(m.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), m.stream));
-    HIP_OK(hipMemsetAsync(m.d_cnt, 0, 64, m.stream));
-    const int ks = m.k1_streams;
-    const uint32_t nthr = m.k1_threads;
+    HIP_OK(hipMemsetAsync(ln.d_kw, 0, kw_n * sizeof(uint32_t), s));
+    HIP_OK(hipMemsetAsync(ln.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), s));
+    HIP_OK(hipMemsetAsync(ln.d_cnt, 0, 64, s));
+    const int ks = k1_streams_;
+    const uint32_t nthr = k1_threads_;
     const uint64_t want_blocks = (nchunks + static_cast<uint64_t>(nthr) * ks - 1) / (static_cast<uint64_t>(nthr) * ks);
     // one resident workgroup per CU (the LDS table takes most of the CU's
     // 160 KiB): a grid of exactly one workgroup per CU, grid-stride
     bool all_lds = true;
-    for (const K1Group& g : m.k1g) all_lds &= g.in_lds;
-    uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, all_lds ? sms : sms * 2ull)));
+    for (const K1Group& g : dt.k1g) all_lds &= g.in_lds;
+    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, all_lds ? sms : sms * 2ull)));
     st->k1_blocks = blocks;
     st->k1_threads = nthr;
     st->table_in_lds = all_lds;
     // one hit region per (group, workgroup); K2 walks all of them
     const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
-    uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(m.hit_cap / nregions, 0xffffffffu));
-    HIP_OK(hipMemsetAsync(m.d_bh, 0, nregions * sizeof(uint32_t), m.stream));
+    const uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(ln.hit_cap / nregions, 0xffffffffu));
+    HIP_OK(hipMemsetAsync(ln.d_bh, 0, nregions * sizeof(uint32_t), s));
     auto k1_lds = [&](const K1Group& g) {
       return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
              (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
     };
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
-      const K1Group& g = m.k1g[gi];
+      const K1Group& g = dt.k1g[gi];
       const void* kfn = k1_kernel(g.in_lds, nthr, ks);
       if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
       HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(k1_lds(g))));
     }
-    HIP_OK(hipEventRecord(m.ev[0], m.stream));
+    HIP_OK(hipEventRecord(ln.ev[0], s));
+    uint32_t launches = 0;
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
-      const K1Group& g = m.k1g[gi];
+      const K1Group& g = dt.k1g[gi];
       const size_t lds = k1_lds(g);
       const void* kfn = k1_kernel(g.in_lds, nthr, ks);
       unsigned long long a_total = total;
@@ -862,82 +1003,85 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
       uint32_t a_warm = g.warm_lines;
       unsigned long long a_nchunks = nchunks;
       uint32_t a_chunk = kChunk;
-      uint32_t a_kww = m.kw_words, a_kwbase = g.kw_base, a_primary = gi == 0;
+      uint32_t a_kww = dt.kw_words, a_kwbase = g.kw_base, a_primary = gi == 0;
       const uint8_t* a_data = d_data;
-      unsigned long long* a_hits = m.d_hits + static_cast<size_t>(gi) * blocks * region_cap;
-      uint32_t* a_bh = m.d_bh + static_cast<size_t>(gi) * blocks;
+      unsigned long long* a_hits = ln.d_hits + static_cast<size_t>(gi) * blocks * region_cap;
+      uint32_t* a_bh = ln.d_bh + static_cast<size_t>(gi) * blocks;
       uint16_t* a_next = g.next;
       uint8_t* a_cls = g.cls;
       OutMeta* a_meta = g.meta;
       uint32_t* a_list = g.list;
-      uint32_t* a_ocnt = m.d_cnt + 2;
-      uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(m.over_cap, 0xffffffffu));
-      void* args[] = {&a_data, &a_total, &m.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
+      uint32_t* a_ocnt = ln.d_cnt + 2;
+      uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
+      uint32_t a_rcap = region_cap;
+      void* args[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
-                      &m.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &region_cap,
-                      &m.d_over, &a_ocnt, &a_ocap, &m.d_nl, &m.d_ff};
-      HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, m.stream));
+                      &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
+                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff};
+      HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, s));
+      ++launches;
     }
-    HIP_OK(hipEventRecord(m.ev[1], m.stream));
-    m.h_bh.resize(nregions + 1);
-    HIP_OK(hipMemcpyAsync(m.h_bh.data(), m.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
-    HIP_OK(hipMemcpyAsync(m.h_bh.data() + nregions, m.d_cnt + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
-    HIP_OK(hipStreamSynchronize(m.stream));
+    HIP_OK(hipEventRecord(ln.ev[1], s));
+    ln.h_bh.resize(nregions + 1);
+    HIP_OK(hipMemcpyAsync(ln.h_bh.data(), ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(ln.h_bh.data() + nregions, ln.d_cnt + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
     float k1 = 0;
-    HIP_OK(hipEventElapsedTime(&k1, m.ev[0], m.ev[1]));
+    HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
     st->k1_ms += k1;
+    st->k1_launches += launches;
     uint64_t nhits = 0;
     uint32_t maxr = 0;
-    for (uint32_t r = 0; r < nregions; ++r) { nhits += m.h_bh[r]; maxr = std::max(maxr, std::min(m.h_bh[r], region_cap)); }
-    const uint32_t nover = m.h_bh[nregions];
-    if (nover > m.over_cap) {
+    for (uint32_t r = 0; r < nregions; ++r) { nhits += ln.h_bh[r]; maxr = std::max(maxr, std::min(ln.h_bh[r], region_cap)); }
+    const uint32_t nover = ln.h_bh[nregions];
+    if (nover > ln.over_cap) {
       // the overflow pool (shared by every workgroup) was too small: grow it
       // to the exact need and run K1 again.  Growth follows the batch's total
       // hit count, not the fullest region times the region count.
-      m.over_cap = static_cast<size_t>(nover) * 5 / 4 + 1024;
-      if (!ensure(&m.d_over, &m.d_over_cap, m.over_cap, err)) return false;
+      ln.over_cap = static_cast<size_t>(nover) * 5 / 4 + 1024;
+      if (!ensure(&ln.d_over, &ln.d_over_cap, ln.over_cap, err)) return false;
       continue;
     }
-    st->hits = nhits;
+    st->hits += nhits;
     // K2 (re-run only if the candidate buffer overflows)
     for (int a2 = 0; a2 < 3; ++a2) {
-      if (!ensure(&m.d_cands, &m.d_cands_cap, m.cand_cap, err)) return false;
-      HIP_OK(hipMemsetAsync(m.d_cnt + 1, 0, 4, m.stream));
-      HIP_OK(hipEventRecord(m.ev[2], m.stream));
+      if (!ensure(&ln.d_cands, &ln.d_cands_cap, ln.cand_cap, err)) return false;
+      HIP_OK(hipMemsetAsync(ln.d_cnt + 1, 0, 4, s));
+      HIP_OK(hipEventRecord(ln.ev[2], s));
       if (nhits > 0) {
         // (region, sub-block) grid: enough sub-blocks that the fullest region is done in ~4 strides
         const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(64, (maxr + 1023) / 1024)));
-        hipLaunchKernelGGL(tsg_k2_verify, dim3(nregions * nsub), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles,
-                           m.d_hits, m.d_bh, region_cap, nregions, m.anchors, m.rules, m.rule_kw, m.d_kw, m.kw_words, m.vdfa, m.v_next, m.v_acc,
-                           m.v_cls, m.d_cands, m.d_cnt, static_cast<uint32_t>(m.cand_cap));
+        hipLaunchKernelGGL(tsg_k2_verify, dim3(nregions * nsub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+                           ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words,
+                           dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, static_cast<uint32_t>(ln.cand_cap));
         HIP_OK(hipGetLastError());
         if (nover > 0) {                               // the overflow pool as one more region
           const uint32_t osub = static_cast<uint32_t>(std::min<uint64_t>(4096, (nover + 1023) / 1024));
-          hipLaunchKernelGGL(tsg_k2_verify, dim3(osub), dim3(256), 0, m.stream, d_data, m.d_off, in.nfiles,
-                             m.d_over, m.d_cnt + 2, static_cast<uint32_t>(m.over_cap), 1u, m.anchors, m.rules, m.rule_kw, m.d_kw,
-                             m.kw_words, m.vdfa, m.v_next, m.v_acc, m.v_cls, m.d_cands, m.d_cnt,
-                             static_cast<uint32_t>(m.cand_cap));
+          hipLaunchKernelGGL(tsg_k2_verify, dim3(osub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+                             ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
+                             dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
+                             ln.d_cnt, static_cast<uint32_t>(ln.cand_cap));
           HIP_OK(hipGetLastError());
         }
       }
-      HIP_OK(hipEventRecord(m.ev[3], m.stream));
+      HIP_OK(hipEventRecord(ln.ev[3], s));
       unsigned int c2 = 0;
-      HIP_OK(hipMemcpyAsync(&c2, m.d_cnt + 1, 4, hipMemcpyDeviceToHost, m.stream));
-      HIP_OK(hipStreamSynchronize(m.stream));
+      HIP_OK(hipMemcpyAsync(&c2, ln.d_cnt + 1, 4, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
       float k2 = 0;
-      HIP_OK(hipEventElapsedTime(&k2, m.ev[2], m.ev[3]));
+      HIP_OK(hipEventElapsedTime(&k2, ln.ev[2], ln.ev[3]));
       st->k2_ms += k2;
-      if (c2 > m.cand_cap) { m.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
+      if (c2 > ln.cand_cap) { ln.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
       auto t_d2h = std::chrono::steady_clock::now();
       out->cands.resize(c2);
-      if (c2) HIP_OK(hipMemcpyAsync(out->cands.data(), m.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, m.stream));
+      if (c2) HIP_OK(hipMemcpyAsync(out->cands.data(), ln.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, s));
       out->ff.resize(in.nfiles);
-      if (in.nfiles) HIP_OK(hipMemcpyAsync(out->ff.data(), m.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
+      if (in.nfiles) HIP_OK(hipMemcpyAsync(out->ff.data(), ln.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       out->nl.resize(nchunks);
-      if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), m.d_nl, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, m.stream));
-      HIP_OK(hipStreamSynchronize(m.stream));
+      if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), ln.d_nl, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
       st->d2h_ms += ms_since(t_d2h);
-      st->candidates = c2;
+      st->candidates += c2;
       return true;
     }
     *err = "candidate buffer overflow persisted";
@@ -947,33 +1091,24 @@ bool Engine::run_gpu(const BatchInput& in, ScanStats* st, GpuOut* out, std::stri
   return false;
 }
 
-bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
-                            std::vector<std::vector<std::vector<uint64_t>>>* cands, ScanStats* st,
-                            std::string* err) {
+bool Engine::prefilter_only(const BatchInput& in, std::vector<std::vector<std::vector<uint64_t>>>* cands,
+                            ScanStats* st, std::string* err) {
   ScanStats local;
   if (!st) st = &local;
-  Impl& m = *impl_;
-  if (!run_gpu(in, st, &m.out[0], err)) return false;
+  if (!in.d_data) { *err = "prefilter_only needs device-resident data"; return false; }
+  DeviceTables& dt = *dev_[0];
+  Lane* ln = acquire_lane(dt, err);
+  if (!ln) return false;
+  Segment sg;
+  sg.in = in;
+  GpuOut out;
+  const bool ok = run_segment(dt, *ln, sg, in.d_data, st, &out, err);
+  release_lane(dt, ln);
+  if (!ok) return false;
   const size_t nr = rs_->rules.size();   // real rules only (exclude pseudo-rules follow)
-  if (kw_gate) {
-    m.h_kw.resize(static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * m.kw_words);
-    HIP_OK(hipMemcpy(m.h_kw.data(), m.d_kw, m.h_kw.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    kw_gate->assign(static_cast<size_t>(in.nfiles) * nr, 0);
-    for (uint32_t f = 0; f < in.nfiles; ++f) {
-      for (size_t r = 0; r < nr; ++r) {
-        const RuleGpuInfo& gi = pf_.rules[r];
-        uint8_t g = gi.always_gate;
-        for (uint32_t k = 0; k < gi.kw_count && !g; ++k) {
-          uint32_t id = pf_.rule_kw[gi.kw_begin + k];
-          g = (m.h_kw[static_cast<size_t>(f) * m.kw_words + (id >> 5)] >> (id & 31)) & 1u;
-        }
-        (*kw_gate)[static_cast<size_t>(f) * nr + r] = g;
-      }
-    }
-  }
   if (cands) {
     cands->assign(in.nfiles, std::vector<std::vector<uint64_t>>(nr));
-    for (const CandDev& c : m.out[0].cands)
+    for (const CandDev& c : out.cands)
       if (c.rule < nr) (*cands)[c.file][c.rule].push_back(c.start);
     for (auto& f : *cands)
       for (auto& v : f) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); }
@@ -981,11 +1116,31 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<uint8_t>* kw_gate,
   return true;
 }
 
-// Host confirmation of one piece (files [0, in.nfiles) of `in`, results into
-// results[0..nfiles)) from that piece's GPU output `g`.
-void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* results, uint64_t* nconf_out,
-                           uint64_t* nfind_out, bool gpu_in_flight) {
-  Impl& m = *impl_;
+bool Engine::feed_probe(const uint8_t* h_data, uint64_t bytes, double* ms, std::string* err) {
+  DeviceTables& dt = *dev_[0];
+  Lane* ln = acquire_lane(dt, err);
+  if (!ln) return false;
+  bool ok = hipSetDevice(dt.device) == hipSuccess;
+  const uint64_t seg = std::min<uint64_t>(segment_, std::max<uint64_t>(bytes, 1));
+  for (int i = 0; i < 2 && ok; ++i) ok = ensure(&ln->ring[i], &ln->ring_cap[i], seg + 64, err);
+  auto t0 = std::chrono::steady_clock::now();
+  int slot = 0;
+  for (uint64_t o = 0; ok && o < bytes; o += seg, slot ^= 1) {
+    const uint64_t n = std::min(seg, bytes - o);
+    ok = hipMemcpyAsync(ln->ring[slot], h_data + o, n, hipMemcpyHostToDevice, ln->copy) == hipSuccess;
+  }
+  ok = ok && hipStreamSynchronize(ln->copy) == hipSuccess;
+  *ms = ms_since(t0);
+  release_lane(dt, ln);
+  if (!ok && err->empty()) *err = "feed probe copy failed";
+  return ok;
+}
+
+// Host confirmation of one segment (files [0, in.nfiles) of sg.in, results
+// into results[0..nfiles)) from that segment's GPU output `g`.
+void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Secret* results, uint64_t* nconf_out,
+                             uint64_t* nfind_out, bool gpu_in_flight) {
+  const BatchInput& in = sg.in;
   const Ruleset& rs = *rs_;
   const size_t nr = rs.rules.size();
   const size_t nplan = pf_.rules.size();   // rules + exclude-block pseudo-rules
@@ -1094,12 +1249,11 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
       results[f] = std::move(s);
     }
   };
-  int nt = threads_ > 0 ? threads_ : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
-  if (!m.pool || m.pool->size() != nt) m.pool.reset(new ThreadPool(nt));
-  // while the next piece's GPU passes are in flight one core stays with the
-  // thread driving them (a preempted driver thread stalls the GPU)
+  const int nt = cc.pool->size();
+  // while GPU passes are in flight one core stays with each thread driving
+  // them (a preempted driver thread stalls its GPU)
   const int active = gpu_in_flight && nt > 1 ? nt - 1 : nt;
-  m.pool->run([&](int idx) {
+  cc.pool->run([&](int idx) {
     if (idx >= active) return;
     worker();
     light_files();
@@ -1108,108 +1262,213 @@ void Engine::confirm_piece(const BatchInput& in, const GpuOut& g, Secret* result
   *nfind_out += nfind.load();
 }
 
-// A batch is cut into pieces at file boundaries (about equal bytes each).  The
-// GPU passes of piece i+1 run on a driver thread while the host pool confirms
-// piece i: the step costs ~max(GPU, host) + one piece of the other, instead of
-// their sum.  Each piece is a self-contained batch (offsets rebased to 0, its
-// device data a 16-byte aligned sub-range of the batch), so the kernels are
-// unchanged and the result equals the one-piece scan.
+// One batch through the pipeline:
+//  * uploaded data (h_data only): the batch is cut into segments of about
+//    segment_ bytes at file boundaries; each device's driver thread takes
+//    segments from a shared queue, uploads the next one on its copy stream
+//    while K1/K2 of the current one run on its compute stream (two-slot
+//    upload ring), and hands each finished segment to this thread, which
+//    confirms it on the host while the drivers go on;
+//  * resident data (d_data on one of the engine's devices): pieces (TSG_PIECES,
+//    the first taking first_piece_ of the bytes), GPU passes of piece i+1 on
+//    the driver while this thread confirms piece i.
+// Every segment is a self-contained batch (offsets rebased to 0, data a
+// 16-byte aligned sub-range), so the kernels are unchanged and the result is
+// the one-segment result.
 bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* st, std::string* err) {
-  constexpr uint32_t kManyFiles = 1u << 16;
   ScanStats local;
   if (!st) st = &local;
-  auto t0 = std::chrono::steady_clock::now();
-  Impl& m = *impl_;
-  const uint64_t total = in.nfiles ? in.offsets[in.nfiles] - in.offsets[0] : 0;
-  if (in.offsets && in.offsets[0] != 0) { *err = "offsets[0] must be 0"; return false; }
-  uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(m.pieces, std::max<uint64_t>(1, total / m.min_piece)));
-  // piece boundaries: file indices, each piece start 16-byte aligned within the batch
-  std::vector<uint32_t> cut{0};
-  for (uint32_t p = 1; p < want; ++p) {
-    // piece 0 takes first_piece of the bytes, the others share the rest
-    const double share = p == 0 ? 0.0 : m.first_piece + (1.0 - m.first_piece) * (p - 1) / (want - 1);
-    const uint64_t target = static_cast<uint64_t>(share * static_cast<double>(total));
-    uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
-    while (in.d_data && f < in.nfiles && (in.offsets[f] & 15) != 0) ++f;   // resident data: aligned piece starts
-    if (f > cut.back() && f < in.nfiles) cut.push_back(f);
-  }
-  cut.push_back(in.nfiles);
-  const size_t np = cut.size() - 1;
-  std::vector<BatchInput> piece(np);
-  std::vector<std::vector<uint64_t>> poff(np);
-  std::vector<ScanStats> pst(np);
-  for (size_t p = 0; p < np; ++p) {
-    const uint32_t a = cut[p], b = cut[p + 1];
-    BatchInput& q = piece[p];
-    q = in;
-    const uint64_t base = in.offsets[a];
-    if (np > 1) {
-      poff[p].resize(b - a + 1);
-      for (uint32_t f = a; f <= b; ++f) poff[p][f - a] = in.offsets[f] - base;
-      q.offsets = poff[p].data();
-    }
-    q.nfiles = b - a;
-    q.h_data = in.h_data ? in.h_data + base : nullptr;
-    q.d_data = in.d_data ? static_cast<const uint8_t*>(in.d_data) + base : nullptr;
-    q.paths = in.paths ? in.paths + a : nullptr;
-    q.path_lens = in.path_lens ? in.path_lens + a : nullptr;
-    q.binary = in.binary ? in.binary + a : nullptr;
-  }
-  uint64_t nconf = 0, nfind = 0;
-  double gpu_ms = 0, host_ms = 0;
-  if (in.nfiles >= kManyFiles) {
-    // piece 0's GPU passes on a driver thread while this thread sets up the
-    // per-file result slots (hundreds of thousands for image layers; with few
-    // files the extra thread hand-off measured slower, so they run in line)
-    bool ok0 = true;
-    std::thread gpu0([&]() {
-      auto tg = std::chrono::steady_clock::now();
-      ok0 = run_gpu(piece[0], &pst[0], &m.out[0], err);
-      gpu_ms += ms_since(tg);
-    });
-    results->clear();
-    results->resize(in.nfiles);
-    gpu0.join();
-    if (!ok0) return false;
-  } else {
-    results->assign(in.nfiles, Secret());
-    auto tg = std::chrono::steady_clock::now();
-    if (!run_gpu(piece[0], &pst[0], &m.out[0], err)) return false;
-    gpu_ms += ms_since(tg);
-  }
-  for (size_t p = 0; p < np; ++p) {
-    std::thread gpu;
-    bool ok_next = true;
-    std::string err_next;
-    double next_ms = 0;
-    if (p + 1 < np) {
-      gpu = std::thread([&, p]() {
-        auto t = std::chrono::steady_clock::now();
-        ok_next = run_gpu(piece[p + 1], &pst[p + 1], &m.out[(p + 1) & 1], &err_next);
-        next_ms = ms_since(t);
-      });
-    }
-    auto th = std::chrono::steady_clock::now();
-    confirm_piece(piece[p], m.out[p & 1], results->data() + cut[p], &nconf, &nfind, gpu.joinable());
-    host_ms += ms_since(th);
-    if (gpu.joinable()) gpu.join();
-    gpu_ms += next_ms;
-    if (!ok_next) { *err = err_next; return false; }
-  }
   *st = ScanStats();
-  for (const ScanStats& s : pst) {
-    st->k1_ms += s.k1_ms; st->k2_ms += s.k2_ms; st->h2d_ms += s.h2d_ms; st->d2h_ms += s.d2h_ms;
-    st->hits += s.hits; st->candidates += s.candidates;
-    st->k1_blocks = s.k1_blocks; st->k1_threads = s.k1_threads; st->chunk_bytes = s.chunk_bytes;
-    st->table_in_lds = s.table_in_lds;
+  auto t0 = std::chrono::steady_clock::now();
+  if (in.nfiles && !in.offsets) { *err = "offsets is NULL"; return false; }
+  if (in.offsets && in.offsets[0] != 0) { *err = "offsets[0] must be 0"; return false; }
+  for (uint32_t i = 0; i < in.nfiles; ++i) {
+    if (in.offsets[i + 1] < in.offsets[i]) { *err = "offsets must be non-decreasing"; return false; }
   }
+  const uint64_t total = in.nfiles ? in.offsets[in.nfiles] : 0;
   st->bytes = total;
   st->files = in.nfiles;
-  st->pieces = static_cast<uint32_t>(np);
-  st->gpu_wall_ms = gpu_ms;
+  if (in.nfiles == 0 || total == 0) {
+    // nothing for the GPU: every file is empty, so only the global
+    // allow-path outcome (scanner.go:381-386) can make a Secret non-empty
+    results->assign(in.nfiles, Secret());
+    for (uint32_t f = 0; f < in.nfiles; ++f)
+      (*results)[f] = scan_file(*rs_, in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]),
+                                in.h_data, 0, in.binary ? in.binary[f] != 0 : false, nullptr);
+    st->pieces = 0;
+    st->total_ms = ms_since(t0);
+    return true;
+  }
+  // --- segments
+  std::vector<Segment> segs;
+  std::vector<DeviceTables*> drivers;
+  const bool resident = in.d_data != nullptr;
+  {
+    std::vector<uint32_t> cut{0};
+    if (resident) {
+      const int dev = device_of(in.d_data);
+      for (auto& d : dev_) if (d->device == dev) { drivers.push_back(d.get()); break; }
+      if (drivers.empty()) { *err = "d_data is not device memory of one of the engine's devices"; return false; }
+      const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(pieces_, std::max<uint64_t>(1, total / min_piece_)));
+      for (uint32_t p = 1; p < want; ++p) {
+        // piece 0 takes first_piece_ of the bytes, the others share the rest
+        const double share = first_piece_ + (1.0 - first_piece_) * (p - 1) / (want - 1);
+        const uint64_t target = static_cast<uint64_t>(share * static_cast<double>(total));
+        uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
+        while (f < in.nfiles && (in.offsets[f] & 15) != 0) ++f;   // resident data: aligned piece starts
+        if (f > cut.back() && f < in.nfiles) cut.push_back(f);
+      }
+    } else {
+      for (uint32_t f = 0; f < in.nfiles;) {
+        // next cut: the first file boundary at or past segment_ bytes from here
+        const uint64_t target = in.offsets[f] + segment_;
+        uint32_t g = static_cast<uint32_t>(std::lower_bound(in.offsets + f, in.offsets + in.nfiles, target) - in.offsets);
+        if (g <= f) g = f + 1;
+        if (g >= in.nfiles) break;
+        cut.push_back(g);
+        f = g;
+      }
+      const size_t nseg = cut.size();
+      for (auto& d : dev_) {
+        if (drivers.size() >= nseg) break;
+        drivers.push_back(d.get());
+      }
+    }
+    cut.push_back(in.nfiles);
+    segs.resize(cut.size() - 1);
+    for (size_t p = 0; p < segs.size(); ++p) {
+      const uint32_t a = cut[p], b = cut[p + 1];
+      Segment& sg = segs[p];
+      BatchInput& q = sg.in;
+      q = in;
+      sg.f0 = a;
+      sg.b0 = in.offsets[a];
+      sg.bytes = in.offsets[b] - in.offsets[a];
+      if (segs.size() > 1) {
+        sg.off.resize(b - a + 1);
+        for (uint32_t f = a; f <= b; ++f) sg.off[f - a] = in.offsets[f] - sg.b0;
+        q.offsets = sg.off.data();
+      }
+      q.nfiles = b - a;
+      q.h_data = in.h_data ? in.h_data + sg.b0 : nullptr;
+      q.d_data = resident ? static_cast<const uint8_t*>(in.d_data) + sg.b0 : nullptr;
+      q.paths = in.paths ? in.paths + a : nullptr;
+      q.path_lens = in.path_lens ? in.path_lens + a : nullptr;
+      q.binary = in.binary ? in.binary + a : nullptr;
+    }
+  }
+  uint64_t max_seg = 0;
+  for (const Segment& sg : segs) max_seg = std::max(max_seg, sg.bytes);
+
+  struct Job {
+    size_t seg = 0;
+    GpuOut out;
+  };
+  JobQueue<Job> q(static_cast<int>(drivers.size()), 2 * drivers.size() + 2);
+  std::atomic<size_t> next_seg{0};
+  std::mutex st_mu;
+  std::string drv_err;
+  double gpu_busy = 0;
+  auto t_feed0 = std::chrono::steady_clock::now();
+  std::atomic<int64_t> feed_end_ns{0};
+  auto driver = [&](DeviceTables* dt) {
+    std::string e;
+    ScanStats dst;
+    auto tb = std::chrono::steady_clock::now();
+    Lane* ln = acquire_lane(*dt, &e);
+    bool ok = ln != nullptr;
+    if (ok && hipSetDevice(dt->device) != hipSuccess) { ok = false; e = "hipSetDevice failed"; }
+    if (ok && !resident) {
+      for (int i = 0; i < 2 && ok; ++i) ok = ensure(&ln->ring[i], &ln->ring_cap[i], max_seg + 64, &e);
+    }
+    // upload of segment `si` into ring slot `slot` (copy stream)
+    auto upload = [&](size_t si, int slot) -> bool {
+      const Segment& sg = segs[si];
+      std::string* err = &e;
+      HIP_OK(hipEventRecord(ln->up_begin[slot], ln->copy));
+      HIP_OK(hipMemcpyAsync(ln->ring[slot], sg.in.h_data, sg.bytes, hipMemcpyHostToDevice, ln->copy));
+      HIP_OK(hipMemsetAsync(ln->ring[slot] + sg.bytes, 0, 64, ln->copy));   // K1 reads 16-B words past the end
+      HIP_OK(hipEventRecord(ln->up_done[slot], ln->copy));
+      return true;
+    };
+    size_t cur = ok ? next_seg.fetch_add(1) : segs.size();
+    int slot = 0;
+    if (ok && cur < segs.size() && !resident) ok = upload(cur, slot);
+    while (ok && cur < segs.size() && !q.aborted()) {
+      const size_t nxt = next_seg.fetch_add(1);
+      // the next segment's upload goes behind this one's on the copy stream;
+      // its ring slot was last read by the segment before this one, whose
+      // kernels have completed (run_segment returns after its D2H)
+      if (nxt < segs.size() && !resident && !(ok = upload(nxt, slot ^ 1))) break;
+      const void* d_data = resident ? segs[cur].in.d_data : ln->ring[slot];
+      if (!resident) {
+        std::string* err = &e;
+        auto wait_up = [&]() -> bool {
+          HIP_OK(hipStreamWaitEvent(ln->compute, ln->up_done[slot], 0));
+          return true;
+        };
+        if (!(ok = wait_up())) break;
+      }
+      std::unique_ptr<Job> job(new Job());
+      job->seg = cur;
+      ScanStats sst;
+      ok = run_segment(*dt, *ln, segs[cur], d_data, &sst, &job->out, &e);
+      if (!ok) break;
+      if (!resident) {
+        float h2d = 0;
+        if (hipEventElapsedTime(&h2d, ln->up_begin[slot], ln->up_done[slot]) == hipSuccess) sst.h2d_ms += h2d;
+        const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_feed0).count();
+        int64_t prev = feed_end_ns.load();
+        while (ns > prev && !feed_end_ns.compare_exchange_weak(prev, ns)) {}
+      }
+      add_stats(&dst, sst);
+      q.push(std::move(job));
+      cur = nxt;
+      slot ^= 1;
+    }
+    if (ln) {
+      if (!ok) { hipStreamSynchronize(ln->copy); hipStreamSynchronize(ln->compute); }
+      release_lane(*dt, ln);
+    }
+    {
+      std::lock_guard<std::mutex> lk(st_mu);
+      add_stats(st, dst);
+      gpu_busy += ms_since(tb);
+      if (!ok && drv_err.empty()) drv_err = e.empty() ? "device driver failed" : e;
+    }
+    if (!ok) q.abort();
+    q.producer_done();
+  };
+  CallCtx* cc = acquire_call();
+  std::vector<std::thread> threads;
+  for (DeviceTables* dt : drivers) threads.emplace_back(driver, dt);
+  // per-file result slots (hundreds of thousands for image layers) are set up
+  // while the first segment's upload and GPU passes run
+  results->clear();
+  results->resize(in.nfiles);
+  uint64_t nconf = 0, nfind = 0;
+  double host_ms = 0;
+  for (;;) {
+    int left = 0;
+    std::unique_ptr<Job> job = q.pop(&left);
+    if (!job) break;
+    auto th = std::chrono::steady_clock::now();
+    const Segment& sg = segs[job->seg];
+    confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0);
+    host_ms += ms_since(th);
+  }
+  for (auto& t : threads) t.join();
+  release_call(cc);
+  if (!drv_err.empty()) { *err = drv_err; return false; }
+  st->bytes = total;
+  st->files = in.nfiles;
+  st->pieces = static_cast<uint32_t>(segs.size());
+  st->devices = static_cast<uint32_t>(drivers.size());
+  st->gpu_wall_ms = gpu_busy;
   st->host_ms = host_ms;
   st->confirm_files = nconf;
   st->findings = nfind;
+  st->feed_ms = resident ? 0.0 : feed_end_ns.load() / 1e6;
   st->total_ms = ms_since(t0);
   return true;
 }

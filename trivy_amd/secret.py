@@ -131,7 +131,8 @@ class Scanner:
         if self._engine is None:
             L = _lib.lib()
             e = ctypes.c_void_p()
-            _lib.check(L.tsg_engine_create(self._rs, self._device, ctypes.byref(e)))
+            mask = 0 if self._device == "all" else (1 << int(self._device))
+            _lib.check(L.tsg_engine_create(self._rs, mask, ctypes.byref(e)))
             if self._threads:
                 L.tsg_engine_set_threads(e, self._threads)
             self._engine = e
