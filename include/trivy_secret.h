@@ -9,6 +9,8 @@
  *                           pkg/fanal/secret/scanner.go:277-307, 320-364
  *   tsg_ruleset_allow_path  (Global).AllowPath        scanner.go:56-59
  *   tsg_builtin_rules_json  secret.GetBuiltinRules     builtin-rules.go:87-89
+ *   tsg_secret_rules_metadata_json
+ *                           secret.GetSecretRulesMetadata builtin-rules.go:91-99
  *   tsg_engine_create       (no reference analogue: binds the compiled
  *                           rules to one GPU; the reference's regexes are
  *                           compiled inside ParseConfig/NewScanner)
@@ -108,8 +110,16 @@ const char* tsg_ruleset_rule_id(const tsg_ruleset* rs, int i);
 int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t path_len);
 /* Compile report of the GPU prefilter (NUL-terminated, owned by the engine). */
 const char* tsg_engine_report(const tsg_engine* e);
-/* Builtin rule data as JSON (NUL-terminated, static). */
+/* Builtin rule data as JSON (NUL-terminated, static).  GetBuiltinRules,
+ * pkg/fanal/secret/builtin-rules.go:87-89. */
 const char* tsg_builtin_rules_json(void);
+/* GetSecretRulesMetadata (builtin-rules.go:91-99): json.Marshal of the
+ * []iacRules.Check{Name: rule ID, Description: rule title} for the builtin
+ * rules (NUL-terminated, static). */
+const char* tsg_secret_rules_metadata_json(void);
+/* Test hook: Go encoding/json string encoding of s (json.Marshal; with
+ * escape_html = 0 as an Encoder with SetEscapeHTML(false)).  Free with tsg_free. */
+int tsg_go_json_string(const uint8_t* s, size_t n, int escape_html, char** out, size_t* len);
 
 int tsg_device_count(void);
 /* device_mask: bit d selects HIP device d (0 = every visible device).  With

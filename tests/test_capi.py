@@ -78,3 +78,12 @@ def test_parse_config_document_rules(tmp_path):
             want = [r.id for r in so.Scanner(so.parse_config(str(p))).rules]
             assert ids == want
     assert "aws-access-key-id" not in S.Scanner(S.ParseConfig(str(tmp_path / "two.yaml"))).rule_ids
+
+
+def test_get_secret_rules_metadata():
+    # builtin-rules.go:91-99: one iacRules.Check{Name: ID, Description: Title} per builtin rule, in order
+    from trivy_amd import secret as S
+    md = S.GetSecretRulesMetadata()
+    rules = S.GetBuiltinRules()
+    assert md == [{"name": r["id"], "description": r["title"]} for r in rules]
+    assert len(md) == 87

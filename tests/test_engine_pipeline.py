@@ -82,7 +82,8 @@ def test_pinned_segments_equal_one_segment(monkeypatch):
     L = _lib.lib()
     paths, lens, _keep = _lib.pack_paths(c.paths)
     res = ctypes.c_void_p()
-    _lib.check(L.tsg_scan_batch_resident(S.Scanner(None).engine(), ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
+    sc = S.Scanner(None)                                    # keeps the engine alive across the call
+    _lib.check(L.tsg_scan_batch_resident(sc.engine(), ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
                                          c.offsets.ctypes.data, len(c.paths), paths, lens, None, ctypes.byref(res)))
     try:
         res_json = _lib.result_json(res)

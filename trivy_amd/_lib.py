@@ -36,6 +36,9 @@ SIGNATURES = [
     ("tsg_ruleset_allow_path", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("tsg_engine_report", ctypes.c_char_p, [ctypes.c_void_p]),
     ("tsg_builtin_rules_json", ctypes.c_char_p, []),
+    ("tsg_secret_rules_metadata_json", ctypes.c_char_p, []),
+    ("tsg_go_json_string", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
     ("tsg_device_count", ctypes.c_int, []),
     ("tsg_engine_create", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_engine_destroy", None, [ctypes.c_void_p]),
@@ -140,3 +143,15 @@ def pack_paths(paths):
     arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
     lens = (ctypes.c_uint32 * max(len(enc), 1))(*[len(e) for e in enc])
     return arr, lens, enc
+
+
+def go_json_string(b, escape_html=True):
+    """Go encoding/json encoding of the byte string b (test hook)."""
+    L = lib()
+    buf = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    check(L.tsg_go_json_string(b, len(b), 1 if escape_html else 0, ctypes.byref(buf), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(buf, n.value)
+    finally:
+        L.tsg_free(buf)

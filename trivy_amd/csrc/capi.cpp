@@ -408,6 +408,43 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
 
 const char* tsg_builtin_rules_json(void) { return tsg_builtin_json_ptr(); }
 
+// GetSecretRulesMetadata (builtin-rules.go:91-99): lo.Map(builtinRules, ...
+// iacRules.Check{Name: rule.ID, Description: rule.Title}) as json.Marshal
+// writes []iacRules.Check (pkg/iac/rules/providers.go:18-21 json tags).
+const char* tsg_secret_rules_metadata_json(void) {
+  static const std::string out = [] {
+    JValue doc;
+    std::string err;
+    if (!json_parse(tsg_builtin_json_ptr(), &doc, &err) || !doc.get("rules")) return std::string("null");
+    std::string o = "[";
+    bool first = true;
+    for (const auto& r : doc.get("rules")->arr) {
+      if (!first) o += ",";
+      first = false;
+      o += "{\"name\":";
+      go_json_string(&o, r.get("id") ? r.get("id")->as_string() : std::string());
+      o += ",\"description\":";
+      go_json_string(&o, r.get("title") ? r.get("title")->as_string() : std::string());
+      o += "}";
+    }
+    return o + "]";
+  }();
+  return out.c_str();
+}
+
+int tsg_go_json_string(const uint8_t* s, size_t n, int escape_html, char** out, size_t* len) {
+  if ((n && !s) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string o;
+  go_json_string(&o, reinterpret_cast<const char*>(s), n, escape_html != 0);
+  char* buf = static_cast<char*>(malloc(o.size() + 1));
+  if (!buf) return fail(TSG_ERR_INTERNAL, "out of memory");
+  memcpy(buf, o.data(), o.size());
+  buf[o.size()] = 0;
+  *out = buf;
+  if (len) *len = o.size();
+  return TSG_OK;
+}
+
 int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, int* gated, int* plain,
                           int* has_gate) {
   if (!pattern || (len && !text) || !gated || !plain || !has_gate) return fail(TSG_ERR_INVALID, "NULL argument");

@@ -134,4 +134,67 @@ bool json_parse(const std::string& text, JValue* out, std::string* err) {
   return true;
 }
 
+void go_json_string(std::string* out, const char* src, size_t n, bool escape_html) {
+  static const char hex[] = "0123456789abcdef";
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(src);
+  out->push_back('"');
+  size_t start = 0, i = 0;
+  while (i < n) {
+    const uint8_t b = p[i];
+    if (b < 0x80) {
+      const bool html = b == '<' || b == '>' || b == '&';
+      if (b >= 0x20 && b != '"' && b != '\\' && !(escape_html && html)) { ++i; continue; }
+      out->append(src + start, i - start);
+      switch (b) {
+        case '\\': case '"': out->push_back('\\'); out->push_back(static_cast<char>(b)); break;
+        case '\b': *out += "\\b"; break;
+        case '\f': *out += "\\f"; break;
+        case '\n': *out += "\\n"; break;
+        case '\r': *out += "\\r"; break;
+        case '\t': *out += "\\t"; break;
+        default:
+          *out += "\\u00";
+          out->push_back(hex[b >> 4]);
+          out->push_back(hex[b & 0xF]);
+      }
+      start = ++i;
+      continue;
+    }
+    // utf8.DecodeRune
+    uint32_t r = 0xFFFD;
+    size_t w = 1;
+    auto cont = [&](size_t k) { return i + k < n && (p[i + k] & 0xC0) == 0x80; };
+    if (b >= 0xC2 && b <= 0xDF && cont(1)) {
+      r = ((b & 0x1Fu) << 6) | (p[i + 1] & 0x3Fu); w = 2;
+    } else if (b >= 0xE0 && b <= 0xEF && i + 2 < n) {
+      const uint8_t lo = b == 0xE0 ? 0xA0 : 0x80, hi = b == 0xED ? 0x9F : 0xBF;
+      if (p[i + 1] >= lo && p[i + 1] <= hi && cont(2)) {
+        r = ((b & 0x0Fu) << 12) | ((p[i + 1] & 0x3Fu) << 6) | (p[i + 2] & 0x3Fu); w = 3;
+      }
+    } else if (b >= 0xF0 && b <= 0xF4 && i + 3 < n) {
+      const uint8_t lo = b == 0xF0 ? 0x90 : 0x80, hi = b == 0xF4 ? 0x8F : 0xBF;
+      if (p[i + 1] >= lo && p[i + 1] <= hi && cont(2) && cont(3)) {
+        r = ((b & 0x07u) << 18) | ((p[i + 1] & 0x3Fu) << 12) | ((p[i + 2] & 0x3Fu) << 6) | (p[i + 3] & 0x3Fu); w = 4;
+      }
+    }
+    if (r == 0xFFFD && w == 1) {
+      out->append(src + start, i - start);
+      *out += "\\ufffd";
+      start = ++i;
+      continue;
+    }
+    if (r == 0x2028 || r == 0x2029) {
+      out->append(src + start, i - start);
+      *out += "\\u202";
+      out->push_back(hex[r & 0xF]);
+      i += w;
+      start = i;
+      continue;
+    }
+    i += w;
+  }
+  out->append(src + start, n - start);
+  out->push_back('"');
+}
+
 }  // namespace tsg

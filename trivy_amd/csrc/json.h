@@ -41,4 +41,14 @@ struct JValue {
 // Returns false and sets *err on malformed input.
 bool json_parse(const std::string& text, JValue* out, std::string* err);
 
+// Go encoding/json string encoding (go1.23 encoding/json/encode.go
+// appendString): '"' and '\\' backslashed; \\b \\f \\n \\r \\t short escapes;
+// other bytes < 0x20 as \\u00XX; with escape_html (json.Marshal's default)
+// '<' '>' '&' as \\u003c \\u003e \\u0026; an invalid UTF-8 byte as \\ufffd;
+// U+2028 / U+2029 as \\u2028 / \\u2029; everything else raw.
+void go_json_string(std::string* out, const char* s, size_t n, bool escape_html = true);
+inline void go_json_string(std::string* out, const std::string& s, bool escape_html = true) {
+  go_json_string(out, s.data(), s.size(), escape_html);
+}
+
 }  // namespace tsg

@@ -9,6 +9,7 @@ include/trivy_secret.h:
   Scanner.Scan(ScanArgs)   -> types.Secret      scanner.go:377-463
   Scanner.ScanBatch([ScanArgs]) -> [types.Secret]   (batched entry)
   GetBuiltinRules()                             builtin-rules.go:87-89
+  GetSecretRulesMetadata()                      builtin-rules.go:91-99
 
 types.Secret is returned as a dict with the Go field names
 ({"FilePath", "Findings": [{"RuleID", ..., "Code": {"Lines": [...]}, "Match"}]});
@@ -81,6 +82,12 @@ def ParseConfig(config_path):
 
 def GetBuiltinRules():
     return json.loads(_lib.lib().tsg_builtin_rules_json().decode("utf-8"))["rules"]
+
+
+def GetSecretRulesMetadata():
+    """builtin-rules.go:91-99: [{"name": rule ID, "description": rule title}]
+    (iacRules.Check's json form) for the builtin rules."""
+    return json.loads(_lib.lib().tsg_secret_rules_metadata_json().decode("utf-8"))
 
 
 def _device_default():
