@@ -1,0 +1,71 @@
+#!/usr/bin/env python
+"""K1/K2 probe: one HBM-resident batch through the two GPU passes only
+(tsg_prefilter_resident: one K1 launch per scan-DFA group + K2), repeated.
+
+  python tools/k1_probe.py [--gb 4] [--reps 5] [--sizes loguniform] [--config 2|5]
+
+Prints per-launch K1 / K2 times and GB/s; used for K1 tuning and for
+rocprofv3 runs (a short program with few dispatches).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gb", type=float, default=4.0)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sizes", default="loguniform")
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0x71215EC7)
+    ap.add_argument("--json", action="store_true")
+    args = ap.parse_args()
+    import torch
+
+    from trivy_amd import _lib
+    from trivy_amd import secret as S
+    from workload import synth
+    c = synth.generate(int(args.gb * 1e9), seed=args.seed, sizes=args.sizes)
+    cfg = None
+    if args.config == 5:
+        cfg5, plants = synth.config5(500, seed=args.seed)
+        cfg = "/tmp/tsg_k1probe_c5.yaml"
+        synth.write_yaml(cfg5, cfg)
+        synth.plant_custom(c, plants, seed=args.seed, rate=1e-4)
+    d = torch.from_numpy(c.data).to("cuda:0")
+    torch.cuda.synchronize()
+    sc = S.Scanner(S.ParseConfig(cfg) if cfg else None)
+    eng = sc.engine()
+    L = _lib.lib()
+    rows = []
+    for r in range(args.reps + 1):
+        res = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        _lib.check(L.tsg_prefilter_resident(eng, ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
+                                            c.offsets.ctypes.data, len(c.paths), ctypes.byref(res)))
+        wall = (time.perf_counter() - t0) * 1e3
+        st = _lib.result_stats(res)
+        L.tsg_result_free(res)
+        if r == 0:
+            continue                              # warm-up (allocations)
+        rows.append((st["k1_ms"], st["k2_ms"], wall, st["hits"], st["candidates"], st["k1_launches"]))
+    k1 = float(np.median([x[0] for x in rows]))
+    k2 = float(np.median([x[1] for x in rows]))
+    out = {"bytes": c.nbytes, "files": len(c.paths), "k1_ms": round(k1, 4), "k2_ms": round(k2, 4),
+           "k1_gbps": round(c.nbytes / k1 / 1e6, 1), "k1_launches": rows[-1][5], "hits": rows[-1][3],
+           "candidates": rows[-1][4], "wall_ms": round(float(np.median([x[2] for x in rows])), 3),
+           "env": {k: v for k, v in os.environ.items() if k.startswith("TSG_")}}
+    print(json.dumps(out) if args.json else out, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -164,6 +164,40 @@ __device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Str
   return min(t.emit + x.chunk, x.total);
 }
 
+// The output list of an output state (anchor hits, keyword ids >= 128): out
+// of line, so the per-position output checks stay small.
+__device__ __noinline__ void k1_out_list(const K1Ctx& x, K1Stream& t, uint32_t begin, uint32_t count,
+                                         unsigned long long q) {
+  for (uint32_t j = 0; j < count; ++j) {
+    const uint32_t id = x.list[begin + j];
+    if (id < x.nkw) {
+      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
+    } else {
+      const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
+      if (li < kWaveHits) {
+        x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
+      } else {                                           // buffer full: straight to the region
+        const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
+        if (gi < x.region_cap) {
+          x.hits[gi] = (q << 24) | (id - x.nkw);
+        } else {                                         // region full: the shared overflow pool
+          const uint32_t oi = atomicAdd(x.over_cnt, 1u);
+          if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
+        }
+      }
+    }
+  }
+}
+
+// K1 v2's per-output work: keyword masks in registers, the list out of line.
+__device__ __forceinline__ void k1_out2(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
+  const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
+  const OutMeta m = x.meta[o];
+  t.kw0 |= m.kw0;
+  t.kw1 |= m.kw1;
+  if (m.list_count) k1_out_list(x, t, m.list_begin, m.list_count, q);
+}
+
 __device__ __forceinline__ void k1_out(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
   const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
   const OutMeta m = x.meta[o];
@@ -520,6 +554,174 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
   }
 }
 
+// K1 v2: the same pass with a leaner per-byte path.  The LDS layout puts the
+// class map and the scan table at compile-time offsets, so a transition is
+// one v_lshl_add + one ds_read_u16 with an immediate offset and a class
+// lookup one ds_read_u8 with an immediate offset; 64-byte lines are
+// double-buffered (the next line's loads are in flight while this one is
+// walked); per-position output handling keeps only the keyword-mask update
+// inline (k1_out2) and the special-rune check is out of line.
+__device__ __noinline__ void k1_special_call(const K1Ctx& x, const K1Stream& t, uint32_t w0, uint32_t w1, uint32_t w2,
+                                             uint32_t w3) {
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  k1_special(x, t, w, ~0ull, ~0ull);
+}
+
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v2(
+    const uint8_t* __restrict__ data, unsigned long long total,
+    const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
+    uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
+    const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
+    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
+    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
+    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
+    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
+    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | class map (256) |
+  //              scan table | output meta | output list]
+  constexpr uint32_t kWaves = kThreads / 64;
+  constexpr uint32_t kClsOff = kWaves * kWaveHits * 4 + kMaxWaves * 4 + 16;
+  constexpr uint32_t kTabOff = kClsOff + 256;
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
+  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count, [1] next item
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) { s_block[0] = 0; s_block[1] = 0; }
+  const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(g_next);
+    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff);
+    for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[kClsOff + i] = g_cls[i];
+    OutMeta* s_meta = reinterpret_cast<OutMeta*>(smem + kTabOff + padded);
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_meta + nmeta);
+    for (uint32_t i = threadIdx.x; i < nmeta; i += blockDim.x) s_meta[i] = g_meta[i];
+    for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
+  }
+  K1Ctx x;
+  x.data = data; x.total = total; x.chunk = chunk;
+  x.offsets = offsets; x.nfiles = nfiles;
+  x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
+  x.cls = smem + kClsOff;
+  x.first_out = first_out; x.nclasses = nclasses;
+  x.meta = reinterpret_cast<const OutMeta*>(smem + kTabOff + padded);
+  x.list = reinterpret_cast<const uint32_t*>(x.meta + nmeta);
+  x.nkw = nkw;
+  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
+  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
+  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
+  x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
+  __syncthreads();
+  const unsigned long long nitems = (nchunks + 63) / 64;       // wave work items (64 chunks)
+  const unsigned long long per_block = (nitems + gridDim.x - 1) / gridDim.x;
+  const unsigned long long first_item = per_block * blockIdx.x;
+  const unsigned long long last_item = min(first_item + per_block, nitems);
+  for (;;) {
+    unsigned long long item = 0;
+    if (lane == 0) {
+      item = first_item + atomicAdd(&s_block[1], 1u);
+      *x.w_hitcnt = 0;
+    }
+    item = __shfl(item, 0);
+    if (item >= last_item) break;                              // wave-uniform exit
+    __builtin_amdgcn_wave_barrier();
+    x.item_base = item * 64 * static_cast<unsigned long long>(chunk);
+    const unsigned long long c = item * 64 + lane;
+    if (c < nchunks) {
+      K1Stream t;
+      k1_init(x, t, min(c * chunk, total), warm_lines);
+      v4u nxt[4];
+      bool have_next = false;
+      for (;;) {
+        if (!(t.p < t.lim || t.p < k1_end(x, t))) break;
+        if (t.p + 64 <= t.lim) {
+          v4u cur[4];
+          if (have_next) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cur[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + t.p + 16 * i));
+          }
+          have_next = t.p + 128 <= t.lim;
+          if (have_next) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              nxt[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + t.p + 64 + 16 * i));
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t w0 = cur[i].x, w1 = cur[i].y, w2 = cur[i].z, w3 = cur[i].w;
+            const bool emit = t.p >= t.emit;
+            if (x.primary && ((w0 | w1 | w2 | w3) & 0x80808080u) && emit) k1_special_call(x, t, w0, w1, w2, w3);
+            const uint32_t w[4] = {w0, w1, w2, w3};
+            uint32_t cl[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) cl[k] = smem[kClsOff + ((w[k >> 2] >> ((k & 3) * 8)) & 0xffu)];
+            uint32_t st[16], mx = 0, s = t.s;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+              s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 1) + cl[k]);
+              st[k] = s;
+              mx = max(mx, s);
+            }
+            t.s = s;
+            if (emit) {
+              t.nl += nl_in_word(w0) + nl_in_word(w1) + nl_in_word(w2) + nl_in_word(w3);
+              if (mx >= first_out) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                  if (st[k] >= first_out) k1_out2(x, t, st[k], t.p + k);
+              }
+            }
+            t.p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
+            t.p += 16;
+          }
+        } else {
+          // a line with a file boundary or the chunk end (rare): word by word
+          have_next = false;
+          for (int i = 0; i < 4 && t.p < k1_end(x, t); ++i) {
+            const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            k1_word_slow(x, t, w);
+          }
+        }
+      }
+      flush_kw(x.kwmask, kw_words, t.f, t.kw0, t.kw1);
+      if (x.primary) nl_count[c] = t.nl;
+    }
+    // flush this wave's hit buffer (the wave has reconverged here)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t n = min(*x.w_hitcnt, kWaveHits);
+    uint32_t b0 = 0, o0 = 0;
+    if (lane == 0 && n) {
+      b0 = atomicAdd(x.b_hitcnt, n);
+      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
+    }
+    b0 = __shfl(b0, 0);
+    o0 = __shfl(o0, 0);
+    const uint32_t spill_from = max(b0, region_cap);
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t h = x.w_hits[i];
+      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
+      if (b0 + i < region_cap) {
+        x.hits[b0 + i] = v;
+      } else {
+        const uint32_t oi = o0 + (b0 + i - spill_from);
+        if (oi < x.over_cap) x.over[oi] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
+}
+
 // K1 instantiations: (workgroup size, interleaved streams per lane)
 template <bool kLds>
 const void* k1_kernel_t(uint32_t threads, int ks) {
@@ -528,7 +730,9 @@ const void* k1_kernel_t(uint32_t threads, int ks) {
   return nullptr;
 }
 
-const void* k1_kernel(bool lds, uint32_t threads, int ks) {
+// variant 2 (tsg_k1_scan_v2) needs the table in LDS, 1024 threads, one stream per lane
+const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1) {
+  if (variant == 2 && lds && threads == 1024 && ks == 1) return reinterpret_cast<const void*>(&tsg_k1_scan_v2<1024>);
   return lds ? k1_kernel_t<true>(threads, ks) : k1_kernel_t<false>(threads, ks);
 }
 
@@ -857,6 +1061,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
       e->k1_streams_ = static_cast<int>(k);
     }
   }
+  if (const char* c = std::getenv("TSG_K1_VARIANT")) {
+    const int v = std::atoi(c);
+    if (v == 1 || v == 2) e->k1_variant_ = v;
+  }
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
     // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
     // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
@@ -987,7 +1195,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     };
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
       const K1Group& g = dt.k1g[gi];
-      const void* kfn = k1_kernel(g.in_lds, nthr, ks);
+      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_variant_);
       if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
       HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(k1_lds(g))));
     }
@@ -996,7 +1204,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = dt.k1g[gi];
       const size_t lds = k1_lds(g);
-      const void* kfn = k1_kernel(g.in_lds, nthr, ks);
+      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_variant_);
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
       uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
