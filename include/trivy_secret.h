@@ -225,6 +225,52 @@ void tsg_prepared_free(tsg_prepared* p);
 int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, int* gated, int* plain,
                           int* has_gate);
 
+/* ---- report and image semantics ---- */
+typedef struct tsg_layer {          /* ftypes.Layer, pkg/fanal/types/artifact.go:75-79 */
+  const char* digest;
+  const char* diff_id;
+  const char* created_by;
+} tsg_layer;
+
+typedef struct tsg_report_opts {
+  int64_t schema_version;           /* report.SchemaVersion = 2 (pkg/report/writer.go:24); 0 omits it */
+  const char* created_at;           /* CreatedAt, RFC 3339; re-encoded as time.Time marshals */
+  const char* artifact_name;        /* ArtifactName; also the Target of image-config secrets */
+  const char* artifact_type;        /* artifact.Type: "filesystem", "repository", "container_image", ... */
+  const char* metadata_json;        /* types.Metadata as JSON (re-encoded in Go's field order); NULL = zero */
+  const char* severities;           /* comma-separated --severity list; NULL = all five */
+  int32_t layers_sorted;            /* 1: layers are cached blobs (AnalysisResult.Sort already applied) */
+} tsg_report_opts;
+
+/* `trivy -f json` output (pkg/report/json.go:22-50) for the secret results of
+ * one artifact.  layers[i] = tsg_scan_batch results of layer i, lowest layer
+ * first (an fs scan is one layer, layer_refs may be NULL); per layer
+ * AnalysisResult.Sort (analyzer.go:224-235), across layers ApplyLayers'
+ * mergeSecrets (applier/docker.go:134-146, 297-316); image_config = the scan
+ * of tsg_image_config_content's output (file "config.json"), or NULL, merged
+ * as local/scan.go:487-496 does; then secretsToResults (local/scan.go:236-254),
+ * the severity part of filterSecrets (result/filter.go:154-169) and
+ * json.MarshalIndent(report, "", "  ") + "\n".  Go iterates the merged
+ * secrets map in random order; this report lists them by FilePath.  Free
+ * *out with tsg_free. */
+int tsg_report_json(const tsg_result* const* layers, const tsg_layer* layer_refs, uint32_t nlayers,
+                    const tsg_result* image_config, const tsg_report_opts* opts, char** out, size_t* len);
+/* The image-config secret analyzer's input (imgconf/secret/secret.go:44):
+ * json.MarshalIndent(v1.ConfigFile, "  ", "") of the config decoded from
+ * config_json.  Scan it as ScanArgs{FilePath: "config.json"}.  Free with tsg_free. */
+int tsg_image_config_content(const char* config_json, size_t config_len, char** out, size_t* len);
+/* Base-layer secret skip (artifact/image/image.go:331-335, 526-554;
+ * image/image.go:111-137): is_base[i] = 1 when layer diff_ids[i] belongs to
+ * the base image, whose layers are analysed without the secret analyzer. */
+int tsg_guess_base_layers(const char* config_json, size_t config_len, const char* const* diff_ids, uint32_t n,
+                          uint8_t* is_base);
+/* Test hook: a result holding the JSON array of types.Secret given (Go field
+ * names), to check report assembly against the reference's types.Secret
+ * fixtures.  Never used by a scan. */
+int tsg_result_from_json(const char* json, size_t len, tsg_result** out);
+/* Test hook: time.Time JSON round trip (RFC 3339 in, MarshalJSON's form out). */
+int tsg_go_time_rfc3339(const char* in, char* out, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -182,6 +182,9 @@ def integration_cases():
                       "ref": "integration/testdata/secrets.json.golden"})
     copy_data(["deploy.sh", "trivy-secret.yaml"], os.path.join(base, "fixtures/repo/secrets"),
               os.path.join(HERE, "integration"))
+    # the golden report itself (the bytes `trivy -f json` wrote with -update,
+    # integration/integration_test.go:244-247), for the report writer's test
+    copy_data(["secrets.json.golden"], base, os.path.join(HERE, "integration"))
     return cases
 
 

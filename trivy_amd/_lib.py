@@ -90,6 +90,29 @@ SIGNATURES = [
                                         ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
 ]
 
+class TsgLayer(ctypes.Structure):
+    _fields_ = [("digest", ctypes.c_char_p), ("diff_id", ctypes.c_char_p), ("created_by", ctypes.c_char_p)]
+
+
+class TsgReportOpts(ctypes.Structure):
+    _fields_ = [("schema_version", ctypes.c_int64), ("created_at", ctypes.c_char_p),
+                ("artifact_name", ctypes.c_char_p), ("artifact_type", ctypes.c_char_p),
+                ("metadata_json", ctypes.c_char_p), ("severities", ctypes.c_char_p),
+                ("layers_sorted", ctypes.c_int32)]
+
+
+SIGNATURES += [
+    ("tsg_report_json", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.POINTER(TsgReportOpts), ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_size_t)]),
+    ("tsg_image_config_content", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_size_t)]),
+    ("tsg_guess_base_layers", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, c_char_pp, ctypes.c_uint32,
+                                              ctypes.c_void_p]),
+    ("tsg_go_time_rfc3339", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tsg_result_from_json", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+]
+
 _lib = None
 
 

@@ -2,15 +2,18 @@
 // host confirmer.
 #include "../../include/trivy_secret.h"
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 
 #include "engine.h"
 #include "feed.h"
 #include "prefilter.h"
+#include "report.h"
 #include "scanner.h"
 
 using namespace tsg;
@@ -37,6 +40,7 @@ struct tsg_prepared {
 
 struct tsg_result {
   std::shared_ptr<const Ruleset> rs;     // findings point at its rules
+  std::shared_ptr<std::deque<Rule>> own_rules;   // or at these (tsg_result_from_json)
   std::vector<Secret> files;
   ScanStats stats;
   std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
@@ -476,6 +480,148 @@ int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const 
     dfa_end[i] = rx->match_end(text, len, pos[i]);
     vm_end[i] = rx->match_at(text, len, pos[i], true, 0, caps.data()) ? caps[1] : -1;
   }
+  return TSG_OK;
+}
+
+static std::string cstr(const char* p) { return p ? std::string(p) : std::string(); }
+
+// Test hook: a result holding the types.Secret list given as JSON (Go field
+// names), so report assembly can be checked against the reference's own
+// types.Secret fixtures (e.g. applier/docker_test.go).
+int tsg_result_from_json(const char* json, size_t len, tsg_result** out) {
+  if (!json || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  JValue doc;
+  std::string err;
+  if (!json_parse(std::string(json, len), &doc, &err) || doc.kind != JValue::Arr) return fail(TSG_ERR_INVALID, "json: " + err);
+  auto* r = new tsg_result();
+  r->own_rules = std::make_shared<std::deque<Rule>>();
+  auto sget = [](const JValue* o, const char* k) { const JValue* v = o ? o->get(k) : nullptr; return v ? v->as_string() : std::string(); };
+  auto iget = [](const JValue* o, const char* k) { const JValue* v = o ? o->get(k) : nullptr; return v && v->kind == JValue::Num ? static_cast<int>(v->num) : 0; };
+  auto bget = [](const JValue* o, const char* k) { const JValue* v = o ? o->get(k) : nullptr; return v && v->kind == JValue::Bool && v->b; };
+  auto put = [](Secret* s, const std::string& v) {
+    StrRef ref{static_cast<uint32_t>(s->arena.size()), static_cast<uint32_t>(v.size())};
+    s->arena += v;
+    return ref;
+  };
+  for (const auto& js : doc.arr) {
+    Secret s;
+    s.file_path = sget(&js, "FilePath");
+    const JValue* fs = js.get("Findings");
+    if (fs && fs->kind == JValue::Arr) {
+      for (const auto& jf : fs->arr) {
+        Rule rule;
+        rule.id = sget(&jf, "RuleID");
+        rule.category = sget(&jf, "Category");
+        rule.title = sget(&jf, "Title");
+        rule.severity = sget(&jf, "Severity");
+        r->own_rules->push_back(rule);
+        FindingRec f;
+        f.rule = &r->own_rules->back();
+        f.start_line = iget(&jf, "StartLine");
+        f.end_line = iget(&jf, "EndLine");
+        f.match = put(&s, sget(&jf, "Match"));
+        f.line_begin = static_cast<uint32_t>(s.lines.size());
+        const JValue* code = jf.get("Code");
+        const JValue* lines = code ? code->get("Lines") : nullptr;
+        if (lines && lines->kind == JValue::Arr) {
+          for (const auto& jl : lines->arr) {
+            LineRec ln;
+            ln.number = iget(&jl, "Number");
+            ln.content = put(&s, sget(&jl, "Content"));
+            ln.is_cause = bget(&jl, "IsCause");
+            ln.first_cause = bget(&jl, "FirstCause");
+            ln.last_cause = bget(&jl, "LastCause");
+            s.lines.push_back(ln);
+          }
+        }
+        f.line_count = static_cast<uint32_t>(s.lines.size()) - f.line_begin;
+        s.findings.push_back(f);
+      }
+    }
+    r->files.push_back(std::move(s));
+  }
+  *out = r;
+  return TSG_OK;
+}
+
+int tsg_report_json(const tsg_result* const* layers, const tsg_layer* layer_refs, uint32_t nlayers,
+                    const tsg_result* image_config, const tsg_report_opts* opts, char** out, size_t* len) {
+  if ((nlayers && !layers) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::vector<const std::vector<Secret>*> ls;
+  std::vector<LayerRef> refs;
+  for (uint32_t i = 0; i < nlayers; ++i) {
+    if (!layers[i]) return fail(TSG_ERR_INVALID, "NULL layer result");
+    ls.push_back(&layers[i]->files);
+    LayerRef r;
+    if (layer_refs) {
+      r.digest = cstr(layer_refs[i].digest);
+      r.diff_id = cstr(layer_refs[i].diff_id);
+      r.created_by = cstr(layer_refs[i].created_by);
+    }
+    refs.push_back(r);
+  }
+  const Secret* cfg = image_config && !image_config->files.empty() ? &image_config->files[0] : nullptr;
+  ReportOptions o;
+  JValue md;
+  std::string err;
+  if (opts) {
+    o.schema_version = opts->schema_version;
+    if (opts->created_at) o.created_at = opts->created_at;
+    o.artifact_name = cstr(opts->artifact_name);
+    o.artifact_type = cstr(opts->artifact_type);
+    if (opts->metadata_json) {
+      if (!json_parse(opts->metadata_json, &md, &err)) return fail(TSG_ERR_INVALID, "metadata_json: " + err);
+      o.metadata = &md;
+    }
+    o.layers_sorted = opts->layers_sorted != 0;
+    if (opts->severities) {
+      o.severities.clear();
+      std::string cur;
+      for (const char* q = opts->severities;; ++q) {
+        if (*q == ',' || *q == 0) { if (!cur.empty()) o.severities.push_back(cur); cur.clear(); if (!*q) break; }
+        else cur.push_back(*q);
+      }
+    }
+  }
+  std::string doc;
+  if (!report_json(ls, refs, cfg, o, &doc, &err)) return fail(TSG_ERR_INVALID, err);
+  char* buf = static_cast<char*>(malloc(doc.size() + 1));
+  if (!buf) return fail(TSG_ERR_INTERNAL, "out of memory");
+  memcpy(buf, doc.data(), doc.size());
+  buf[doc.size()] = 0;
+  *out = buf;
+  if (len) *len = doc.size();
+  return TSG_OK;
+}
+
+int tsg_image_config_content(const char* config_json, size_t config_len, char** out, size_t* len) {
+  if (!config_json || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string doc, err;
+  if (!image_config_content(std::string(config_json, config_len), &doc, &err)) return fail(TSG_ERR_INVALID, err);
+  char* buf = static_cast<char*>(malloc(doc.size() + 1));
+  if (!buf) return fail(TSG_ERR_INTERNAL, "out of memory");
+  memcpy(buf, doc.data(), doc.size());
+  buf[doc.size()] = 0;
+  *out = buf;
+  if (len) *len = doc.size();
+  return TSG_OK;
+}
+
+int tsg_guess_base_layers(const char* config_json, size_t config_len, const char* const* diff_ids, uint32_t n,
+                          uint8_t* is_base) {
+  if (!config_json || (n && (!diff_ids || !is_base))) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::vector<std::string> ids, base;
+  for (uint32_t i = 0; i < n; ++i) ids.push_back(cstr(diff_ids[i]));
+  std::string err;
+  if (!guess_base_layers(std::string(config_json, config_len), ids, &base, &err)) return fail(TSG_ERR_INVALID, err);
+  for (uint32_t i = 0; i < n; ++i) is_base[i] = std::find(base.begin(), base.end(), ids[i]) != base.end();
+  return TSG_OK;
+}
+
+int tsg_go_time_rfc3339(const char* in, char* out, size_t cap) {
+  std::string t;
+  if (!in || !out || !go_time_rfc3339(in, &t) || t.size() + 1 > cap) return fail(TSG_ERR_INVALID, "not an RFC 3339 time");
+  memcpy(out, t.c_str(), t.size() + 1);
   return TSG_OK;
 }
 

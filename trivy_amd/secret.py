@@ -151,6 +151,19 @@ class Scanner:
     def Scan(self, args):
         return self.ScanBatch([args])[0]
 
+    def ScanBatchResult(self, args_list):
+        """ScanBatch keeping the C result object (trivy_amd.report.ScanResult),
+        for report assembly (trivy_amd.report.JSONReport)."""
+        from .report import ScanResult
+        data, offsets = pack(args_list)
+        paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
+        binary = np.array([1 if a.Binary else 0 for a in args_list] or [0], dtype=np.uint8)
+        res = ctypes.c_void_p()
+        _lib.check(_lib.lib().tsg_scan_batch(self.engine(), data.ctypes.data, offsets.ctypes.data,
+                                             len(args_list), paths, lens, binary.ctypes.data,
+                                             ctypes.byref(res)))
+        return ScanResult(res)
+
     def ScanBatch(self, args_list, with_stats=False):
         data, offsets = pack(args_list)
         paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
@@ -232,6 +245,19 @@ def scan_host_reference(scanner, args_list, threads=1):
     for s in out:
         s.pop("Error", None)
     return out
+
+
+def scan_host_reference_result(scanner, args_list, threads=1):
+    """scan_host_reference keeping the C result object (tests only)."""
+    from .report import ScanResult
+    data, offsets = pack(args_list)
+    paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
+    binary = np.array([1 if a.Binary else 0 for a in args_list] or [0], dtype=np.uint8)
+    res = ctypes.c_void_p()
+    _lib.check(_lib.lib().tsg_scan_host_reference(scanner._rs, data.ctypes.data, offsets.ctypes.data,
+                                                  len(args_list), paths, lens, binary.ctypes.data, threads,
+                                                  ctypes.byref(res)))
+    return ScanResult(res)
 
 
 def scan_table_model(scanner, args_list):
