@@ -271,6 +271,19 @@ int tsg_result_from_json(const char* json, size_t len, tsg_result** out);
 /* Test hook: time.Time JSON round trip (RFC 3339 in, MarshalJSON's form out). */
 int tsg_go_time_rfc3339(const char* in, char* out, size_t cap);
 
+/* ---- client/server wire format ---- */
+/* proto.Marshal of the trivy.common.Secret message (rpc/common/service.proto:
+ * 152-156, 191-223) that ConvertToRPCSecrets (pkg/rpc/convert.go:146-175)
+ * makes of file `file` of the result.  layers: NULL (every finding's Layer is
+ * the empty message, as an fs scan) or one tsg_layer per finding.  Fails with
+ * TSG_ERR_INVALID where proto.Marshal fails: a string that is not valid UTF-8.
+ * Free *out with tsg_free. */
+int tsg_result_to_proto(const tsg_result* r, size_t file, const tsg_layer* layers, char** out, size_t* len);
+/* proto.Unmarshal of n Secret messages + ConvertFromRPCSecrets
+ * (convert.go:504-533): a result with one types.Secret per message; the
+ * findings' Layers appear in tsg_result_json as "Layer". */
+int tsg_result_from_proto(const char* const* msgs, const size_t* lens, size_t n, tsg_result** out);
+
 #ifdef __cplusplus
 }
 #endif

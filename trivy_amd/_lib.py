@@ -111,6 +111,10 @@ SIGNATURES += [
                                               ctypes.c_void_p]),
     ("tsg_go_time_rfc3339", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("tsg_result_from_json", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_result_to_proto", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
+    ("tsg_result_from_proto", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.POINTER(ctypes.c_void_p)]),
 ]
 
 _lib = None

@@ -15,6 +15,7 @@
 #include "prefilter.h"
 #include "report.h"
 #include "scanner.h"
+#include "wire.h"
 
 using namespace tsg;
 
@@ -44,6 +45,7 @@ struct tsg_result {
   std::vector<Secret> files;
   ScanStats stats;
   std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
+  std::vector<std::vector<LayerRef>> layers;               // optional [file][finding] (tsg_result_from_proto)
 };
 
 extern "C" {
@@ -291,6 +293,13 @@ int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
       }
       o += "]},\"Match\":";
       json_bytes(&o, s.ptr(x.match), x.match.len);
+      if (f < r->layers.size() && k < r->layers[f].size()) {
+        const LayerRef& lr = r->layers[f][k];
+        o += ",\"Layer\":{\"Digest\":"; json_str(&o, lr.digest);
+        o += ",\"DiffID\":"; json_str(&o, lr.diff_id);
+        o += ",\"CreatedBy\":"; json_str(&o, lr.created_by);
+        o += "}";
+      }
       o += "}";
     }
     o += "]";
@@ -541,6 +550,43 @@ int tsg_result_from_json(const char* json, size_t len, tsg_result** out) {
     r->files.push_back(std::move(s));
   }
   *out = r;
+  return TSG_OK;
+}
+
+int tsg_result_to_proto(const tsg_result* r, size_t file, const tsg_layer* layers, char** out, size_t* len) {
+  if (!r || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  if (file >= r->files.size()) return fail(TSG_ERR_INVALID, "file index out of range");
+  const Secret& s = r->files[file];
+  std::vector<LayerRef> refs;
+  if (layers) {
+    for (size_t k = 0; k < s.findings.size(); ++k)
+      refs.push_back(LayerRef{cstr(layers[k].digest), cstr(layers[k].diff_id), cstr(layers[k].created_by)});
+  }
+  std::string msg, err;
+  if (!secret_to_proto(s, layers ? &refs : nullptr, &msg, &err)) return fail(TSG_ERR_INVALID, err);
+  char* buf = static_cast<char*>(malloc(msg.size() + 1));
+  if (!buf) return fail(TSG_ERR_INTERNAL, "out of memory");
+  memcpy(buf, msg.data(), msg.size());
+  buf[msg.size()] = 0;
+  *out = buf;
+  if (len) *len = msg.size();
+  return TSG_OK;
+}
+
+int tsg_result_from_proto(const char* const* msgs, const size_t* lens, size_t n, tsg_result** out) {
+  if ((n && (!msgs || !lens)) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  auto r = std::make_unique<tsg_result>();
+  r->own_rules = std::make_shared<std::deque<Rule>>();
+  r->files.resize(n);
+  r->layers.resize(n);
+  std::string err;
+  for (size_t i = 0; i < n; ++i) {
+    if (!msgs[i] && lens[i]) return fail(TSG_ERR_INVALID, "NULL message");
+    if (!secret_from_proto(reinterpret_cast<const uint8_t*>(msgs[i]), lens[i], r->own_rules.get(), &r->files[i],
+                           &r->layers[i], &err))
+      return fail(TSG_ERR_INVALID, err);
+  }
+  *out = r.release();
   return TSG_OK;
 }
 

@@ -46,6 +46,39 @@ class ScanResult:
         except Exception:
             pass
 
+    def to_proto(self, file=0, layers=None):
+        """proto.Marshal of the trivy.common.Secret message of file `file`
+        (pkg/rpc/convert.go:146-175); layers: one {"Digest", "DiffID",
+        "CreatedBy"} per finding, or None."""
+        L = _lib.lib()
+        refs = None
+        keep = []
+        if layers is not None:
+            refs = (_lib.TsgLayer * max(len(layers), 1))()
+            for i, r in enumerate(layers):
+                vals = [_b(r.get(k, "")) for k in ("Digest", "DiffID", "CreatedBy")]
+                keep.extend(vals)
+                refs[i].digest, refs[i].diff_id, refs[i].created_by = vals
+        buf = ctypes.c_void_p()
+        ln = ctypes.c_size_t()
+        _lib.check(L.tsg_result_to_proto(self._h, file, refs, ctypes.byref(buf), ctypes.byref(ln)))
+        try:
+            return ctypes.string_at(buf, ln.value)
+        finally:
+            L.tsg_free(buf)
+
+    @classmethod
+    def from_proto(cls, messages):
+        """proto.Unmarshal + ConvertFromRPCSecrets (convert.go:526-533) of
+        Secret messages, one types.Secret per message."""
+        n = len(messages)
+        bufs = [ctypes.create_string_buffer(bytes(m), max(len(m), 1)) for m in messages]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in bufs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(m) for m in messages])
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().tsg_result_from_proto(ptrs, lens, n, ctypes.byref(h)))
+        return cls(h)
+
     @classmethod
     def from_secrets(cls, secrets):
         """Test hook: a result holding the given types.Secret dicts."""
