@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--variants", default="",
+                    help="comma list of VARIANT[:ABL[:CHUNK]] (TSG_K1_VARIANT / TSG_K1_ABL / TSG_K1_CHUNK), "
+                         "one engine each")
     args = ap.parse_args()
     import torch
 
@@ -43,9 +46,24 @@ def main():
         synth.plant_custom(c, plants, seed=args.seed, rate=1e-4)
     d = torch.from_numpy(c.data).to("cuda:0")
     torch.cuda.synchronize()
-    sc = S.Scanner(S.ParseConfig(cfg) if cfg else None)
-    eng = sc.engine()
     L = _lib.lib()
+    variants = [v for v in args.variants.split(",") if v] or [None]
+    for v in variants:
+        if v is not None:
+            parts = v.split(":") + ["", ""]
+            os.environ["TSG_K1_VARIANT"] = parts[0]
+            os.environ["TSG_K1_ABL"] = parts[1] or "0"
+            if parts[2]:
+                os.environ["TSG_K1_CHUNK"] = parts[2]
+            else:
+                os.environ.pop("TSG_K1_CHUNK", None)
+        sc = S.Scanner(S.ParseConfig(cfg) if cfg else None)
+        probe(args, sc, c, d, L)
+
+
+def probe(args, sc, c, d, L):
+    from trivy_amd import _lib
+    eng = sc.engine()
     rows = []
     for r in range(args.reps + 1):
         res = ctypes.c_void_p()

@@ -126,6 +126,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("libtrivysecret.so is not built (run __graft_entry__.build() or "
                                "python -m trivy_amd.build); there is no fallback")
+        # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+        # libamdhip64.so.7, loaded by file name), so load it first and the
+        # library's libamdhip64.so.7 dependency binds to that copy.  Loading
+        # /opt/rocm's copy first leaves torch a second runtime that finds no
+        # device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)

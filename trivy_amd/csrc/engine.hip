@@ -68,6 +68,7 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
 constexpr uint32_t kWaveHits = 1024;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
+constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [2] overflow, [4 + g] v3 items of group g
 
 // Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
 // record's 32 - kAnchorBits offset bits.
@@ -164,40 +165,6 @@ __device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Str
   return min(t.emit + x.chunk, x.total);
 }
 
-// The output list of an output state (anchor hits, keyword ids >= 128): out
-// of line, so the per-position output checks stay small.
-__device__ __noinline__ void k1_out_list(const K1Ctx& x, K1Stream& t, uint32_t begin, uint32_t count,
-                                         unsigned long long q) {
-  for (uint32_t j = 0; j < count; ++j) {
-    const uint32_t id = x.list[begin + j];
-    if (id < x.nkw) {
-      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
-    } else {
-      const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
-      if (li < kWaveHits) {
-        x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
-      } else {                                           // buffer full: straight to the region
-        const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
-        if (gi < x.region_cap) {
-          x.hits[gi] = (q << 24) | (id - x.nkw);
-        } else {                                         // region full: the shared overflow pool
-          const uint32_t oi = atomicAdd(x.over_cnt, 1u);
-          if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
-        }
-      }
-    }
-  }
-}
-
-// K1 v2's per-output work: keyword masks in registers, the list out of line.
-__device__ __forceinline__ void k1_out2(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
-  const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
-  const OutMeta m = x.meta[o];
-  t.kw0 |= m.kw0;
-  t.kw1 |= m.kw1;
-  if (m.list_count) k1_out_list(x, t, m.list_begin, m.list_count, q);
-}
-
 __device__ __forceinline__ void k1_out(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
   const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
   const OutMeta m = x.meta[o];
@@ -243,8 +210,39 @@ __device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, co
   }
 }
 
+// The outputs of output state `st` (row offset): its row carries the keyword
+// masks and the list position inline after the spare slot (S = silent-row
+// stride), so one LDS round trip fetches them.
+__device__ __forceinline__ void k1_out_v3(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q, uint32_t S) {
+  const uint32_t* m = reinterpret_cast<const uint32_t*>(x.next + st + S);   // 4-byte aligned: st and S are even
+  const uint32_t a0 = m[0], a1 = m[1], a2 = m[2], a3 = m[3], li = m[4];
+  t.kw0 |= (static_cast<unsigned long long>(a1) << 32) | a0;
+  t.kw1 |= (static_cast<unsigned long long>(a3) << 32) | a2;
+  const uint32_t begin = li & 0xffffu, count = li >> 16;
+  for (uint32_t j = 0; j < count; ++j) {
+    const uint32_t id = x.list[begin + j];
+    if (id < x.nkw) {
+      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
+    } else {
+      const uint32_t li2 = atomicAdd(x.w_hitcnt, 1u);
+      if (li2 < kWaveHits) {
+        x.w_hits[li2] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
+      } else {                                           // buffer full: straight to the region
+        const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
+        if (gi < x.region_cap) {
+          x.hits[gi] = (q << 24) | (id - x.nkw);
+        } else {                                         // region full: the shared overflow pool
+          const uint32_t oi = atomicAdd(x.over_cnt, 1u);
+          if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
+        }
+      }
+    }
+  }
+}
+
 // One 16-byte word of one stream with file-boundary and stream-end checks.
-__device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4]) {
+template <bool kInlineMeta = false>
+__device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4], uint32_t S = 0) {
   const unsigned long long end = k1_end(x, t);
   unsigned long long fend = x.offsets[t.f + 1];
   if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
@@ -261,7 +259,10 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
     t.s = k1_step(x.next, t.s, x.cls[b]);
     if (q >= t.emit) {
       t.nl += (b == 0x0au);
-      if (t.s >= x.first_out) k1_out(x, t, t.s, q);
+      if (t.s >= x.first_out) {
+        if (kInlineMeta) k1_out_v3(x, t, t.s, q, S);
+        else k1_out(x, t, t.s, q);
+      }
     }
     t.p12 = ((t.p12 << 8) & 0xff00u) | b;
   }
@@ -311,7 +312,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
+    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ /*item_ctr: v3*/,
+    uint32_t* __restrict__ /*obuf: v3*/) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | (scan table | class map |
   //              output meta | output list)]
@@ -554,21 +556,126 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
   }
 }
 
-// K1 v2: the same pass with a leaner per-byte path.  The LDS layout puts the
-// class map and the scan table at compile-time offsets, so a transition is
-// one v_lshl_add + one ds_read_u16 with an immediate offset and a class
-// lookup one ds_read_u8 with an immediate offset; 64-byte lines are
-// double-buffered (the next line's loads are in flight while this one is
-// walked); per-position output handling keeps only the keyword-mask update
-// inline (k1_out2) and the special-rune check is out of line.
-__device__ __noinline__ void k1_special_call(const K1Ctx& x, const K1Stream& t, uint32_t w0, uint32_t w1, uint32_t w2,
-                                             uint32_t w3) {
-  const uint32_t w[4] = {w0, w1, w2, w3};
-  k1_special(x, t, w, ~0ull, ~0ull);
+// K1 v3: the same pass, built around the per-byte cost.
+//  * LDS layout [class map (256 B) | scan table | output meta | output list |
+//    per-wave hit buffers | counters]: the class map and the table sit at
+//    compile-time offsets below 64 KiB, so a class lookup is one ds_read_u8
+//    addressed by the byte itself and a transition one v_lshl_add + one
+//    ds_read_u16 with an immediate offset;
+//  * 128-byte lines are double-buffered in registers: the next line's loads
+//    are in flight while this one is walked;
+//  * newlines are counted with one popcount per dword (32 - popc of the
+//    zero-byte mask word);
+//  * output positions of a word are found from one max over its 16 states,
+//    then handled through a position mask, so each word carries one copy of
+//    the output code;
+//  * wave work items come from one global counter per launch (no static
+//    per-workgroup ranges, no tail of idle CUs).
+// kAbl (measurement only, results are wrong with any bit set except
+// kAblTemporal): drop a part of the per-byte work to price it.
+constexpr int kAblNoNl = 1, kAblNoOut = 2, kAblNoCls = 4, kAblNoSpecial = 8, kAblTemporal = 16, kAblLoadOnly = 32;
+// layout bits (results stay valid): 64-byte lines instead of 128; word loop
+// rolled (register-indexed) instead of unrolled
+constexpr int kAblLine64 = 64, kAblRolled = 128, kAblDefer = 256;
+// Deferred outputs (kAblDefer): a lane parks each output position of its
+// fast lines as (offset from the chunk start << 16 | state) in its own slots
+// of a global buffer (L2-resident) and handles them when its file or chunk
+// ends, every lane at once, instead of the wave stopping at each position
+// where any lane has one.
+constexpr uint32_t kOutSlots = 8;
+struct OutBuf { uint32_t* p; uint32_t stride, n; };
+
+template <int kAbl>
+__device__ __forceinline__ v4u k1_load(const uint8_t* p) {
+  if (kAbl & kAblTemporal) return *reinterpret_cast<const v4u*>(p);
+  return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
 }
 
-template <int kThreads>
-__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v2(
+// Does a U+0130 / U+017F / U+212A encoding end inside the 128-byte line at p
+// (p12: the two bytes before it)?  Out of line: only lines with a byte >= 0x80
+// get here.  The fast path's line lies in one file, which is flagged.
+__device__ __noinline__ bool k1_line_special(const uint8_t* __restrict__ p, uint32_t p12, uint32_t n) {
+  uint32_t a = p12 & 0xffu, bb = p12 >> 8;
+  bool hit = false;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t b = p[k];
+    hit |= (b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u);
+    bb = a;
+    a = b;
+  }
+  return hit;
+}
+
+__device__ __forceinline__ void k1_drain(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t S) {
+  for (uint32_t i = 0; i < ob.n; ++i) {
+    const uint32_t e = ob.p[i * ob.stride];
+    k1_out_v3(x, t, e & 0xffffu, t.emit + (e >> 16), S);
+  }
+  ob.n = 0;
+}
+
+template <int kAbl>
+__device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& ob, const uint8_t* smem, uint32_t S,
+                                           uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  constexpr uint32_t kTabOff = 256;
+  const bool emit = t.p >= t.emit;
+  if (kAbl & kAblLoadOnly) {            // the loads kept live through kw1 (discarded at the end)
+    t.kw1 += w0 ^ w1 ^ w2 ^ w3;
+    t.p += 16;
+    return;
+  }
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t c2[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    c2[k] = (kAbl & kAblNoCls) ? ((b & 31u) << 1) : static_cast<uint32_t>(smem[b]);   // NoCls: nclasses >= 32
+  }
+  uint32_t st[16];
+  uint32_t s = t.s;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 1) + c2[k]);
+    st[k] = s;
+  }
+  t.s = s;
+  if (emit) {
+    if (!(kAbl & kAblNoNl)) {
+      uint32_t u[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t xx = w[j] ^ 0x0a0a0a0au;
+        u[j] = ((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu;   // bit 7 of a byte: not '\n'
+      }
+      t.nl += 128u - (__popc(u[0]) + __popc(u[1]) + __popc(u[2]) + __popc(u[3]));
+    }
+    if (!(kAbl & kAblNoOut)) {
+      // outputs: one max per 4 positions decides (wave-wide) whether to look
+      // at them one by one; each output position costs one LDS round trip
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (max(max(st[4 * j], st[4 * j + 1]), max(st[4 * j + 2], st[4 * j + 3])) >= x.first_out) {
+#pragma unroll
+          for (int k = 4 * j; k < 4 * j + 4; ++k) {
+            if (st[k] >= x.first_out) {
+              if ((kAbl & kAblDefer) && ob.n < kOutSlots) {
+                ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k - t.emit) << 16) | st[k];
+                ++ob.n;
+              } else {
+                k1_out_v3(x, t, st[k], t.p + k, S);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  t.p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
+  t.p += 16;
+}
+
+template <int kThreads, int kAbl>
+__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const uint8_t* __restrict__ data, unsigned long long total,
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
@@ -578,37 +685,38 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v2(
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags) {
+    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
+    uint32_t* __restrict__ obuf) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | class map (256) |
-  //              scan table | output meta | output list]
   constexpr uint32_t kWaves = kThreads / 64;
-  constexpr uint32_t kClsOff = kWaves * kWaveHits * 4 + kMaxWaves * 4 + 16;
-  constexpr uint32_t kTabOff = kClsOff + 256;
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
-  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count, [1] next item
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) { s_block[0] = 0; s_block[1] = 0; }
+  constexpr uint32_t kTabOff = 256;
   const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
+  const uint32_t meta_off = kTabOff + padded;
+  const uint32_t list_off = meta_off;            // output metadata is inline in the table rows
+  const uint32_t hits_off = (list_off + nlist * 4 + 15) & ~15u;
+  uint32_t S = (nclasses + 2) & ~1u;             // k1_row_stride(nclasses): the silent-row stride
+  if (((S / 2) & 1u) == 0) S += 2;
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
+  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
+  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_block[0] = 0;
   {
     const uint4* src = reinterpret_cast<const uint4*>(g_next);
     uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff);
     for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[kClsOff + i] = g_cls[i];
-    OutMeta* s_meta = reinterpret_cast<OutMeta*>(smem + kTabOff + padded);
-    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_meta + nmeta);
-    for (uint32_t i = threadIdx.x; i < nmeta; i += blockDim.x) s_meta[i] = g_meta[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[i] = g_cls[i];
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(smem + list_off);
     for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
   }
   K1Ctx x;
   x.data = data; x.total = total; x.chunk = chunk;
   x.offsets = offsets; x.nfiles = nfiles;
   x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
-  x.cls = smem + kClsOff;
+  x.cls = smem;
   x.first_out = first_out; x.nclasses = nclasses;
-  x.meta = reinterpret_cast<const OutMeta*>(smem + kTabOff + padded);
-  x.list = reinterpret_cast<const uint32_t*>(x.meta + nmeta);
+  x.meta = nullptr;
+  x.list = reinterpret_cast<const uint32_t*>(smem + list_off);
   x.nkw = nkw;
   x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
   x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
@@ -616,79 +724,71 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v2(
   x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
   __syncthreads();
   const unsigned long long nitems = (nchunks + 63) / 64;       // wave work items (64 chunks)
-  const unsigned long long per_block = (nitems + gridDim.x - 1) / gridDim.x;
-  const unsigned long long first_item = per_block * blockIdx.x;
-  const unsigned long long last_item = min(first_item + per_block, nitems);
   for (;;) {
     unsigned long long item = 0;
     if (lane == 0) {
-      item = first_item + atomicAdd(&s_block[1], 1u);
+      item = atomicAdd(item_ctr, 1u);
       *x.w_hitcnt = 0;
     }
     item = __shfl(item, 0);
-    if (item >= last_item) break;                              // wave-uniform exit
+    if (item >= nitems) break;                                 // wave-uniform exit
     __builtin_amdgcn_wave_barrier();
     x.item_base = item * 64 * static_cast<unsigned long long>(chunk);
     const unsigned long long c = item * 64 + lane;
     if (c < nchunks) {
       K1Stream t;
       k1_init(x, t, min(c * chunk, total), warm_lines);
-      v4u nxt[4];
-      bool have_next = false;
+      OutBuf ob{obuf + blockIdx.x * kThreads + threadIdx.x, gridDim.x * kThreads, 0};
+      constexpr int kW = (kAbl & kAblLine64) ? 4 : 8;     // words per line
+      constexpr uint32_t kL = kW * 16;
+      v4u cur[kW], nxt[kW];
+      bool have = false;
       for (;;) {
         if (!(t.p < t.lim || t.p < k1_end(x, t))) break;
-        if (t.p + 64 <= t.lim) {
-          v4u cur[4];
-          if (have_next) {
+        if (t.p + kL <= t.lim) {
+          if (!have) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+            for (int i = 0; i < kW; ++i) cur[i] = k1_load<kAbl>(data + t.p + 16 * i);
+          }
+          have = t.p + 2 * kL <= t.lim;
+          if (have) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) nxt[i] = k1_load<kAbl>(data + t.p + kL + 16 * i);
+          }
+          if (!(kAbl & (kAblNoSpecial | kAblLoadOnly)) && x.primary) {
+            uint32_t hb = 0;
+#pragma unroll
+            for (int i = 0; i < kW; ++i) hb |= cur[i].x | cur[i].y | cur[i].z | cur[i].w;
+            if ((hb & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
+          }
+          if (kAbl & kAblRolled) {
+            // one copy of the word body: the uniform word index selects
+            // cur[i] by register indexing
+#pragma unroll 1
+            for (int i = 0; i < kW; ++i) k1_word_v3<kAbl>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
           } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cur[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + t.p + 16 * i));
+            for (int i = 0; i < kW; ++i) k1_word_v3<kAbl>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
           }
-          have_next = t.p + 128 <= t.lim;
-          if (have_next) {
+          if (have) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              nxt[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + t.p + 64 + 16 * i));
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t w0 = cur[i].x, w1 = cur[i].y, w2 = cur[i].z, w3 = cur[i].w;
-            const bool emit = t.p >= t.emit;
-            if (x.primary && ((w0 | w1 | w2 | w3) & 0x80808080u) && emit) k1_special_call(x, t, w0, w1, w2, w3);
-            const uint32_t w[4] = {w0, w1, w2, w3};
-            uint32_t cl[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) cl[k] = smem[kClsOff + ((w[k >> 2] >> ((k & 3) * 8)) & 0xffu)];
-            uint32_t st[16], mx = 0, s = t.s;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-              s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 1) + cl[k]);
-              st[k] = s;
-              mx = max(mx, s);
-            }
-            t.s = s;
-            if (emit) {
-              t.nl += nl_in_word(w0) + nl_in_word(w1) + nl_in_word(w2) + nl_in_word(w3);
-              if (mx >= first_out) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                  if (st[k] >= first_out) k1_out2(x, t, st[k], t.p + k);
-              }
-            }
-            t.p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
-            t.p += 16;
+            for (int i = 0; i < kW; ++i) cur[i] = nxt[i];
           }
         } else {
           // a line with a file boundary or the chunk end (rare): word by word
-          have_next = false;
-          for (int i = 0; i < 4 && t.p < k1_end(x, t); ++i) {
+          have = false;
+          if (kAbl & kAblDefer) k1_drain(x, t, ob, S);     // parked outputs belong to file t.f
+          for (int i = 0; i < kW && t.p < k1_end(x, t); ++i) {
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            k1_word_slow(x, t, w);
+            k1_word_slow<true>(x, t, w, S);
           }
         }
+      }
+      if (kAbl & kAblDefer) k1_drain(x, t, ob, S);
+      if (kAbl & kAblLoadOnly) {
+        t.nl = static_cast<uint32_t>(t.kw1);
+        t.kw1 = 0;
       }
       flush_kw(x.kwmask, kw_words, t.f, t.kw0, t.kw1);
       if (x.primary) nl_count[c] = t.nl;
@@ -730,9 +830,21 @@ const void* k1_kernel_t(uint32_t threads, int ks) {
   return nullptr;
 }
 
-// variant 2 (tsg_k1_scan_v2) needs the table in LDS, 1024 threads, one stream per lane
-const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1) {
-  if (variant == 2 && lds && threads == 1024 && ks == 1) return reinterpret_cast<const void*>(&tsg_k1_scan_v2<1024>);
+// variant 3 (tsg_k1_scan_v3) needs the table in LDS, 1024 threads, one stream
+// per lane; `abl` selects a measurement build (kAbl*)
+const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int abl = 0) {
+  if (variant == 3) {
+    if (!lds || threads != 1024 || ks != 1) return nullptr;
+    switch (abl) {
+#define TSG_K1_V3(A) case (A): return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, (A)>);
+      TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(17) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(26) TSG_K1_V3(27)
+      TSG_K1_V3(31) TSG_K1_V3(32) TSG_K1_V3(48)
+      TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(82) TSG_K1_V3(146) TSG_K1_V3(210) TSG_K1_V3(112) TSG_K1_V3(240)
+      TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(464) TSG_K1_V3(466)
+#undef TSG_K1_V3
+      default: return nullptr;
+    }
+  }
   return lds ? k1_kernel_t<true>(threads, ks) : k1_kernel_t<false>(threads, ks);
 }
 
@@ -768,7 +880,7 @@ struct K1Group {
   uint8_t* cls = nullptr;      // byte -> class * 2
   OutMeta* meta = nullptr;
   uint32_t* list = nullptr;
-  uint32_t nmeta = 0, nlist = 0, table_words16 = 0, stride = 0, nclasses = 0, first_out = 0;
+  uint32_t nmeta = 0, nlist = 0, table_words16 = 0, stride = 0, ostride = 0, nclasses = 0, first_out = 0;
   uint32_t kw_base = 0, warm_lines = 0;
   size_t meta_bytes = 0;
   bool in_lds = false;
@@ -811,6 +923,7 @@ struct Lane {
   CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
   uint32_t* d_nl = nullptr; size_t d_nl_cap = 0;
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
+  uint32_t* d_ob = nullptr; size_t d_ob_cap = 0;    // K1 v3 deferred-output slots (kOutSlots per thread)
   unsigned int* d_cnt = nullptr;
   std::vector<uint32_t> h_bh;
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
@@ -855,7 +968,7 @@ Lane::~Lane() {
   hipSetDevice(device);
   if (compute) hipStreamSynchronize(compute);
   if (copy) hipStreamSynchronize(copy);
-  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_cnt};
+  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
@@ -885,27 +998,34 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     K1Group g;
     // scan table with an odd dword row stride: next[s*stride + c] then spreads
     // the same class of different states over different LDS banks (a 64-class
-    // row is 32 dwords, which would put every state's class c in one bank)
+    // row is 32 dwords, which would put every state's class c in one bank).
+    // Silent rows first (stride S), then output rows (stride So): slot C of an
+    // output row holds the output-state index (K1 v1's meta lookup), slots
+    // S..S+9 its metadata inline (v3: keyword masks and list in the same LDS
+    // round trip as the row address)
     const uint32_t C = sd.t.nclasses;
-    const uint32_t stride = k1_row_stride(C);   // slot C holds the output-state index
+    const uint32_t stride = k1_row_stride(C);
+    const uint32_t ostride = k1_out_row_stride(C);
+    const uint32_t fo = sd.first_out_state;
     g.stride = stride;
     g.nclasses = C;
-    g.first_out = sd.first_out_state * stride;
+    g.first_out = fo * stride;
     g.kw_base = sd.kw_base;
     const uint32_t warm = sd.max_pattern_bytes > 0 ? sd.max_pattern_bytes - 1 : 0;
     g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk
-    // entries hold the next state's row offset (state * stride): the DFA chain
-    // is then one add + one LDS read per byte (no multiply)
-    if (static_cast<uint64_t>(sd.t.nstates) * stride > 65535) {
+    // entries hold the next state's row offset: the DFA chain is then one
+    // add + one LDS read per byte (no multiply)
+    if (k1_table_words16(sd) > 65535) {
       *err = "scan DFA group too large for 16-bit pre-multiplied offsets";
       return false;
     }
     if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return false; }
-    std::vector<uint16_t> sn(static_cast<size_t>(sd.t.nstates) * stride, 0);
+    auto row = [&](uint32_t st) { return st < fo ? st * stride : fo * stride + (st - fo) * ostride; };
+    std::vector<uint16_t> sn(k1_table_words16(sd), 0);
     for (uint32_t st = 0; st < sd.t.nstates; ++st) {
       for (uint32_t c = 0; c < C; ++c)
-        sn[static_cast<size_t>(st) * stride + c] = static_cast<uint16_t>(sd.t.next[static_cast<size_t>(st) * C + c] * stride);
-      if (st >= sd.first_out_state) sn[static_cast<size_t>(st) * stride + C] = static_cast<uint16_t>(st - sd.first_out_state);
+        sn[row(st) + c] = static_cast<uint16_t>(row(sd.t.next[static_cast<size_t>(st) * C + c]));
+      if (st >= fo) sn[row(st) + C] = static_cast<uint16_t>(st - fo);
     }
     // per output state: keyword masks (ids kw_base .. kw_base+127) + list of other output ids
     std::vector<OutMeta> meta;
@@ -919,8 +1039,17 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
         else olist.push_back(id);
       }
       om.list_count = static_cast<uint32_t>(olist.size()) - om.list_begin;
+      if (om.list_begin > 0xffff || om.list_count > 0xffff) { *err = "scan DFA output list too long"; return false; }
       meta.push_back(om);
+      uint16_t* m = &sn[row(fo + o) + stride];
+      for (int k = 0; k < 4; ++k) {
+        m[k] = static_cast<uint16_t>(om.kw0 >> (16 * k));
+        m[4 + k] = static_cast<uint16_t>(om.kw1 >> (16 * k));
+      }
+      m[8] = static_cast<uint16_t>(om.list_begin);
+      m[9] = static_cast<uint16_t>(om.list_count);
     }
+    g.ostride = ostride;
     g.nmeta = static_cast<uint32_t>(meta.size());
     g.nlist = static_cast<uint32_t>(olist.size());
     g.meta_bytes = ((meta.size() * sizeof(OutMeta) + olist.size() * 4) + 15) & ~size_t(15);
@@ -1063,8 +1192,9 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   }
   if (const char* c = std::getenv("TSG_K1_VARIANT")) {
     const int v = std::atoi(c);
-    if (v == 1 || v == 2) e->k1_variant_ = v;
+    if (v == 1 || v == 3) e->k1_variant_ = v;
   }
+  if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // measurement builds of v3 only
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
     // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
     // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
@@ -1098,7 +1228,7 @@ Lane* Engine::acquire_lane(DeviceTables& dt, std::string* err) {
   std::unique_ptr<Lane> l(new Lane());
   l->device = dt.device;
   if (hipSetDevice(dt.device) != hipSuccess || hipStreamCreateWithFlags(&l->compute, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&l->copy, hipStreamNonBlocking) != hipSuccess || hipMalloc(&l->d_cnt, 64) != hipSuccess) {
+      hipStreamCreateWithFlags(&l->copy, hipStreamNonBlocking) != hipSuccess || hipMalloc(&l->d_cnt, kCntBytes) != hipSuccess) {
     *err = "lane setup (streams, counters) failed";
     return nullptr;
   }
@@ -1165,15 +1295,17 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   ln.over_cap = std::max<size_t>(ln.over_cap, total / 2048);
   if (!ensure(&ln.d_over, &ln.d_over_cap, ln.over_cap, err)) return false;
   const uint32_t ngroups = static_cast<uint32_t>(dt.k1g.size());
+  if (4 + ngroups > kCntBytes / 4) { *err = "too many scan-DFA groups"; return false; }
   if (!ensure(&ln.d_bh, &ln.d_bh_cap, 2ull * std::max(dt.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
   if (!ensure(&ln.d_ff, &ln.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
+  if (!ensure(&ln.d_ob, &ln.d_ob_cap, 2ull * std::max(dt.sms, 1) * 1024 * kOutSlots, err)) return false;
 
   const uint32_t sms = static_cast<uint32_t>(dt.sms);
   const Prefilter& pf = pf_;
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_OK(hipMemsetAsync(ln.d_kw, 0, kw_n * sizeof(uint32_t), s));
     HIP_OK(hipMemsetAsync(ln.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), s));
-    HIP_OK(hipMemsetAsync(ln.d_cnt, 0, 64, s));
+    HIP_OK(hipMemsetAsync(ln.d_cnt, 0, kCntBytes, s));
     const int ks = k1_streams_;
     const uint32_t nthr = k1_threads_;
     const uint64_t want_blocks = (nchunks + static_cast<uint64_t>(nthr) * ks - 1) / (static_cast<uint64_t>(nthr) * ks);
@@ -1189,14 +1321,17 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
     const uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(ln.hit_cap / nregions, 0xffffffffu));
     HIP_OK(hipMemsetAsync(ln.d_bh, 0, nregions * sizeof(uint32_t), s));
+    // v3 runs the groups whose table is in LDS (1024 threads, one stream per
+    // lane); the others keep v1
+    auto k1_var = [&](const K1Group& g) { return k1_variant_ == 3 && g.in_lds && nthr == 1024 && ks == 1 ? 3 : 1; };
     auto k1_lds = [&](const K1Group& g) {
       return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
              (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
     };
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
       const K1Group& g = dt.k1g[gi];
-      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_variant_);
-      if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG)"; return false; }
+      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_var(g), k1_abl_);
+      if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG / TSG_K1_ABL)"; return false; }
       HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(k1_lds(g))));
     }
     HIP_OK(hipEventRecord(ln.ev[0], s));
@@ -1204,7 +1339,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = dt.k1g[gi];
       const size_t lds = k1_lds(g);
-      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_variant_);
+      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_var(g), k1_abl_);
+      uint32_t* a_items = ln.d_cnt + 4 + gi;         // v3's work-item counter (zeroed with d_cnt)
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
       uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
@@ -1225,7 +1361,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       void* args[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
-                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff};
+                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob};
       HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, s));
       ++launches;
     }

@@ -3,6 +3,8 @@
 #include "prefilter.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <bitset>
 #include <cstring>
 #include <map>
@@ -23,6 +25,8 @@ constexpr uint32_t kMaxPrefixBytes = 96; // dmax cap for a usable anchor
 constexpr uint32_t kVerifyStateCap = 3000;
 constexpr uint32_t kScanStateCap = 60000;
 constexpr uint32_t kVerifyLimitCap = 8192;
+constexpr double kWeakAnchor = 3.0;
+constexpr size_t kHostKeywordLen = 3;     // keywords this short gate on the host      // literal anchors scoring below this get class extensions
 
 using Bits = std::bitset<256>;
 
@@ -317,35 +321,59 @@ bool finite_set(const Node& n, SeqSet* out) {
   }
 }
 
-// Set of sequences one of which begins every match of items[k..] (Seq{} = no info).
-SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k);
+// A character class of ASCII characters only, as one unit of single-byte
+// alternatives (anchor extensions: a weak literal followed by such a class).
+bool class_unit(const Node& n, Unit* u) {
+  if (n.op != Op::CharClass) return false;
+  for (const auto& r : n.ranges) {
+    if (r.hi >= 0x80) return false;
+    for (uint32_t c = r.lo; c <= r.hi; ++c) u->push_back(std::string(1, static_cast<char>(c)));
+  }
+  return !u->empty() && u->size() <= 96;
+}
 
-SeqSet prefix_set(const Node& n) {
+// Set of sequences one of which begins every match of items[k..] (Seq{} = no
+// info).  ext: a class item that ends the literal part contributes up to
+// kExtUnits class units (used for weak anchors only: they add scan states).
+int ext_units() {
+  static const int n = [] { const char* e = std::getenv("TSG_ANCHOR_EXT"); return e ? std::atoi(e) : 0; }();
+  return n;
+}
+SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k, bool ext = false);
+
+SeqSet prefix_set(const Node& n, bool ext = false) {
   SeqSet f;
   if (finite_set(n, &f)) return f;
+  Unit u;
   switch (n.op) {
-    case Op::Capture: return prefix_set(*n.sub[0]);
+    case Op::Capture: return prefix_set(*n.sub[0], ext);
     case Op::Concat: {
       std::vector<const Node*> items;
       for (const auto& s : n.sub) items.push_back(s.get());
-      return prefix_of_items(items, 0);
+      return prefix_of_items(items, 0, ext);
     }
     case Op::Alternate: {
       SeqSet out;
       for (const auto& s : n.sub) {
-        SeqSet p = prefix_set(*s);
+        SeqSet p = prefix_set(*s, ext);
         out.insert(p.begin(), p.end());
         if (static_cast<int>(out.size()) > kMaxSetSize) return SeqSet{Seq{}};
       }
       return out;
     }
-    case Op::Plus: return prefix_set(*n.sub[0]);
-    case Op::Repeat: if (n.min >= 1) return prefix_set(*n.sub[0]); return SeqSet{Seq{}};
+    case Op::CharClass:
+      if (ext && ext_units() > 0 && class_unit(n, &u)) return SeqSet{Seq{u}};
+      return SeqSet{Seq{}};
+    case Op::Plus: return prefix_set(*n.sub[0], ext);
+    case Op::Repeat:
+      if (n.min < 1) return SeqSet{Seq{}};
+      if (ext && class_unit(*n.sub[0], &u)) return SeqSet{Seq(std::min(n.min, ext_units()), u)};
+      return prefix_set(*n.sub[0], ext);
     default: return SeqSet{Seq{}};
   }
 }
 
-SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k) {
+SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k, bool ext) {
   SeqSet acc{Seq{}};
   for (size_t i = k; i < items.size(); ++i) {
     SeqSet f, t;
@@ -354,7 +382,7 @@ SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k) {
       acc.swap(t);
       continue;
     }
-    SeqSet p = prefix_set(*items[i]);
+    SeqSet p = prefix_set(*items[i], ext);
     if (!cross(acc, p, &t)) return acc;
     acc.swap(t);
     break;
@@ -380,9 +408,34 @@ uint32_t seq_max_len(const Seq& s) {
 }
 
 // Selectivity score of a literal unit sequence: longer and case-sensitive is better.
+// "abc" for single-string units, "(a|A)" for alternatives (report only)
+std::string seq_str(const Seq& s) {
+  std::string o;
+  auto esc = [&](const std::string& b) {
+    for (unsigned char c : b) {
+      if (c >= 0x20 && c < 0x7f && c != '|' && c != '(' && c != ')' && c != '\\') o.push_back(static_cast<char>(c));
+      else { char t[8]; snprintf(t, sizeof t, "\\x%02x", c); o += t; }
+    }
+  };
+  for (const auto& u : s) {
+    if (u.size() == 1) { esc(u[0]); continue; }
+    o.push_back('(');
+    for (size_t i = 0; i < u.size(); ++i) { if (i) o.push_back('|'); esc(u[i]); }
+    o.push_back(')');
+  }
+  return o;
+}
+
+std::string seqs_str(const SeqSet& ss) {
+  std::string o;
+  for (const auto& s : ss) { if (!o.empty()) o += " "; o += seq_str(s); }
+  return o;
+}
+
 double seq_score(const Seq& s) {
   double sc = 0;
   for (const auto& u : s) {
+    if (u.size() > 8) { sc += 0.3; continue; }      // a class unit (anchor extension)
     const char c = static_cast<char>(tolower(static_cast<unsigned char>(u[0][0])));
     bool common = u[0].size() == 1 && strchr(" etaoinsr\"'=:_-.,", c) != nullptr;
     sc += common ? 0.7 : 1.0;
@@ -557,14 +610,31 @@ AnchorChoice choose_anchor(const std::vector<const Node*>& items, bool bounded =
   uint32_t plo = 0, phi = 0;
   for (size_t k = 0; k < items.size(); ++k) {
     if (!bounded || phi <= kMaxPrefixBytes) {
-      SeqSet raw = prefix_of_items(items, k);
-      SeqSet lits;
-      for (const auto& s : raw) lits.insert(scan_form(s));
-      double score = 1e9;
-      bool usable = !lits.empty();
-      for (const auto& s : lits) {
-        if (s.empty()) { usable = false; break; }
-        score = std::min(score, seq_score(s));
+      auto form = [&](bool ext, SeqSet* raw, SeqSet* lits, double* score) {
+        *raw = prefix_of_items(items, k, ext);
+        lits->clear();
+        for (const auto& s : *raw) lits->insert(scan_form(s));
+        *score = 1e9;
+        bool ok = !lits->empty();
+        for (const auto& s : *lits) {
+          if (s.empty()) { ok = false; break; }
+          *score = std::min(*score, seq_score(s));
+        }
+        return ok;
+      };
+      SeqSet raw, lits;
+      double score;
+      bool usable = form(false, &raw, &lits, &score);
+      if (usable && score < kWeakAnchor) {
+        // a weak literal ("ey", "sk"): extend it by the class that follows
+        // (ey[a-zA-Z0-9]{17,} -> ey + 2 alnum units), far fewer K1 hits
+        SeqSet xraw, xlits;
+        double xscore;
+        if (form(true, &xraw, &xlits, &xscore) && xscore > score) {
+          raw.swap(xraw);
+          lits.swap(xlits);
+          score = xscore;
+        }
       }
       if (usable) {
         // every extra literal costs scan-DFA states: prefer small sets
@@ -769,6 +839,10 @@ bool make_groups(Prefilter* pf, std::vector<Pattern> pats, std::string* err) {
       pf->groups.push_back(std::move(all));
       return true;
     }
+    if (std::getenv("TSG_PREFILTER_DEBUG"))
+      fprintf(stderr, "one-group scan DFA: %u states x %u classes (%u silent), %zu table words, LDS %zu B\n",
+              all.t.nstates, all.t.nclasses, all.first_out_state, static_cast<size_t>(k1_table_words16(all)),
+              k1_lds_table_bytes(all));
   }
   std::vector<std::string> keys(pats.size());
   std::vector<size_t> order(pats.size());
@@ -848,16 +922,26 @@ uint32_t k1_row_stride(uint32_t nclasses) {
   return s;
 }
 
+uint32_t k1_out_row_stride(uint32_t nclasses) {
+  uint32_t s = k1_row_stride(nclasses) + 10;
+  if (((s / 2) & 1u) == 0) s += 2;
+  return s;
+}
+
+uint64_t k1_table_words16(const ScanDfa& d) {
+  return static_cast<uint64_t>(d.first_out_state) * k1_row_stride(d.t.nclasses) +
+         static_cast<uint64_t>(d.t.nstates - d.first_out_state) * k1_out_row_stride(d.t.nclasses);
+}
+
 size_t k1_lds_table_bytes(const ScanDfa& d) {
-  const size_t tab = (static_cast<size_t>(d.t.nstates) * k1_row_stride(d.t.nclasses) * 2 + 15) & ~size_t(15);
+  const size_t tab = (k1_table_words16(d) * 2 + 15) & ~size_t(15);
   const size_t nout = d.t.nstates - d.first_out_state;
   const size_t meta = (nout * 24 + d.out_ids.size() * 4 + 15) & ~size_t(15);   // OutMeta + (at most) every id listed
   return tab + 256 + meta;
 }
 
 bool k1_fits(const ScanDfa& d) {
-  return static_cast<uint64_t>(d.t.nstates) * k1_row_stride(d.t.nclasses) <= 65535 &&
-         kK1HitLdsBytes + k1_lds_table_bytes(d) <= kK1LdsBytes;
+  return k1_table_words16(d) <= 65535 && kK1HitLdsBytes + k1_lds_table_bytes(d) <= kK1LdsBytes;
 }
 
 bool literal_gate(const re::Node& ast, re::LitGate* out, bool* bounded, uint32_t* dmin, uint32_t* dmax) {
@@ -902,7 +986,10 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
     gi.gate_on_gpu = 1;
     for (const auto& kw : rule.keywords_lower) {
       if (kw.empty()) { gi.always_gate = 1; continue; }
-      if (!is_ascii(kw)) { gi.gate_on_gpu = 0; continue; }
+      // non-ASCII keywords, and short ones ("sk", "key": outputs at a few
+      // positions per KB of text, the most expensive part of K1), are
+      // evaluated on the host, only for files with candidates of the rule
+      if (!is_ascii(kw) || kw.size() <= kHostKeywordLen) { gi.gate_on_gpu = 0; continue; }
       auto it = kw_ids.find(kw);
       if (it == kw_ids.end()) {
         it = kw_ids.emplace(kw, static_cast<uint32_t>(pf->kw_text.size())).first;
@@ -968,7 +1055,7 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
         pf->host_anchors.push_back(ha);
       }
       rep += name + ": FULL (" + why + ") where present: item " + std::to_string(req.k) + ", " +
-             std::to_string(req.lits.size()) + " literal(s)\n";
+             std::to_string(req.lits.size()) + " literal(s) {" + seqs_str(req.lits) + "}\n";
       continue;
     }
     gi.mode = 0;
@@ -1002,7 +1089,7 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
     rep += name + ": anchored item " + std::to_string(ch.k) + ", " + std::to_string(ch.lits.size()) +
            " literal(s), offset [" + std::to_string(ch.dmin) + "," + std::to_string(ch.dmax) + "], verify " +
            std::to_string(pf->verify.back().nstates) + " states x " + std::to_string(pf->verify.back().nclasses) +
-           " classes, limit " + std::to_string(gi.verify_limit) + note + "\n";
+           " classes, limit " + std::to_string(gi.verify_limit) + note + " {" + seqs_str(ch.lits) + "}\n";
   }
   if (!make_groups(pf, pats, err)) return false;
   if (!make_scan_dfa(host, h0, hmaxb, &pf->host_scan, err)) return false;

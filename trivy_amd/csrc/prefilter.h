@@ -51,6 +51,10 @@ struct ScanDfa {
 constexpr uint32_t kK1LdsBytes = 160 * 1024;
 constexpr uint32_t kK1HitLdsBytes = 16 * 1024 * 4 + 16 * 4 + 16;
 uint32_t k1_row_stride(uint32_t nclasses);          // >= nclasses + 1, odd number of dwords
+// Output-state rows carry their output metadata inline after the spare slot:
+// keyword masks (8 x uint16) and the output list's begin / count (2 x uint16).
+uint32_t k1_out_row_stride(uint32_t nclasses);      // k1_row_stride + 10, rounded to an odd number of dwords
+uint64_t k1_table_words16(const ScanDfa& d);        // silent rows then output rows
 size_t k1_lds_table_bytes(const ScanDfa& d);        // scan table + class map + output metadata
 bool k1_fits(const ScanDfa& d);
 
