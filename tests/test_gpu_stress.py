@@ -82,3 +82,22 @@ def test_largest_k1_chunk_gpu(monkeypatch):
     assert stats["chunk_bytes"] == 32768
     assert got == want
     assert sum(len(w["Findings"]) for w in want) > 20
+
+
+@pytest.mark.parametrize("variant,abl,chunk", [("1", "0", "4096"), ("3", "464", "2048"), ("3", "16", "4096"),
+                                               ("3", "0", "8192")])
+def test_k1_variants_agree_gpu(monkeypatch, variant, abl, chunk):
+    # every K1 build whose layout bits keep results valid (v1; v3 with
+    # deferred outputs / rolled loop / 64-B lines / temporal loads) gives the
+    # default engine's result, and both equal the host confirmer's
+    c = synth.generate(24_000_000, seed=31, sizes="loguniform", plant_rate=3e-3)
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    assert S.Scanner(None).ScanBatch(args) == want
+    monkeypatch.setenv("TSG_K1_VARIANT", variant)
+    monkeypatch.setenv("TSG_K1_ABL", abl)
+    monkeypatch.setenv("TSG_K1_CHUNK", chunk)
+    got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
+    assert stats["chunk_bytes"] == int(chunk)
+    assert got == want
+    assert sum(len(w["Findings"]) for w in want) > 20

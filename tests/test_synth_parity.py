@@ -45,3 +45,45 @@ def test_fold_special_and_invalid_utf8_cpu():
     assert S.scan_host_reference(sc, args) == want
     assert S.scan_table_model(sc, args) == want
     assert sum(len(w["Findings"]) for w in want) >= 3
+
+
+def _short_kw_case(tmp_path):
+    # keywords of <= 3 bytes are gated on the host from the raw bytes
+    # (scanner.cpp keywords_match_raw); U+212A / U+0130 lower onto 'k' / 'i'
+    # (bytes.ToLower, scanner.go:174-186), so "KiT" and "kİt" hold
+    # the keyword "kit" while "KſT" does not
+    cfg = tmp_path / "s.yaml"
+    cfg.write_text(
+        "rules:\n"
+        "  - id: short-kw\n    category: general\n    title: short\n    severity: HIGH\n"
+        "    regex: 'tok_[a-z0-9]{8}'\n    keywords: [kit]\n"
+        "  - id: short-kw2\n    category: general\n    title: short2\n    severity: LOW\n"
+        "    regex: 'tik_[a-z0-9]{8}'\n    keywords: [zz, 'q.']\n")
+    files = [
+        ("a/1.txt", b"KIT tok_abcdefgh\n"),
+        ("a/2.txt", b"tok_abcdefgh but no keyword\n"),
+        ("a/3.txt", "KiT\ntok_abcdefgh\n".encode()),
+        ("a/4.txt", "kİt tok_abcdefgh\n".encode()),
+        ("a/5.txt", "KſT tok_abcdefgh\n".encode()),
+        ("a/6.txt", b"\xffki\xfft tok_abcdefgh q. tik_01234567\n"),
+        ("a/7.txt", b"Q. tik_01234567 ZZ tik_abcdefgh\n"),
+        ("a/8.txt", b"tik_01234567\n"),
+    ]
+    args = [S.ScanArgs(p, c) for p, c in files]
+    ref = so.Scanner(so.parse_config(str(cfg)))
+    want = [ref.scan(a.FilePath, a.Content) for a in args]
+    got = {a.FilePath for a, w in zip(args, want) if w["Findings"]}
+    assert got == {"a/1.txt", "a/3.txt", "a/4.txt", "a/6.txt", "a/7.txt"}
+    return S.Scanner(S.ParseConfig(str(cfg))), args, want
+
+
+def test_host_gated_short_keywords_cpu(tmp_path):
+    sc, args, want = _short_kw_case(tmp_path)
+    assert S.scan_host_reference(sc, args) == want
+    assert S.scan_table_model(sc, args) == want
+
+
+@pytest.mark.gpu
+def test_host_gated_short_keywords_gpu(tmp_path):
+    sc, args, want = _short_kw_case(tmp_path)
+    assert sc.ScanBatch(args) == want

@@ -96,8 +96,11 @@ class Engine {
   uint32_t chunk_ = 4096;               // K1 bytes per lane chunk (TSG_K1_CHUNK)
   int k1_streams_ = 1;                  // TSG_K1_CFG="threads,streams"
   uint32_t k1_threads_ = 1024;
-  int k1_variant_ = 1;                  // TSG_K1_VARIANT: 1 = tsg_k1_scan, 3 = tsg_k1_scan_v3
-  int k1_abl_ = 0;                      // TSG_K1_ABL: v3 measurement builds (kAbl* bits; results invalid)
+  int k1_variant_ = 3;                  // TSG_K1_VARIANT: 1 = tsg_k1_scan, 3 = tsg_k1_scan_v3
+  // TSG_K1_ABL: v3 build (kAbl* bits).  Default 464 = deferred outputs +
+  // rolled word loop + 64-byte lines + temporal loads (layout bits, results
+  // valid); the other bits are measurement builds whose results are invalid.
+  int k1_abl_ = 464;
   uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)
   double first_piece_ = 0.7;            // resident data: share of the first piece (TSG_FIRST_PIECE)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)

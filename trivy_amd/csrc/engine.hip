@@ -840,7 +840,8 @@ const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int a
       TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(17) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(26) TSG_K1_V3(27)
       TSG_K1_V3(31) TSG_K1_V3(32) TSG_K1_V3(48)
       TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(82) TSG_K1_V3(146) TSG_K1_V3(210) TSG_K1_V3(112) TSG_K1_V3(240)
-      TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(464) TSG_K1_V3(466)
+      TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466)
+      TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496)
 #undef TSG_K1_V3
       default: return nullptr;
     }

@@ -631,6 +631,61 @@ bool keywords_match(const Rule& r, const std::string& lower) {   // scanner.go:1
   return false;
 }
 
+// Case-insensitive (ASCII) search of a lowercase ASCII keyword in raw bytes.
+bool ascii_ci_find(const uint8_t* s, size_t n, const std::string& kw) {
+  const size_t m = kw.size();
+  if (m == 0) return true;
+  if (m > n) return false;
+  const uint8_t k0 = static_cast<uint8_t>(kw[0]);
+  const bool alpha0 = k0 >= 'a' && k0 <= 'z';
+  const uint8_t u0 = alpha0 ? static_cast<uint8_t>(k0 - 32) : k0;
+  for (size_t i = 0; i + m <= n; ++i) {
+    const uint8_t c = s[i];
+    if (c != k0 && c != u0) continue;
+    size_t j = 1;
+    for (; j < m; ++j) {
+      uint8_t b = s[i + j];
+      if (b >= 'A' && b <= 'Z') b = static_cast<uint8_t>(b + 32);
+      if (b != static_cast<uint8_t>(kw[j])) break;
+    }
+    if (j == m) return true;
+  }
+  return false;
+}
+
+// U+0130 (C4 B0) or U+212A (E2 84 AA): the only runes bytes.ToLower turns
+// into ASCII letters ('i', 'k')
+bool has_ascii_folding_rune(const uint8_t* s, size_t n) {
+  for (const uint8_t* p = s; (p = static_cast<const uint8_t*>(memchr(p, 0xC4, n - (p - s)))) != nullptr; ++p) {
+    if (p + 1 < s + n && p[1] == 0xB0) return true;
+  }
+  for (const uint8_t* p = s; (p = static_cast<const uint8_t*>(memchr(p, 0xE2, n - (p - s)))) != nullptr; ++p) {
+    if (p + 2 < s + n && p[1] == 0x84 && p[2] == 0xAA) return true;
+  }
+  return false;
+}
+
+// MatchKeywords (scanner.go:174-186) without the lowered copy where the raw
+// bytes decide it: ASCII bytes are single runes that bytes.ToLower keeps in
+// place (A-Z lowered), so an ASCII keyword found case-insensitively in the raw
+// bytes is in the lowered text; if it is not found, only U+0130 / U+212A can
+// still produce it, and files without them are decided too.  Everything else
+// (non-ASCII keywords, files with those runes) takes the exact lowered path.
+template <typename Lowered>
+bool keywords_match_raw(const Rule& r, const uint8_t* content, size_t len, Lowered&& lowered) {
+  if (r.keywords.empty()) return true;
+  bool undecided = false;
+  for (const auto& kw : r.keywords_lower) {
+    if (kw.empty()) return true;
+    bool ascii = true;
+    for (unsigned char c : kw) ascii &= c < 0x80;
+    if (!ascii) { undecided = true; continue; }
+    if (ascii_ci_find(content, len, kw)) return true;
+  }
+  if (!undecided && !has_ascii_folding_rune(content, len)) return false;
+  return keywords_match(r, lowered());
+}
+
 }  // namespace
 
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
@@ -659,7 +714,9 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
     if (rule.path && !rule.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) continue;
     if (allow_path(rule.allow_rules, path)) continue;
     if (kind == kPlanSkip) continue;
-    if ((kind == kPlanFull || kind == kPlanCandHostGate) && !keywords_match(rule, lowered())) continue;
+    // a host-gated rule matches only at GPU candidate starts: none, no match
+    if (kind == kPlanCandHostGate && (!starts || starts->empty())) continue;
+    if ((kind == kPlanFull || kind == kPlanCandHostGate) && !keywords_match_raw(rule, content, len, lowered)) continue;
     if (kind == kPlanNoMatch) continue;
     locs.clear();
     static const std::vector<uint64_t> kEmpty;
