@@ -8,9 +8,9 @@ scanned with the builtin rules.
 
 One step = SURVEY.md 8(d)'s wall clock: the packed batch in PINNED HOST
 memory -> tsg_scan_batch -> assembled types.Secret results for every file.
-Inside, the engine streams the batch to HBM in 1 GB segments (upload of
-segment k+1 on a copy stream overlapping K1/K2 of segment k and the host
-confirmation of segment k-1), so `value` includes PCIe.  Reported beside it,
+Inside, the engine streams the batch to HBM in 4 GiB segments ending in a
+512 MiB one (upload of segment k+1 on a copy stream overlapping K1/K2 of
+segment k and the host confirmation of segment k-1), so `value` includes PCIe.  Reported beside it,
 never as `value`: the HBM-resident rate (corpus already in HBM), the
 host-feed ceiling (the same segmented upload with no kernels) and the host
 content-preparation rate (tsg_prepare_batch).
@@ -116,7 +116,7 @@ class PinnedBatch:
 
 def _segment_bytes():
     v = os.environ.get("TSG_SEGMENT_BYTES")
-    return int(v) if v and int(v) >= 4096 else 1 << 30
+    return int(v) if v and int(v) >= 4096 else 4 << 30
 
 
 def main():
@@ -318,9 +318,11 @@ def main():
             "traffic_source": traffic_src,
             "algorithmic_bytes": "1 byte read per content byte (SURVEY 8d); scan-DFA groups: %d" % groups,
             "launches_per_step": launches,
-            "bytes_per_launch": round(nbytes / segments),
+            "bytes_per_launch": round(nbytes / launches * groups),
             "avg_launch_ms": round(k1_ms / launches, 4),
-            "per_launch_gbps": round(nbytes / segments / (k1_ms / launches / 1e3) / 1e9, 2),
+            "per_launch_gbps": round(nbytes / launches * groups / (k1_ms / launches / 1e3) / 1e9, 2),
+            "note": "mean over the step's K1 launches (segments of unequal size; each segment is read once "
+                    "per scan-DFA group, the bytes counted once as SURVEY 8d prescribes)",
         },
         "link": {"bound": "pcie", "achieved": round(nbytes / (h2d_ms / 1e3) / 1e9, 2), "peak": PCIE_PEAK_GBPS,
                  "unit": "GB/s", "note": "H2D copy time of the step's segments (copy-stream HIP events)"},

@@ -124,7 +124,8 @@ int tsg_go_json_string(const uint8_t* s, size_t n, int escape_html, char** out, 
 int tsg_device_count(void);
 /* device_mask: bit d selects HIP device d (0 = every visible device).  With
  * several devices one tsg_scan_batch call is spread over all of them: the
- * batch is cut into segments (TSG_SEGMENT_BYTES, default 512 MB) that each
+ * batch is cut into segments (TSG_SEGMENT_BYTES, default 4 GiB, the last one
+ * TSG_SEGMENT_TAIL, default 512 MiB) that each
  * device's driver thread pulls from a shared queue. */
 int tsg_engine_create(const tsg_ruleset* rs, uint64_t device_mask, tsg_engine** out);
 void tsg_engine_destroy(tsg_engine* e);

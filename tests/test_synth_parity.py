@@ -87,3 +87,52 @@ def test_host_gated_short_keywords_cpu(tmp_path):
 def test_host_gated_short_keywords_gpu(tmp_path):
     sc, args, want = _short_kw_case(tmp_path)
     assert sc.ScanBatch(args) == want
+
+
+def _reverse_anchor_files():
+    # rules whose best literal sits behind an unbounded prefix are
+    # reverse-anchored (prefilter mode 4): jwt-token on ".ey" after
+    # ey[a-zA-Z0-9]{17,}, private-key on "PRIVAT", lob-* on "live_"/"test_";
+    # cases around the backward walk: several "ey" in one run, the 17-char
+    # minimum, runs past the walk limit (full-file fallback), file starts
+    t = "eyJhbGciOiJIUzI1NiJ9.eyJzdWIiOiIxMjM0NTY3ODkwIn0.SflKxwRJSMeKKF2QT4fwpMeJf36POk6yJV_adQssw5c"
+    k = "-----BEGIN RSA PRIVATE KEY-----\nMIIEpAIBAAKCAQEA" + "q" * 64 + "\n-----END RSA PRIVATE KEY-----\n"
+    return [
+        ("r/jwt1.txt", ("x = '%s'\n" % t).encode()),
+        ("r/jwt2.txt", t.encode()),                                   # match at the file start
+        ("r/jwt3.txt", ("eyey" + t + "\n").encode()),                 # several starts in one run
+        ("r/jwt4.txt", b"ey" + b"a" * 17 + b".eyJ" + b"b" * 17 + b"." + b"c" * 10 + b"\n"),
+        ("r/jwt5.txt", b"ey" + b"a" * 16 + b".ey" + b"b" * 17 + b".\n"),      # prefix one short
+        ("r/jwt6.txt", b"ey" + b"z" * 5000 + b".eyJ" + b"b" * 20 + b".x\n"),    # walk limit: host fallback
+        ("r/jwt7.txt", b"Q" * 6000 + b".eyJ" + b"c" * 30 + b".\n"),            # limit, no match
+        ("r/jwt8.txt", ("a.eyJ b.eyJ ey%s.eyJ%s.eyJ\n" % ("x" * 17, "y" * 17)).encode()),
+        ("r/key1.txt", k.encode()),
+        ("r/key2.txt", ("  " + k.replace("RSA ", "")).encode()),
+        ("r/key3.txt", ("-----BEGIN " + "A" * 100 + "PRIVATE KEY-----\n" + "b" * 70 + "\n-----END x PRIVATE KEY-----").encode()),
+        ("r/key4.txt", b"PRIVATE KEY PRIVATE KEY -----BEGIN\n"),
+        ("r/lob.txt", b"lob_key = 'live_0123456789abcdef0123456789abcdef012'\nLOB: \"test_pub_0123456789abcdef0123456789abcde\"\n"),
+    ]
+
+
+def test_reverse_anchors_cpu():
+    files = _reverse_anchor_files()
+    args = [S.ScanArgs(p, c) for p, c in files]
+    ref = so.Scanner(None)
+    want = [ref.scan(a.FilePath, a.Content) for a in args]
+    sc = S.Scanner(None)
+    rep = S.prefilter_report(sc)
+    assert "jwt-token: reverse-anchored" in rep and "private-key: reverse-anchored" in rep
+    assert S.scan_host_reference(sc, args) == want
+    assert S.scan_table_model(sc, args) == want
+    assert {a.FilePath for a, w in zip(args, want) if w["Findings"]} >= {
+        "r/jwt1.txt", "r/jwt2.txt", "r/jwt3.txt", "r/jwt4.txt", "r/jwt6.txt", "r/jwt8.txt", "r/key1.txt",
+        "r/key2.txt", "r/lob.txt"}
+
+
+@pytest.mark.gpu
+def test_reverse_anchors_gpu():
+    files = _reverse_anchor_files()
+    args = [S.ScanArgs(p, c) for p, c in files]
+    ref = so.Scanner(None)
+    want = [ref.scan(a.FilePath, a.Content) for a in args]
+    assert S.Scanner(None).ScanBatch(args) == want

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                    help="keep the GPU busy (torch elementwise kernels) this long right before each K1/K2 run")
     ap.add_argument("--variants", default="",
                     help="comma list of VARIANT[:ABL[:CHUNK]] (TSG_K1_VARIANT / TSG_K1_ABL / TSG_K1_CHUNK), "
                          "one engine each")
@@ -65,7 +67,15 @@ def probe(args, sc, c, d, L):
     from trivy_amd import _lib
     eng = sc.engine()
     rows = []
+    import torch
+    busy = torch.ones(1 << 26, device="cuda:0") if args.prewarm_ms > 0 else None
     for r in range(args.reps + 1):
+        if busy is not None:                      # clocks up: the GPU was busy until just now
+            t1 = time.perf_counter()
+            while (time.perf_counter() - t1) * 1e3 < args.prewarm_ms:
+                for _ in range(8):
+                    busy.mul_(1.0000001)
+                torch.cuda.synchronize()
         res = ctypes.c_void_p()
         t0 = time.perf_counter()
         _lib.check(L.tsg_prefilter_resident(eng, ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,

@@ -93,7 +93,7 @@ class Engine {
   std::vector<std::unique_ptr<CallCtx>> calls_;
   std::vector<CallCtx*> free_calls_;
   // tuning (TSG_* environment knobs, read once at create)
-  uint32_t chunk_ = 4096;               // K1 bytes per lane chunk (TSG_K1_CHUNK)
+  uint32_t chunk_ = 0;                  // K1 bytes per lane chunk (TSG_K1_CHUNK); 0 = by launch size (k1_chunk_for)
   int k1_streams_ = 1;                  // TSG_K1_CFG="threads,streams"
   uint32_t k1_threads_ = 1024;
   int k1_variant_ = 3;                  // TSG_K1_VARIANT: 1 = tsg_k1_scan, 3 = tsg_k1_scan_v3
@@ -104,7 +104,8 @@ class Engine {
   uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)
   double first_piece_ = 0.7;            // resident data: share of the first piece (TSG_FIRST_PIECE)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
-  uint64_t segment_ = 1ull << 30;       // uploaded data: bytes per pipeline segment (TSG_SEGMENT_BYTES);
+  uint64_t segment_tail_ = 512ull << 20; // uploaded data: the last segment's size (TSG_SEGMENT_TAIL)
+  uint64_t segment_ = 4ull << 30;       // uploaded data: bytes per pipeline segment (TSG_SEGMENT_BYTES);
                                         // 1 GB = one full K1 round (256 CUs x 1024 lanes x 4 KiB chunks)
 };
 

@@ -40,7 +40,7 @@ namespace {
 constexpr uint32_t kLdsBytes = 160 * 1024;     // LDS per CU
 
 struct AnchorDev { uint32_t rule, min_len, max_len, dmin, dmax; };
-struct RuleDev { uint32_t mode, gate_on_gpu, always_gate, kw_begin, kw_count, verify_dfa, verify_limit, pad; };
+struct RuleDev { uint32_t mode, gate_on_gpu, always_gate, kw_begin, kw_count, verify_dfa, verify_limit, rev_dfa; };
 struct VDfaDev { uint32_t next_off, acc_off, cls_off, nclasses, dead, pad0, pad1, pad2; };
 struct CandDev { uint32_t file, rule; unsigned long long start; };
 
@@ -65,7 +65,7 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
   return f;
 }
 
-constexpr uint32_t kWaveHits = 1024;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
+constexpr uint32_t kWaveHits = kK1WaveHits;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
 constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [2] overflow, [4 + g] v3 items of group g
@@ -526,14 +526,21 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     }
     const long long fstart = static_cast<long long>(offsets[f]);
     const long long fend = static_cast<long long>(offsets[f + 1]);
-    long long hi = static_cast<long long>(q) + 1 - an.min_len - an.dmin;
-    long long lo = static_cast<long long>(q) + 1 - an.max_len - an.dmax;
-    if (lo < fstart) lo = fstart;
     const VDfaDev d = vd[r.verify_dfa];
     const uint16_t* nx = v_next + d.next_off;
     const uint8_t* acc = v_acc + d.acc_off;
     const uint8_t* cl = v_cls + d.cls_off;
-    for (long long s = lo; s <= hi; ++s) {
+    auto emit = [&](unsigned long long start) {
+      const unsigned int idx = atomicAdd(&counters[1], 1u);
+      if (idx < cand_cap) {
+        cands[idx].file = f;
+        cands[idx].rule = an.rule;
+        cands[idx].start = start;
+      }
+    };
+    // anchored verify DFA from s: does a prefix of the text from s lie in the
+    // rule's relaxed language?
+    auto verify = [&](long long s) {
       uint32_t st = 0;
       bool ok = acc[0] != 0;
       long long p = s;
@@ -544,14 +551,31 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
         else if (st == d.dead) break;
       }
       if (!ok && st != d.dead && p < fend && p >= lim) ok = true;   // gave up: conservative
-      if (ok) {
-        const unsigned int idx = atomicAdd(&counters[1], 1u);
-        if (idx < cand_cap) {
-          cands[idx].file = f;
-          cands[idx].rule = an.rule;
-          cands[idx].start = static_cast<unsigned long long>(s - fstart);
-        }
+      return ok;
+    };
+    if (r.mode == 4) {
+      // reverse-anchored: walk the reverse DFA backwards from the hit's last
+      // byte; every accepting position may start a match and is verified
+      // forwards.  A walk still alive after kRevLimit bytes gives up: the
+      // host evaluates the rule on the whole file (kFullScanStart).
+      const VDfaDev rd = vd[r.rev_dfa];
+      const uint16_t* rnx = v_next + rd.next_off;
+      const uint8_t* racc = v_acc + rd.acc_off;
+      const uint8_t* rcl = v_cls + rd.cls_off;
+      uint32_t st = 0;
+      for (long long p = static_cast<long long>(q); p >= fstart; --p) {
+        if (static_cast<long long>(q) - p >= static_cast<long long>(kRevLimit)) { emit(kFullScanStart); break; }
+        st = rnx[st * rd.nclasses + rcl[data[p]]];
+        if (st == rd.dead) break;
+        if (racc[st] && verify(p)) emit(static_cast<unsigned long long>(p - fstart));
       }
+      continue;
+    }
+    long long hi = static_cast<long long>(q) + 1 - an.min_len - an.dmin;
+    long long lo = static_cast<long long>(q) + 1 - an.max_len - an.dmax;
+    if (lo < fstart) lo = fstart;
+    for (long long s = lo; s <= hi; ++s) {
+      if (verify(s)) emit(static_cast<unsigned long long>(s - fstart));
     }
   }
 }
@@ -869,6 +893,16 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
   return true;
 }
 
+// Default K1 chunk for a launch of `bytes`: about a million lane chunks per
+// launch, 1-4 KiB.  Measured on MI355X (r2g, v3 K1): a 1 GB launch 0.52 ms
+// at 1 KiB vs 0.56 at 4 KiB (shorter wave items, shorter tail); 2 GB best at
+// 2 KiB; 4 GB and more best at 4 KiB (less warm-up per byte).
+uint32_t k1_chunk_for(uint64_t bytes) {
+  uint32_t c = 1024;
+  while (c < 4096 && static_cast<uint64_t>(c) * (1u << 20) < bytes) c <<= 1;
+  return c;
+}
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -1071,7 +1105,7 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
   std::vector<AnchorDev> an;
   for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
   std::vector<RuleDev> rd;
-  for (const auto& r : pf.rules) rd.push_back({r.mode, r.gate_on_gpu, r.always_gate, r.kw_begin, r.kw_count, r.verify_dfa, r.verify_limit, 0});
+  for (const auto& r : pf.rules) rd.push_back({r.mode, r.gate_on_gpu, r.always_gate, r.kw_begin, r.kw_count, r.verify_dfa, r.verify_limit, r.rev_dfa});
   std::vector<VDfaDev> vd;
   std::vector<uint16_t> vn;
   std::vector<uint8_t> va, vc;
@@ -1184,6 +1218,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const long long v = std::atoll(c);
     if (v >= 4096) e->segment_ = static_cast<uint64_t>(v);
   }
+  if (const char* c = std::getenv("TSG_SEGMENT_TAIL")) {
+    const long long v = std::atoll(c);
+    if (v >= 0) e->segment_tail_ = static_cast<uint64_t>(v);
+  }
   if (const char* cfg = std::getenv("TSG_K1_CFG")) {
     unsigned t = 0, k = 0;
     if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k))) {
@@ -1280,7 +1318,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
-  const uint32_t kChunk = chunk_;
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total);
   if (kChunk > k1_max_chunk(k1_streams_) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
@@ -1580,7 +1618,9 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
           if (rc.starts.empty() || rc.starts.back() != sorted[k].start) rc.starts.push_back(sorted[k].start);
           ++k;
         }
-        plan.kind[r] = pf_.rules[r].mode == 3 ? kPlanFull
+        // mode 3 presence candidates, and a mode-4 walk that gave up
+        // (kFullScanStart sorts last): the rule in full on the host
+        plan.kind[r] = pf_.rules[r].mode == 3 || rc.starts.back() == kFullScanStart ? kPlanFull
                      : pf_.rules[r].gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
         plan.cands.push_back(std::move(rc));
       }
@@ -1665,8 +1705,15 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       }
     } else {
       for (uint32_t f = 0; f < in.nfiles;) {
-        // next cut: the first file boundary at or past segment_ bytes from here
-        const uint64_t target = in.offsets[f] + segment_;
+        // next cut: the first file boundary at or past segment_ bytes from
+        // here; the batch ends in a short segment (segment_tail_), so the
+        // kernels and confirmation left after the last upload are short while
+        // the other K1 launches stay large
+        const uint64_t rest = total - in.offsets[f];
+        uint64_t target;
+        if (rest > segment_ + segment_tail_) target = in.offsets[f] + segment_;
+        else if (segment_tail_ > 0 && rest > 2 * segment_tail_) target = total - segment_tail_;
+        else break;
         uint32_t g = static_cast<uint32_t>(std::lower_bound(in.offsets + f, in.offsets + in.nfiles, target) - in.offsets);
         if (g <= f) g = f + 1;
         if (g >= in.nfiles) break;

@@ -38,6 +38,7 @@ struct NState {
 };
 
 struct Nfa {
+  bool rev = false;                         // build the reversed language (reverse anchors, mode 4)
   std::vector<NState> st;
   std::vector<Bits> sets;
   std::map<std::string, int> set_index;
@@ -53,7 +54,8 @@ struct Nfa {
     return id;
   }
   void edge(int a, const Bits& b, int to) { st[a].edges.push_back({set_id(b), to}); }
-  void byte_chain(int from, const std::string& bytes, int to) {
+  void byte_chain(int from, const std::string& fwd, int to) {
+    const std::string bytes = rev ? std::string(fwd.rbegin(), fwd.rend()) : fwd;
     int cur = from;
     for (size_t i = 0; i < bytes.size(); ++i) {
       int nx = (i + 1 == bytes.size()) ? to : add();
@@ -168,7 +170,8 @@ int build(Nfa* nfa, const Node& n, int from) {
       return build(nfa, *n.sub[0], from);
     case Op::Concat: {
       int cur = from;
-      for (const auto& s : n.sub) cur = build(nfa, *s, cur);
+      if (nfa->rev) for (size_t i = n.sub.size(); i-- > 0;) cur = build(nfa, *n.sub[i], cur);
+      else for (const auto& s : n.sub) cur = build(nfa, *s, cur);
       return cur;
     }
     case Op::Alternate: {
@@ -339,6 +342,11 @@ int ext_units() {
   static const int n = [] { const char* e = std::getenv("TSG_ANCHOR_EXT"); return e ? std::atoi(e) : 0; }();
   return n;
 }
+// Reverse anchors (mode 4) on unless TSG_REVERSE_ANCHORS=0.
+bool ext_rev() {
+  static const bool on = [] { const char* e = std::getenv("TSG_REVERSE_ANCHORS"); return !e || std::atoi(e) != 0; }();
+  return on;
+}
 SeqSet prefix_of_items(const std::vector<const Node*>& items, size_t k, bool ext = false);
 
 SeqSet prefix_set(const Node& n, bool ext = false) {
@@ -480,7 +488,8 @@ struct RawDfa {
 
 // Subset construction.  `loop_start`: scan DFA (the start closure is re-added
 // after every byte).  `absorb_accept`: verify DFA (accepting subsets stop).
-bool determinize(const Nfa& nfa, int start, bool loop_start, int accept_state, uint32_t cap, RawDfa* out) {
+bool determinize(const Nfa& nfa, int start, bool loop_start, int accept_state, uint32_t cap, RawDfa* out,
+                 bool absorb_accept = true) {
   out->cm = byte_classes(nfa);
   const uint32_t C = out->cm.n;
   std::vector<int> s0{start};
@@ -495,7 +504,7 @@ bool determinize(const Nfa& nfa, int start, bool loop_start, int accept_state, u
     if (out->subsets.size() > cap) return false;
     std::vector<uint32_t> row(C, 0);
     const std::vector<int> cur = out->subsets[i];
-    bool acc = accept_state >= 0 && std::binary_search(cur.begin(), cur.end(), accept_state);
+    bool acc = absorb_accept && accept_state >= 0 && std::binary_search(cur.begin(), cur.end(), accept_state);
     for (uint32_t c = 0; c < C; ++c) {
       std::vector<int> nx;
       if (acc) { row[c] = static_cast<uint32_t>(i); continue; }
@@ -598,7 +607,8 @@ struct AnchorChoice {
   size_t k = 0;
   SeqSet lits;
   SeqSet raw;
-  uint32_t dmin = 0, dmax = 0;
+  uint32_t dmin = 0, dmax = 0;         // dmax = kInf: unbounded prefix
+  double score = -1;
 };
 
 // bounded: the literal's offset from the match start must be bounded (a
@@ -656,6 +666,7 @@ AnchorChoice choose_anchor(const std::vector<const Node*>& items, bool bounded =
     phi = (phi >= kInf || hi >= kInf) ? kInf : std::min(phi + hi, kInf);
   }
   if (best.ok && best_score < 1.5) best.ok = false;   // a 1-unit anchor is useless
+  best.score = best_score;
   return best;
 }
 
@@ -710,6 +721,46 @@ bool build_verify(const std::vector<const Node*>& items, size_t min_items, DfaTa
     return true;
   }
   return false;
+}
+
+// Reverse DFA of a mode-4 anchor: the anchor literals (raw units, cut to the
+// length of their scan form, which is where a K1 hit ends) preceded by the
+// relaxed prefix items[0..k), all read BACKWARDS from the hit's last byte.
+// After consuming the byte at p the DFA is accepting iff text[p..hit] is in
+// relaxed(prefix) . literal, i.e. p may start a match; accepting states are
+// not absorbing, so one walk visits every possible start until the DFA dies.
+bool build_reverse(const std::vector<const Node*>& items, size_t k, const SeqSet& raw, DfaTable* out) {
+  Nfa nfa;
+  nfa.rev = true;
+  const int start = nfa.add();
+  const int lit_end = nfa.add();
+  for (const Seq& r : raw) {
+    const size_t n = scan_form(r).size();
+    if (n == 0) return false;
+    int cur = start;
+    for (size_t i = n; i-- > 0;) {
+      const int nx = i == 0 ? lit_end : nfa.add();
+      for (const auto& alt : r[i]) nfa.byte_chain(cur, alt, nx);
+      cur = nx;
+    }
+  }
+  int cur = lit_end;
+  for (size_t i = k; i-- > 0;) cur = build(&nfa, *items[i], cur);
+  const int acc = nfa.add();
+  nfa.eps(cur, acc);
+  nfa.st[acc].out = 0;
+  RawDfa rd;
+  if (!determinize(nfa, start, false, acc, kVerifyStateCap, &rd, /*absorb_accept=*/false)) return false;
+  bool has_dead = false;
+  for (const auto& sub : rd.subsets) if (sub.empty()) has_dead = true;
+  if (!has_dead) {
+    rd.subsets.push_back({});
+    rd.next.push_back(std::vector<uint32_t>(rd.cm.n, static_cast<uint32_t>(rd.subsets.size() - 1)));
+  }
+  std::vector<uint32_t> order(rd.subsets.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
+  *out = to_table(rd, order, acc);
+  return true;
 }
 
 bool make_scan_dfa(const Nfa& nfa, int s0, uint32_t maxb, ScanDfa* out, std::string* err) {
@@ -779,10 +830,7 @@ void two_pass(const Prefilter& pf, const ScanDfa* dfas, size_t ndfa, const std::
       continue;
     }
     const DfaTable& v = pf.verify[gi.verify_dfa];
-    long hi = static_cast<long>(h.end) + 1 - a.min_len - a.dmin;
-    long lo = static_cast<long>(h.end) + 1 - a.max_len - a.dmax;
-    if (lo < 0) lo = 0;
-    for (long st = lo; st <= hi; ++st) {
+    auto verify_from = [&](size_t st) {
       uint32_t q = 0;
       bool emit = v.accept[0];
       size_t p = st;
@@ -792,7 +840,26 @@ void two_pass(const Prefilter& pf, const ScanDfa* dfas, size_t ndfa, const std::
         else if (q == v.dead) break;
       }
       if (!emit && q != v.dead && p < len && p - st >= gi.verify_limit) emit = true;   // gave up: conservative
-      if (emit) (*cand)[a.rule].push_back(static_cast<uint64_t>(st));
+      return emit;
+    };
+    if (gi.mode == 4) {
+      // backward walk of the reverse DFA from the hit's last byte: every
+      // accepting position may start a match (then verified forwards)
+      const DfaTable& rv = pf.verify[gi.rev_dfa];
+      uint32_t q = 0;
+      for (size_t p = h.end + 1; p-- > 0;) {
+        if (h.end - p >= kRevLimit) { (*cand)[a.rule].push_back(kFullScanStart); break; }
+        q = rv.next[static_cast<size_t>(q) * rv.nclasses + rv.byte_class[data[p]]];
+        if (q == rv.dead) break;
+        if (rv.accept[q] && verify_from(p)) (*cand)[a.rule].push_back(static_cast<uint64_t>(p));
+      }
+      continue;
+    }
+    long hi = static_cast<long>(h.end) + 1 - a.min_len - a.dmin;
+    long lo = static_cast<long>(h.end) + 1 - a.max_len - a.dmax;
+    if (lo < 0) lo = 0;
+    for (long st = lo; st <= hi; ++st) {
+      if (verify_from(static_cast<size_t>(st))) (*cand)[a.rule].push_back(static_cast<uint64_t>(st));
     }
   }
   for (auto& c : *cand) {
@@ -1023,8 +1090,20 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
     flatten(*rx->ast(), &items);
     AnchorChoice ch = rx->nullable() ? AnchorChoice() : choose_anchor(items);
     std::string note;
-    DfaTable vt;
+    DfaTable vt, rt;
     uint32_t limit = 0;
+    // a far better literal behind an unbounded (or long) prefix: reverse-anchored
+    // (mode 4), its prefix walked backwards from each hit (jwt-token's `.ey`
+    // after `ey[a-zA-Z0-9]{17,}` instead of `ey` itself)
+    bool reverse = false;
+    if (!rx->nullable() && ext_rev()) {
+      AnchorChoice rv = choose_anchor(items, false);
+      if (rv.ok && rv.dmax > kMaxPrefixBytes && (!ch.ok || rv.score >= ch.score + 0.5) &&
+          build_reverse(items, rv.k, rv.raw, &rt)) {
+        ch = rv;
+        reverse = true;
+      }
+    }
     const char* why = !ch.ok ? "no bounded anchor" : nullptr;
     if (!why && !build_verify(items, ch.k + 1, &vt, &limit, &note)) why = "verify DFA too large";
     if (why) {
@@ -1058,10 +1137,15 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
              std::to_string(req.lits.size()) + " literal(s) {" + seqs_str(req.lits) + "}\n";
       continue;
     }
-    gi.mode = 0;
+    gi.mode = reverse ? 4 : 0;
     gi.verify_dfa = static_cast<uint32_t>(pf->verify.size());
     gi.verify_limit = std::max<uint32_t>(limit, 1);
     pf->verify.push_back(std::move(vt));
+    if (reverse) {
+      gi.rev_dfa = static_cast<uint32_t>(pf->verify.size());
+      note += " reverse " + std::to_string(rt.nstates) + " states x " + std::to_string(rt.nclasses) + " classes";
+      pf->verify.push_back(std::move(rt));
+    }
     for (const auto& s : ch.lits) {
       AnchorInfo a;
       a.rule = static_cast<uint32_t>(r);
@@ -1086,9 +1170,11 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
       }
       pf->host_anchors.push_back(ha);
     }
-    rep += name + ": anchored item " + std::to_string(ch.k) + ", " + std::to_string(ch.lits.size()) +
-           " literal(s), offset [" + std::to_string(ch.dmin) + "," + std::to_string(ch.dmax) + "], verify " +
-           std::to_string(pf->verify.back().nstates) + " states x " + std::to_string(pf->verify.back().nclasses) +
+    rep += name + (reverse ? ": reverse-anchored item " : ": anchored item ") + std::to_string(ch.k) + ", " +
+           std::to_string(ch.lits.size()) + " literal(s), offset [" + std::to_string(ch.dmin) + "," +
+           (ch.dmax >= kInf ? std::string("inf") : std::to_string(ch.dmax)) + "], verify " +
+           std::to_string(pf->verify[gi.verify_dfa].nstates) + " states x " +
+           std::to_string(pf->verify[gi.verify_dfa].nclasses) +
            " classes, limit " + std::to_string(gi.verify_limit) + note + " {" + seqs_str(ch.lits) + "}\n";
   }
   if (!make_groups(pf, pats, err)) return false;
@@ -1128,8 +1214,10 @@ void plan_from_candidates(const Prefilter& pf, std::vector<std::vector<uint64_t>
   plan->cands.clear();
   for (size_t k = 0; k < nr; ++k) {
     const RuleGpuInfo& gi = pf.rules[k];
-    if (gi.mode == 1 || (gi.mode == 3 && !(*cands)[k].empty())) plan->kind[k] = kPlanFull;
-    else if (gi.mode == 0 && !(*cands)[k].empty()) {
+    if (gi.mode == 1 || (gi.mode == 3 && !(*cands)[k].empty()) ||
+        (gi.mode == 4 && !(*cands)[k].empty() && (*cands)[k].back() == kFullScanStart)) {
+      plan->kind[k] = kPlanFull;
+    } else if ((gi.mode == 0 || gi.mode == 4) && !(*cands)[k].empty()) {
       plan->kind[k] = gi.gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
       plan->cands.push_back({static_cast<uint32_t>(k), std::move((*cands)[k])});
     }

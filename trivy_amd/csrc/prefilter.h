@@ -49,7 +49,8 @@ struct ScanDfa {
 // transitions are uint16 row offsets (state * stride), so a GPU scan DFA
 // must satisfy nstates * stride <= 65535 and fit the LDS left over.
 constexpr uint32_t kK1LdsBytes = 160 * 1024;
-constexpr uint32_t kK1HitLdsBytes = 16 * 1024 * 4 + 16 * 4 + 16;
+constexpr uint32_t kK1WaveHits = 512;    // per-wave LDS hit buffer entries (K1); further hits go straight to global
+constexpr uint32_t kK1HitLdsBytes = 16 * kK1WaveHits * 4 + 16 * 4 + 16;
 uint32_t k1_row_stride(uint32_t nclasses);          // >= nclasses + 1, odd number of dwords
 // Output-state rows carry their output metadata inline after the spare slot:
 // keyword masks (8 x uint16) and the output list's begin / count (2 x uint16).
@@ -66,13 +67,22 @@ struct AnchorInfo {                    // one literal of one rule
 
 struct RuleGpuInfo {
   uint8_t mode;                        // 0 = anchored (GPU candidates), 1 = FULL (host), 2 = no regex,
-                                       // 3 = FULL in files containing a required literal (presence anchors)
+                                       // 3 = FULL in files containing a required literal (presence anchors),
+                                       // 4 = reverse-anchored: candidate starts from a backward walk of
+                                       //     the reverse DFA `rev_dfa` from the hit (unbounded prefixes)
   uint8_t gate_on_gpu;                 // keyword gate exact on GPU (ASCII keywords)
   uint8_t always_gate;                 // no keywords (or an empty keyword): gate always true
   uint32_t kw_begin, kw_count;         // keyword ids in Prefilter::rule_kw
   uint32_t verify_dfa;                 // index into verify
   uint32_t verify_limit;               // bytes scanned before giving up (emit conservatively)
+  uint32_t rev_dfa = 0;                // mode 4: index into verify of the reverse DFA
 };
+
+// Mode 4: a backward walk longer than this many bytes that is still alive
+// gives up and asks for the rule in full on the host (candidate start
+// kFullScanStart).
+constexpr uint32_t kRevLimit = 4096;
+constexpr uint64_t kFullScanStart = ~0ull;
 
 struct Prefilter {
   uint32_t nkw = 0;                    // distinct keyword patterns
