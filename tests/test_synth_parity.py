@@ -121,7 +121,7 @@ def test_reverse_anchors_cpu():
     want = [ref.scan(a.FilePath, a.Content) for a in args]
     sc = S.Scanner(None)
     rep = S.prefilter_report(sc)
-    assert "jwt-token: reverse-anchored" in rep and "private-key: reverse-anchored" in rep
+    assert "jwt-token: reverse-anchored" in rep and "lob-api-key: reverse-anchored" in rep
     assert S.scan_host_reference(sc, args) == want
     assert S.scan_table_model(sc, args) == want
     assert {a.FilePath for a, w in zip(args, want) if w["Findings"]} >= {

@@ -1710,9 +1710,10 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         // kernels and confirmation left after the last upload are short while
         // the other K1 launches stay large
         const uint64_t rest = total - in.offsets[f];
+        const uint64_t tail = std::min(segment_tail_, segment_ / 8);
         uint64_t target;
-        if (rest > segment_ + segment_tail_) target = in.offsets[f] + segment_;
-        else if (segment_tail_ > 0 && rest > 2 * segment_tail_) target = total - segment_tail_;
+        if (rest > segment_ + tail) target = in.offsets[f] + segment_;
+        else if (tail > 0 && rest > 2 * tail) target = total - tail;
         else break;
         uint32_t g = static_cast<uint32_t>(std::lower_bound(in.offsets + f, in.offsets + in.nfiles, target) - in.offsets);
         if (g <= f) g = f + 1;

@@ -574,20 +574,35 @@ Seq keyword_seq(const std::string& kw, bool variants) {
   return s;
 }
 
-// Scan-DFA form of an anchor literal: every unit case-folded over ASCII (a
-// superset; the verify DFA re-checks case).  Non-ASCII alternatives that are
+// Anchor literals of at most TSG_EXACT_ANCHORS units (default 3; 0 = none)
+// keep the regex's own case: a case-sensitive `SK` or `pk.` then fires only on
+// that case, while (?i) units already list both cases.  Longer ones are
+// case-folded (a superset; the verify DFA re-checks case).
+int exact_anchors() {
+  static const int n = [] { const char* e = std::getenv("TSG_EXACT_ANCHORS"); return e ? std::atoi(e) : 3; }();
+  return n;
+}
+
+// Scan-DFA form of an anchor literal: the unit's ASCII alternatives (or, with
+// exact_anchors() off, every unit case-folded over ASCII: a superset; the
+// verify DFA re-checks case).  Non-ASCII alternatives that are
 // the fold images of ASCII letters (U+212A, U+017F) are dropped -- files that
 // contain them are flagged by K1 and scanned exactly on the host.  The literal
 // is cut before any unit with another non-ASCII alternative.
 Seq scan_form(const Seq& lit, bool keep_special = false) {
   Seq out;
+  // exact case only for short literals: they fire most often, and folded
+  // long literals share their trie states with the (folded) keywords
+  const int ex = exact_anchors();
+  const bool exact = ex != 0 && (ex >= 99 || static_cast<int>(lit.size()) <= ex);
   for (const Unit& u : lit) {
     Unit f;
     bool ok = true;
     for (const auto& alt : u) {
       if (alt == "\xE2\x84\xAA" || alt == "\xC5\xBF") { if (keep_special) f.push_back(alt); continue; }
       if (alt.size() != 1 || static_cast<unsigned char>(alt[0]) >= 0x80) { ok = false; break; }
-      for (const auto& x : folded_unit(static_cast<unsigned char>(alt[0]))) f.push_back(x);
+      if (exact) f.push_back(alt);
+      else for (const auto& x : folded_unit(static_cast<unsigned char>(alt[0]))) f.push_back(x);
     }
     if (!ok || f.empty()) break;
     std::sort(f.begin(), f.end());
@@ -1098,7 +1113,10 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
     bool reverse = false;
     if (!rx->nullable() && ext_rev()) {
       AnchorChoice rv = choose_anchor(items, false);
-      if (rv.ok && rv.dmax > kMaxPrefixBytes && (!ch.ok || rv.score >= ch.score + 0.5) &&
+      // only when the bounded anchor is weak: a strong one ("-----") is kept
+      // even if a higher-scoring literal ("PRIVAT", common in source code)
+      // sits further in
+      if (rv.ok && rv.dmax > kMaxPrefixBytes && (!ch.ok || (ch.score < kWeakAnchor && rv.score >= ch.score + 0.5)) &&
           build_reverse(items, rv.k, rv.raw, &rt)) {
         ch = rv;
         reverse = true;
