@@ -306,6 +306,7 @@ def main():
             "parallelism": "file shards per GPU, no collective (dp%d)" % world,
             "host_confirm_threads": args.threads,
             "segment_bytes": _segment_bytes(),
+            "config_id": args.config,
         },
         "roofline": {
             "bound": "hbm",
@@ -326,7 +327,7 @@ def main():
         },
         "link": {"bound": "pcie", "achieved": round(nbytes / (h2d_ms / 1e3) / 1e9, 2), "peak": PCIE_PEAK_GBPS,
                  "unit": "GB/s", "note": "H2D copy time of the step's segments (copy-stream HIP events)"},
-        "breakdown_ms": {"segments": segments, "k1": round(k1_ms, 3), "k2": round(k2_ms, 3),
+        "breakdown_ms": {"segments": segments, "chunk_bytes": stats[-1]["chunk_bytes"], "k1": round(k1_ms, 3), "k2": round(k2_ms, 3),
                          "h2d": round(h2d_ms, 3), "host_confirm": round(host_ms, 3),
                          "feed": round(mean("feed_ms"), 3), "engine_total": round(mean("total_ms"), 3),
                          "hits": stats[-1]["hits"], "candidates": stats[-1]["candidates"],

@@ -85,11 +85,13 @@ def test_largest_k1_chunk_gpu(monkeypatch):
 
 
 @pytest.mark.parametrize("variant,abl,chunk", [("1", "0", "4096"), ("3", "464", "2048"), ("3", "16", "4096"),
-                                               ("3", "0", "8192")])
+                                               ("3", "0", "8192"), ("4", "0", "1024"), ("4", "0", "4096"),
+                                               ("4", "0", "16384")])
 def test_k1_variants_agree_gpu(monkeypatch, variant, abl, chunk):
     # every K1 build whose layout bits keep results valid (v1; v3 with
-    # deferred outputs / rolled loop / 64-B lines / temporal loads) gives the
-    # default engine's result, and both equal the host confirmer's
+    # deferred outputs / rolled loop / 64-B lines / temporal loads; v4, two
+    # streams per lane, up to its largest chunk) gives the default engine's
+    # result, and both equal the host confirmer's
     c = synth.generate(24_000_000, seed=31, sizes="loguniform", plant_rate=3e-3)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     want = S.scan_host_reference(S.Scanner(None), args, threads=16)

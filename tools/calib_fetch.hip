@@ -43,6 +43,24 @@ __global__ __launch_bounds__(1024) void calib_k1pattern(const unsigned char* __r
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// K1 v3's layout: lane-owned 4 KiB chunks walked in 64-byte lines of
+// temporal 16-byte loads, one 1024-thread workgroup per CU.
+__global__ __launch_bounds__(1024) void calib_k1v3(const unsigned char* __restrict__ p, size_t nchunks,
+                                                   unsigned chunk, unsigned* out) {
+  unsigned acc = 0;
+  for (size_t c = blockIdx.x * 1024ull + threadIdx.x; c < nchunks; c += gridDim.x * 1024ull) {
+    const unsigned char* q = p + c * chunk;
+    for (unsigned off = 0; off < chunk; off += 64) {
+      v4u line[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) line[i] = *reinterpret_cast<const v4u*>(q + off + 16 * i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc ^= line[i].x ^ line[i].y ^ line[i].z ^ line[i].w;
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 // Same bytes per lane, but each load instruction covers 8 lines: the 8 lanes
 // of a group read one 128-byte line (group g of load k -> lane 8k+g's line),
 // optionally transposed through LDS so every lane ends up with its own line.
@@ -204,6 +222,12 @@ int main(int argc, char** argv) {
     hipEventSynchronize(b);
     hipEventElapsedTime(&ms, a, b);
     printf("calib_k1pattern bytes %zu time %.3f ms %.1f GB/s\n", bytes, ms, bytes / ms / 1e6);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(calib_k1v3, dim3(cus), dim3(1024), 0, 0, d, bytes / chunk, chunk, o);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&ms, a, b);
+    printf("calib_k1v3 bytes %zu time %.3f ms %.1f GB/s\n", bytes, ms, bytes / ms / 1e6);
     hipEventRecord(a);
     hipLaunchKernelGGL(calib_grouped<false>, dim3(cus), dim3(1024), 0, 0, d, bytes / chunk, chunk, o);
     hipEventRecord(b);

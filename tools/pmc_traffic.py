@@ -2,8 +2,8 @@
 
 FETCH_SIZE (KB) is scaled by the calibration run of tools/calib_fetch, which
 reads a known byte count in K1's exact access pattern (lane-owned 4 KiB
-chunks, whole 128-byte lines, nontemporal 16-byte loads):
-    scale = bytes_read / (FETCH_SIZE_KB * 1024)   of calib_k1pattern
+chunks, 64-byte lines of temporal 16-byte loads, as K1 v3 reads):
+    scale = bytes_read / (FETCH_SIZE_KB * 1024)   of calib_k1v3
     traffic(K1) = FETCH_SIZE_KB(K1 launch) * 1024 * scale
 WRITE_SIZE is reported as read (exact for streaming stores per the guide;
 K1's writes are keyword bits, hit records and per-chunk counts).
@@ -25,7 +25,7 @@ def per_kernel(root, counter):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"]
-            m = re.search(r"(tsg_k1_scan|tsg_k2_verify|calib_coalesced|calib_k1pattern)", name)
+            m = re.search(r"(tsg_k1_scan|tsg_k2_verify|calib_coalesced|calib_k1pattern|calib_k1v3)", name)
             if m:
                 vals[(m.group(1), r["Dispatch_Id"])].append(float(r["Counter_Value"]))
     out = collections.defaultdict(list)
@@ -39,12 +39,12 @@ def main():
     calib = per_kernel(run + "/calib", "FETCH_SIZE")
     calib_bytes = None
     for line in open(run + "/calib.log"):
-        m = re.match(r"calib_k1pattern bytes (\d+)", line)
+        m = re.match(r"calib_k1v3 bytes (\d+)", line)
         if m:
             calib_bytes = int(m.group(1))
     k1 = per_kernel(run + "/k1", "FETCH_SIZE")
     k1w = per_kernel(run + "/k1w", "WRITE_SIZE")
-    cal = sorted(calib["calib_k1pattern"])[len(calib["calib_k1pattern"]) // 2]
+    cal = sorted(calib["calib_k1v3"])[len(calib["calib_k1v3"]) // 2]
     scale = calib_bytes / (cal * 1024.0)
     coal = calib.get("calib_coalesced")
     bench = None
@@ -53,12 +53,16 @@ def main():
             bench = json.loads(line)
     out = {
         "kernel": "tsg_k1_scan",
+        "layout": {"config": bench["config"].get("config_id") if bench else None,
+                   "segment_bytes": bench["config"].get("segment_bytes") if bench else None,
+                   "chunk_bytes": bench["breakdown_ms"].get("chunk_bytes") if bench else None},
+        "source": run,
         "bytes_per_launch": bench["roofline"]["bytes_per_launch"] if bench else None,
         "workload": bench["config"]["workload"] if bench else None,
         "k1_fetch_size_kb_per_launch": sorted(k1["tsg_k1_scan"]),
         "k1_write_size_kb_per_launch": sorted(k1w.get("tsg_k1_scan", [])),
         "k2_fetch_size_kb_per_launch": sorted(k1.get("tsg_k2_verify", [])),
-        "calib_k1pattern": {"bytes": calib_bytes, "fetch_size_kb": cal, "scale": scale},
+        "calib_k1v3": {"bytes": calib_bytes, "fetch_size_kb": cal, "scale": scale},
         "calib_coalesced_fetch_size_kb": coal,
     }
     # mean over the K1 launches (a pipelined step launches K1 once per piece,

@@ -68,7 +68,7 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
 constexpr uint32_t kWaveHits = kK1WaveHits;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
-constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [2] overflow, [4 + g] v3 items of group g
+constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [2] overflow, [3] v4 LDS-base error, [4 + g] v3/v4 items of group g
 
 // Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
 // record's 32 - kAnchorBits offset bits.
@@ -601,6 +601,9 @@ constexpr int kAblNoNl = 1, kAblNoOut = 2, kAblNoCls = 4, kAblNoSpecial = 8, kAb
 // layout bits (results stay valid): 64-byte lines instead of 128; word loop
 // rolled (register-indexed) instead of unrolled
 constexpr int kAblLine64 = 64, kAblRolled = 128, kAblDefer = 256;
+// measurement only: every line load reads the batch's first 1 MiB instead
+// (L2-resident), pricing the per-byte work without HBM
+constexpr int kAblNoLoad = 512;
 // Deferred outputs (kAblDefer): a lane parks each output position of its
 // fast lines as (offset from the chunk start << 16 | state) in its own slots
 // of a global buffer (L2-resident) and handles them when its file or chunk
@@ -610,7 +613,9 @@ constexpr uint32_t kOutSlots = 8;
 struct OutBuf { uint32_t* p; uint32_t stride, n; };
 
 template <int kAbl>
-__device__ __forceinline__ v4u k1_load(const uint8_t* p) {
+__device__ __forceinline__ v4u k1_load(const uint8_t* data, unsigned long long off) {
+  if (kAbl & kAblNoLoad) off &= 0xfffffull;   // the batch holds >= 1 MiB in these runs (checked on the host)
+  const uint8_t* p = data + off;
   if (kAbl & kAblTemporal) return *reinterpret_cast<const v4u*>(p);
   return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
 }
@@ -772,12 +777,12 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
         if (t.p + kL <= t.lim) {
           if (!have) {
 #pragma unroll
-            for (int i = 0; i < kW; ++i) cur[i] = k1_load<kAbl>(data + t.p + 16 * i);
+            for (int i = 0; i < kW; ++i) cur[i] = k1_load<kAbl>(data, t.p + 16 * i);
           }
           have = t.p + 2 * kL <= t.lim;
           if (have) {
 #pragma unroll
-            for (int i = 0; i < kW; ++i) nxt[i] = k1_load<kAbl>(data + t.p + kL + 16 * i);
+            for (int i = 0; i < kW; ++i) nxt[i] = k1_load<kAbl>(data, t.p + kL + 16 * i);
           }
           if (!(kAbl & (kAblNoSpecial | kAblLoadOnly)) && x.primary) {
             uint32_t hb = 0;
@@ -846,6 +851,311 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
 }
 
+// K1 v4: v3's per-byte work on TWO streams per lane.  v3's transition chain
+// is one dependent LDS round trip per byte per lane (measured: the no-HBM
+// build runs at 3.3 TB/s against 3.0 with HBM, so K1 is bound by that chain,
+// not by memory); v4 walks the lane's two adjacent chunks (2c, 2c + 1) with
+// their chains interleaved, so two transitions are in flight per lane.
+//  * a wave item is 64 lanes x 2 chunks; the hit record's item offset spans
+//    128 x chunk bytes (k1_max_chunk(2));
+//  * the transition address is one v_lshl_add_u32 ((s << 1) + c2) feeding a
+//    ds_read_u16 with the table's offset as its immediate: the table is read
+//    through an LDS-address-space pointer built from that integer, which
+//    requires the kernel's dynamic LDS to start at address 0 (no static LDS;
+//    checked at run time, the kernel reports a mismatch instead of reading);
+//  * output states are checked per 8 bytes (max of 8 states) and parked in
+//    the stream's deferred-output slots as in v3;
+//  * lines of one stream with a file boundary or chunk end, and the tail of
+//    a stream once the other has finished, take v3's single-stream code.
+typedef __attribute__((address_space(3))) const uint16_t k1_lds16_t;
+typedef __attribute__((address_space(3))) const uint8_t k1_lds8_t;
+__device__ __forceinline__ uint32_t k1_lds16(uint32_t a) { return *reinterpret_cast<k1_lds16_t*>(a); }
+__device__ __forceinline__ uint32_t k1_lds8(uint32_t a) { return *reinterpret_cast<k1_lds8_t*>(a); }
+
+// park (or, slots full, handle) the outputs among 4 consecutive states of a
+// stream; t.p is the word's first byte, k0 the first state's byte in it
+__device__ __forceinline__ void k1_v4_outs(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t S, const uint32_t st[4],
+                                           int k0) {
+  if (max(max(st[0], st[1]), max(st[2], st[3])) >= x.first_out) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (st[k] >= x.first_out) {
+        if (ob.n < kOutSlots) {
+          ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k0 + k - t.emit) << 16) | st[k];
+          ++ob.n;
+        } else {
+          k1_out_v3(x, t, st[k], t.p + k0 + k, S);
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t k1_nl_word(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t xx = w[j] ^ 0x0a0a0a0au;
+    n += __popc(((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu);   // bit 7 of a byte: not '\n'
+  }
+  return 128u - n;
+}
+
+// one 16-byte word of each of two streams, chains interleaved
+__device__ __forceinline__ void k1_v4_pair(const K1Ctx& x, K1Stream& a, K1Stream& b, OutBuf& oa, OutBuf& ob, uint32_t S,
+                                           v4u wa, v4u wb) {
+  constexpr uint32_t kTabOff = 256;
+  const uint32_t A[4] = {wa.x, wa.y, wa.z, wa.w}, B[4] = {wb.x, wb.y, wb.z, wb.w};
+  const bool ea = a.p >= a.emit, eb = b.p >= b.emit;
+  uint32_t sa = a.s, sb = b.s;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {              // dword h of each word: bounded live ranges
+    uint32_t ca[4], cb[4], ta[4], tb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ca[k] = k1_lds8((A[h] >> (k * 8)) & 0xffu);
+      cb[k] = k1_lds8((B[h] >> (k * 8)) & 0xffu);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sa = k1_lds16((sa << 1) + ca[k] + kTabOff);
+      sb = k1_lds16((sb << 1) + cb[k] + kTabOff);
+      ta[k] = sa;
+      tb[k] = sb;
+    }
+    if (ea) k1_v4_outs(x, a, oa, S, ta, 4 * h);
+    if (eb) k1_v4_outs(x, b, ob, S, tb, 4 * h);
+  }
+  a.s = sa;
+  b.s = sb;
+  if (ea) a.nl += k1_nl_word(A[0], A[1], A[2], A[3]);
+  if (eb) b.nl += k1_nl_word(B[0], B[1], B[2], B[3]);
+  a.p12 = (A[3] >> 24) | ((A[3] >> 8) & 0xff00u);
+  b.p12 = (B[3] >> 24) | ((B[3] >> 8) & 0xff00u);
+  a.p += 16;
+  b.p += 16;
+}
+
+// one 16-byte word of one stream (v4's layout, 4-byte output groups)
+__device__ __forceinline__ void k1_v4_single(const K1Ctx& x, K1Stream& a, OutBuf& oa, uint32_t S, v4u wa) {
+  constexpr uint32_t kTabOff = 256;
+  const uint32_t A[4] = {wa.x, wa.y, wa.z, wa.w};
+  const bool ea = a.p >= a.emit;
+  uint32_t sa = a.s;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    uint32_t ca[4], ta[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ca[k] = k1_lds8((A[h] >> (k * 8)) & 0xffu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sa = k1_lds16((sa << 1) + ca[k] + kTabOff);
+      ta[k] = sa;
+    }
+    if (ea) k1_v4_outs(x, a, oa, S, ta, 4 * h);
+  }
+  a.s = sa;
+  if (ea) a.nl += k1_nl_word(A[0], A[1], A[2], A[3]);
+  a.p12 = (A[3] >> 24) | ((A[3] >> 8) & 0xff00u);
+  a.p += 16;
+}
+
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
+    const uint8_t* __restrict__ data, unsigned long long total,
+    const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
+    uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
+    const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
+    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
+    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
+    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
+    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
+    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
+    uint32_t* __restrict__ obuf) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int kAbl = kAblTemporal | kAblLine64 | kAblDefer;   // v3's single-stream code for the odd lines
+  constexpr uint32_t kWaves = kThreads / 64;
+  constexpr uint32_t kTabOff = 256;
+  constexpr int kW = 4;                          // 16-byte words per 64-byte line
+  constexpr uint32_t kL = kW * 16;
+  // the integer LDS addresses assume the dynamic LDS starts at offset 0
+  if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((k1_lds8_t*)(smem))) != 0) {
+    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
+    return;
+  }
+  const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
+  const uint32_t list_off = kTabOff + padded;
+  const uint32_t hits_off = (list_off + nlist * 4 + 15) & ~15u;
+  uint32_t S = (nclasses + 2) & ~1u;             // k1_row_stride(nclasses): the silent-row stride
+  if (((S / 2) & 1u) == 0) S += 2;
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
+  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
+  uint32_t* s_block = s_hitcnt + kMaxWaves;
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_block[0] = 0;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(g_next);
+    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff);
+    for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[i] = g_cls[i];
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(smem + list_off);
+    for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
+  }
+  K1Ctx x;
+  x.data = data; x.total = total; x.chunk = chunk;
+  x.offsets = offsets; x.nfiles = nfiles;
+  x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
+  x.cls = smem;
+  x.first_out = first_out; x.nclasses = nclasses;
+  x.meta = nullptr;
+  x.list = reinterpret_cast<const uint32_t*>(smem + list_off);
+  x.nkw = nkw;
+  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
+  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
+  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
+  x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
+  __syncthreads();
+  const unsigned long long nitems = (nchunks + 127) / 128;      // wave work items (64 lanes x 2 chunks)
+  const uint32_t nthreads = gridDim.x * kThreads;
+  for (;;) {
+    unsigned long long item = 0;
+    if (lane == 0) {
+      item = atomicAdd(item_ctr, 1u);
+      *x.w_hitcnt = 0;
+    }
+    item = __shfl(item, 0);
+    if (item >= nitems) break;                                 // wave-uniform exit
+    __builtin_amdgcn_wave_barrier();
+    x.item_base = item * 128 * static_cast<unsigned long long>(chunk);
+    const unsigned long long ca = item * 128 + 2 * lane;       // stream a's chunk; b's is ca + 1
+    if (ca < nchunks) {
+      K1Stream ta, tb;
+      k1_init(x, ta, min(ca * chunk, total), warm_lines);
+      k1_init(x, tb, min((ca + 1) * chunk, total), warm_lines);
+      OutBuf oa{obuf + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
+      OutBuf ob{obuf + static_cast<size_t>(nthreads) * kOutSlots + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
+      v4u la[kW], lb[kW];
+      bool ha = false, hb = false;                               // la / lb hold the line at t.p
+      // one stream's line holds a file boundary or its chunk end: word by
+      // word (its parked outputs belong to its current file: handle them
+      // first)
+      auto slow_line = [&](K1Stream& t, OutBuf& o) {
+        k1_drain(x, t, o, S);
+        for (int i = 0; i < kW && t.p < k1_end(x, t); ++i) {
+          const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          k1_word_slow<true>(x, t, w, S);
+        }
+      };
+      // the other stream has finished: one stream's fast line
+      auto single_line = [&](K1Stream& t, OutBuf& o, v4u (&l)[kW], bool& h) {
+        if (!h) {
+#pragma unroll
+          for (int i = 0; i < kW; ++i) l[i] = k1_load<kAbl>(data, t.p + 16 * i);
+        }
+        if (x.primary) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int i = 0; i < kW; ++i) m |= l[i].x | l[i].y | l[i].z | l[i].w;
+          if ((m & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
+        }
+        h = t.p + 2 * kL <= t.lim;
+        const unsigned long long q = t.p + kL;
+#pragma unroll
+        for (int i = 0; i < kW; ++i) {
+          const v4u w = l[i];
+          if (h) l[i] = k1_load<kAbl>(data, q + 16 * i);
+          k1_v4_single(x, t, o, S, w);
+        }
+      };
+      for (;;) {
+        const bool ra = ta.p < ta.lim || ta.p < k1_end(x, ta);
+        const bool rb = tb.p < tb.lim || tb.p < k1_end(x, tb);
+        if (!ra && !rb) break;
+        const bool fa = ta.p + kL <= ta.lim, fb = tb.p + kL <= tb.lim;
+        if (fa && fb) {
+          if (!ha) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) la[i] = k1_load<kAbl>(data, ta.p + 16 * i);
+          }
+          if (!hb) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) lb[i] = k1_load<kAbl>(data, tb.p + 16 * i);
+          }
+          if (x.primary) {
+            uint32_t ma = 0, mb = 0;
+#pragma unroll
+            for (int i = 0; i < kW; ++i) {
+              ma |= la[i].x | la[i].y | la[i].z | la[i].w;
+              mb |= lb[i].x | lb[i].y | lb[i].z | lb[i].w;
+            }
+            if ((ma & 0x80808080u) && k1_line_special(data + ta.p, ta.p12, kL)) atomicOr(&x.fflags[ta.f], 1u);
+            if ((mb & 0x80808080u) && k1_line_special(data + tb.p, tb.p12, kL)) atomicOr(&x.fflags[tb.f], 1u);
+          }
+          // rolling prefetch: once word i is taken, word i of the next line
+          // (when that line lies inside the stream) is loaded into its slot
+          ha = ta.p + 2 * kL <= ta.lim;
+          hb = tb.p + 2 * kL <= tb.lim;
+          const unsigned long long qa = ta.p + kL, qb = tb.p + kL;
+#pragma unroll
+          for (int i = 0; i < kW; ++i) {
+            const v4u wa = la[i], wb = lb[i];
+            if (ha) la[i] = k1_load<kAbl>(data, qa + 16 * i);
+            if (hb) lb[i] = k1_load<kAbl>(data, qb + 16 * i);
+            k1_v4_pair(x, ta, tb, oa, ob, S, wa, wb);
+          }
+        } else if (ra && !fa) {
+          ha = false;
+          slow_line(ta, oa);
+        } else if (rb && !fb) {
+          hb = false;
+          slow_line(tb, ob);
+        } else if (fa) {
+          single_line(ta, oa, la, ha);
+        } else {
+          single_line(tb, ob, lb, hb);
+        }
+      }
+      k1_drain(x, ta, oa, S);
+      k1_drain(x, tb, ob, S);
+      flush_kw(x.kwmask, kw_words, ta.f, ta.kw0, ta.kw1);
+      flush_kw(x.kwmask, kw_words, tb.f, tb.kw0, tb.kw1);
+      if (x.primary) {
+        nl_count[ca] = ta.nl;
+        if (ca + 1 < nchunks) nl_count[ca + 1] = tb.nl;
+      }
+    }
+    // flush this wave's hit buffer (the wave has reconverged here)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t n = min(*x.w_hitcnt, kWaveHits);
+    uint32_t b0 = 0, o0 = 0;
+    if (lane == 0 && n) {
+      b0 = atomicAdd(x.b_hitcnt, n);
+      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
+    }
+    b0 = __shfl(b0, 0);
+    o0 = __shfl(o0, 0);
+    const uint32_t spill_from = max(b0, region_cap);
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t h = x.w_hits[i];
+      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
+      if (b0 + i < region_cap) {
+        x.hits[b0 + i] = v;
+      } else {
+        const uint32_t oi = o0 + (b0 + i - spill_from);
+        if (oi < x.over_cap) x.over[oi] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
+}
+
 // K1 instantiations: (workgroup size, interleaved streams per lane)
 template <bool kLds>
 const void* k1_kernel_t(uint32_t threads, int ks) {
@@ -857,6 +1167,10 @@ const void* k1_kernel_t(uint32_t threads, int ks) {
 // variant 3 (tsg_k1_scan_v3) needs the table in LDS, 1024 threads, one stream
 // per lane; `abl` selects a measurement build (kAbl*)
 const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int abl = 0) {
+  if (variant == 4) {
+    if (!lds || threads != 1024 || ks != 1) return nullptr;
+    return reinterpret_cast<const void*>(&tsg_k1_scan_v4<1024>);
+  }
   if (variant == 3) {
     if (!lds || threads != 1024 || ks != 1) return nullptr;
     switch (abl) {
@@ -865,7 +1179,7 @@ const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int a
       TSG_K1_V3(31) TSG_K1_V3(32) TSG_K1_V3(48)
       TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(82) TSG_K1_V3(146) TSG_K1_V3(210) TSG_K1_V3(112) TSG_K1_V3(240)
       TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466)
-      TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496)
+      TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(912) TSG_K1_V3(784)
 #undef TSG_K1_V3
       default: return nullptr;
     }
@@ -1231,7 +1545,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   }
   if (const char* c = std::getenv("TSG_K1_VARIANT")) {
     const int v = std::atoi(c);
-    if (v == 1 || v == 3) e->k1_variant_ = v;
+    if (v == 1 || v == 3 || v == 4) e->k1_variant_ = v;
   }
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // measurement builds of v3 only
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
@@ -1239,7 +1553,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
     // chunks are clamped so the offset cannot wrap
     const long v = std::atol(c);
-    if (v >= 256 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(e->k1_streams_)));
+    if (v >= 256 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(e->k1_item_chunks())));
   }
   for (int d : devices) {
     std::unique_ptr<DeviceTables> dt(new DeviceTables());
@@ -1319,7 +1633,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
   const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total);
-  if (kChunk > k1_max_chunk(k1_streams_) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
+  if (kChunk > k1_max_chunk(k1_item_chunks()) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
+  if ((k1_abl_ & kAblNoLoad) && total < (1u << 20) + 64) { *err = "TSG_K1_ABL no-load build needs a batch of >= 1 MiB"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
   hipStream_t s = ln.compute;
@@ -1362,7 +1677,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     HIP_OK(hipMemsetAsync(ln.d_bh, 0, nregions * sizeof(uint32_t), s));
     // v3 runs the groups whose table is in LDS (1024 threads, one stream per
     // lane); the others keep v1
-    auto k1_var = [&](const K1Group& g) { return k1_variant_ == 3 && g.in_lds && nthr == 1024 && ks == 1 ? 3 : 1; };
+    auto k1_var = [&](const K1Group& g) {
+      return (k1_variant_ == 3 || k1_variant_ == 4) && g.in_lds && nthr == 1024 && ks == 1 ? k1_variant_ : 1;
+    };
     auto k1_lds = [&](const K1Group& g) {
       return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
              (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
@@ -1405,9 +1722,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       ++launches;
     }
     HIP_OK(hipEventRecord(ln.ev[1], s));
-    ln.h_bh.resize(nregions + 1);
+    ln.h_bh.resize(nregions + 2);
     HIP_OK(hipMemcpyAsync(ln.h_bh.data(), ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(ln.h_bh.data() + nregions, ln.d_cnt + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(ln.h_bh.data() + nregions, ln.d_cnt + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     float k1 = 0;
     HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
@@ -1416,6 +1733,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     uint64_t nhits = 0;
     uint32_t maxr = 0;
     for (uint32_t r = 0; r < nregions; ++r) { nhits += ln.h_bh[r]; maxr = std::max(maxr, std::min(ln.h_bh[r], region_cap)); }
+    if (ln.h_bh[nregions + 1] != 0) { *err = "K1 v4: dynamic LDS does not start at address 0"; return false; }
     const uint32_t nover = ln.h_bh[nregions];
     if (nover > ln.over_cap) {
       // the overflow pool (shared by every workgroup) was too small: grow it
