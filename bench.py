@@ -8,9 +8,10 @@ scanned with the builtin rules.
 
 One step = SURVEY.md 8(d)'s wall clock: the packed batch in PINNED HOST
 memory -> tsg_scan_batch -> assembled types.Secret results for every file.
-Inside, the engine streams the batch to HBM in 4 GiB segments ending in a
-512 MiB one (upload of segment k+1 on a copy stream overlapping K1/K2 of
-segment k and the host confirmation of segment k-1), so `value` includes PCIe.  Reported beside it,
+Inside, the engine streams the batch to HBM in 4 GiB segments (the rest
+after the last full one is one more segment; upload of segment k+1 on a copy
+stream overlapping K1/K2 of segment k and the host confirmation of segment
+k-1), so `value` includes PCIe.  Reported beside it,
 never as `value`: the HBM-resident rate (corpus already in HBM), the
 host-feed ceiling (the same segmented upload with no kernels) and the host
 content-preparation rate (tsg_prepare_batch).

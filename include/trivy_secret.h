@@ -194,6 +194,11 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
                          const uint8_t* binary, tsg_result** out);
 /* Prefilter compile report without a GPU (NUL-terminated; free with tsg_free). */
 int tsg_prefilter_report(const tsg_ruleset* rs, char** out);
+/* Tooling (no reference analogue): scan DFA `group` as compiled for K1 --
+ * next[state * nclasses + class] (state ids), byte -> class map (256 bytes),
+ * states >= first_out have outputs.  Both arrays are freed with tsg_free. */
+int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, uint8_t** byte_class,
+                      uint32_t* nstates, uint32_t* nclasses, uint32_t* first_out);
 /* Test hook for the host regexp engine: compiles `pattern` (Go syntax) and,
  * for each of the n positions, writes the end of the leftmost-first match
  * anchored there (-1: none) as computed by the lazy DFA (dfa_end) and by the

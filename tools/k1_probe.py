@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--prewarm-ms", type=float, default=0.0,
                     help="keep the GPU busy (torch elementwise kernels) this long right before each K1/K2 run")
     ap.add_argument("--variants", default="",
-                    help="comma list of VARIANT[:ABL[:CHUNK]] (TSG_K1_VARIANT / TSG_K1_ABL / TSG_K1_CHUNK), "
+                    help="comma list of VARIANT[:ABL[:CHUNK[:THREADS/STREAMS]]] (TSG_K1_VARIANT / TSG_K1_ABL / "
+                         "TSG_K1_CHUNK / TSG_K1_CFG), "
                          "one engine each")
     args = ap.parse_args()
     import torch
@@ -52,13 +53,17 @@ def main():
     variants = [v for v in args.variants.split(",") if v] or [None]
     for v in variants:
         if v is not None:
-            parts = v.split(":") + ["", ""]
+            parts = v.split(":") + ["", "", ""]
             os.environ["TSG_K1_VARIANT"] = parts[0]
             os.environ["TSG_K1_ABL"] = parts[1] or "0"
             if parts[2]:
                 os.environ["TSG_K1_CHUNK"] = parts[2]
             else:
                 os.environ.pop("TSG_K1_CHUNK", None)
+            if parts[3]:
+                os.environ["TSG_K1_CFG"] = parts[3].replace("/", ",")
+            else:
+                os.environ.pop("TSG_K1_CFG", None)
         sc = S.Scanner(S.ParseConfig(cfg) if cfg else None)
         probe(args, sc, c, d, L)
 

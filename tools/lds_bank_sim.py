@@ -1,0 +1,154 @@
+#!/usr/bin/env python
+"""LDS bank-conflict model of K1's transition reads (tooling, CPU only).
+
+K1 (v3) reads one uint16 transition per byte per lane: ds_read_u16 at byte
+address 256 + 2 * row(state) + 2 * class(byte).  On gfx950 a b32-class LDS
+read is served in two groups of 32 lanes, one LDS cycle per group when the
+lanes touch distinct banks ((address / 4) mod 32) or the same dword
+(broadcast); every further distinct dword on a busy bank costs one more cycle
+(MI355X_MICROARCH.md, LDS).  This tool replays the builtin scan DFA over a
+synthetic corpus with 64 lanes per wave, each lane on its own 4 KiB chunk as
+K1 assigns them, and reports LDS cycles per wave-instruction for a table
+layout:
+
+  current   rows of 33 dwords (silent) / 39 dwords (output), classes as compiled
+  freq      classes renumbered by their byte frequency in the corpus (most
+            frequent first), rows as current
+  phase     freq + every state's row start placed so its bank phase
+            ((row dword) mod 32) is chosen greedily against the states that
+            are live together, with padding in LDS
+
+  python tools/lds_bank_sim.py [--mb 64] [--waves 64] [--layouts current,freq,phase]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def dump_dfa():
+    from trivy_amd import _lib
+    from trivy_amd import secret as S
+    L = _lib.lib()
+    global _SCANNER
+    _SCANNER = S.Scanner(None)                       # keeps the ruleset alive
+    rs = _SCANNER._rs
+    nx, bc = ctypes.POINTER(ctypes.c_uint16)(), ctypes.POINTER(ctypes.c_uint8)()
+    ns, nc, fo = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    L.tsg_scan_dfa_dump.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint16)),
+                                    ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_uint32),
+                                    ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    _lib.check(L.tsg_scan_dfa_dump(rs, 0, ctypes.byref(nx), ctypes.byref(bc), ctypes.byref(ns), ctypes.byref(nc),
+                                   ctypes.byref(fo)))
+    n, c = ns.value, nc.value
+    nxt = np.ctypeslib.as_array(nx, shape=(n * c,)).astype(np.int64).reshape(n, c).copy()
+    cls = np.ctypeslib.as_array(bc, shape=(256,)).astype(np.int64).copy()
+    L.tsg_free(ctypes.cast(nx, ctypes.c_void_p))
+    L.tsg_free(ctypes.cast(bc, ctypes.c_void_p))
+    return nxt, cls, fo.value
+
+
+def lane_states(nxt, cls, text, starts, length):
+    """DFA state of each lane after each byte: (length, lanes)."""
+    lanes = len(starts)
+    st = np.zeros(lanes, dtype=np.int64)
+    out = np.empty((length, lanes), dtype=np.int64)
+    byts = np.stack([text[s:s + length] for s in starts], axis=1).astype(np.int64)   # (length, lanes)
+    cl = cls[byts]
+    for j in range(length):
+        out[j] = st                                  # state BEFORE byte j (the row read at step j)
+        st = nxt[st, cl[j]]
+    return out, cl
+
+
+def cycles(dwords):
+    """LDS cycles per wave-instruction: dwords (steps, 64) -> mean over steps of the two half-waves' max bank load."""
+    tot = 0.0
+    for h in range(2):
+        d = np.sort(dwords[:, 32 * h:32 * h + 32], axis=1)
+        new = np.ones_like(d, dtype=bool)
+        new[:, 1:] = d[:, 1:] != d[:, :-1]
+        bank = d % 32
+        rows = np.repeat(np.arange(d.shape[0]), 32).reshape(d.shape)
+        cnt = np.zeros((d.shape[0], 32), dtype=np.int64)
+        np.add.at(cnt, (rows[new], bank[new]), 1)
+        tot += cnt.max(axis=1).mean()
+    return tot
+
+
+def layout_rows(nstates, fo, stride, ostride, phase=None):
+    """Row start (uint16 units) of each state; phase: wanted (row dword mod 32) per state or None."""
+    rows = np.zeros(nstates, dtype=np.int64)
+    pos = 0
+    for s in range(nstates):
+        if phase is not None:
+            d = pos // 2
+            pad = (phase[s] - d) % 32
+            pos += 2 * pad
+        rows[s] = pos
+        pos += stride if s < fo else ostride
+    return rows, pos
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mb", type=float, default=64)
+    ap.add_argument("--waves", type=int, default=48)
+    ap.add_argument("--chunk", type=int, default=4096)
+    ap.add_argument("--layouts", default="current,freq,phase")
+    args = ap.parse_args()
+    from workload import synth
+    nxt, cls, fo = dump_dfa()
+    n, C = nxt.shape
+    corp = synth.generate(int(args.mb * 1e6), seed=7, sizes="loguniform")
+    text = np.asarray(corp.data[:corp.nbytes])
+    rng = np.random.default_rng(1)
+    nchunks = corp.nbytes // args.chunk - 1
+    waves = []
+    for w in range(args.waves):
+        base = int(rng.integers(0, nchunks - 64))
+        starts = [(base + i) * args.chunk for i in range(64)]
+        waves.append(lane_states(nxt, cls, text, starts, args.chunk))
+    # class frequency over the replay (bytes read) and state occupancy
+    cfreq = np.bincount(np.concatenate([cl.ravel() for _, cl in waves]), minlength=C)
+    sfreq = np.bincount(np.concatenate([st.ravel() for st, _ in waves]), minlength=n)
+    print("scan DFA: %d states x %d classes, first output state %d; root occupancy %.3f, top-8 states %s" % (
+        n, C, fo, sfreq[0] / sfreq.sum(), np.argsort(-sfreq)[:8].tolist()))
+    S = (C + 2) & ~1
+    if (S // 2) % 2 == 0:
+        S += 2
+    So = S + 10
+    if (So // 2) % 2 == 0:
+        So += 2
+    perm_id = np.arange(C)
+    order = np.argsort(-cfreq)
+    perm_freq = np.empty(C, dtype=np.int64)
+    perm_freq[order] = np.arange(C)                  # class c -> new index by frequency rank
+    results = {}
+    for name in args.layouts.split(","):
+        perm = perm_id if name == "current" else perm_freq
+        phase = None
+        if name == "phase":
+            # the busiest states get bank phases spread so their hot classes
+            # (low new indices -> dwords 0..) land on different banks: state
+            # rank r gets phase 16 * (r & 1) + 8 * ((r >> 1) & 1) + ...
+            rank = np.empty(n, dtype=np.int64)
+            rank[np.argsort(-sfreq)] = np.arange(n)
+            phase = np.array([int('{:05b}'.format(int(r) & 31)[::-1], 2) for r in rank])
+        rows, size = layout_rows(n, fo, S, So, phase)
+        tot = 0.0
+        for st, cl in waves:
+            dw = (256 + 2 * rows[st] + 2 * perm[cl]) // 4
+            tot += cycles(dw)
+        results[name] = (tot / len(waves), size * 2)
+        print("%-8s LDS cycles per transition read (2 groups, 2.0 = conflict-free): %.3f   table %d B" % (
+            name, results[name][0], results[name][1]))
+
+
+if __name__ == "__main__":
+    main()

@@ -419,6 +419,27 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
   return TSG_OK;
 }
 
+int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, uint8_t** byte_class, uint32_t* nstates,
+                      uint32_t* nclasses, uint32_t* first_out) {
+  if (!rs || !next || !byte_class || !nstates || !nclasses || !first_out) return fail(TSG_ERR_INVALID, "NULL argument");
+  Prefilter pf;
+  std::string err;
+  if (!build_prefilter(*rs->rs, &pf, &err)) return fail(TSG_ERR_INTERNAL, err);
+  if (group >= pf.groups.size()) return fail(TSG_ERR_INVALID, "no such scan DFA group");
+  const ScanDfa& d = pf.groups[group];
+  uint16_t* nx = static_cast<uint16_t*>(malloc(std::max<size_t>(d.t.next.size(), 1) * sizeof(uint16_t)));
+  uint8_t* bc = static_cast<uint8_t*>(malloc(256));
+  if (!nx || !bc) { free(nx); free(bc); return fail(TSG_ERR_INTERNAL, "out of memory"); }
+  std::copy(d.t.next.begin(), d.t.next.end(), nx);
+  memcpy(bc, d.t.byte_class, 256);
+  *next = nx;
+  *byte_class = bc;
+  *nstates = d.t.nstates;
+  *nclasses = d.t.nclasses;
+  *first_out = d.first_out_state;
+  return TSG_OK;
+}
+
 const char* tsg_builtin_rules_json(void) { return tsg_builtin_json_ptr(); }
 
 // GetSecretRulesMetadata (builtin-rules.go:91-99): lo.Map(builtinRules, ...

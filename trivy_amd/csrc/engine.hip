@@ -161,6 +161,18 @@ __device__ __forceinline__ uint32_t k1_step(const uint16_t* next, uint32_t s, ui
   return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(next) + ((s << 1) + c2));
 }
 
+// LDS reads by integer LDS address (v3 / v4): the kernel's dynamic LDS starts
+// at offset 0 (no static LDS; checked at run time by k1_lds_base_ok), so a
+// transition address is one v_lshl_add_u32 feeding a ds_read_u16 whose
+// immediate offset is the table's position.
+typedef __attribute__((address_space(3))) const uint16_t k1_lds16_t;
+typedef __attribute__((address_space(3))) const uint8_t k1_lds8_t;
+__device__ __forceinline__ uint32_t k1_lds16(uint32_t a) { return *reinterpret_cast<k1_lds16_t*>(a); }
+__device__ __forceinline__ uint32_t k1_lds8(uint32_t a) { return *reinterpret_cast<k1_lds8_t*>(a); }
+__device__ __forceinline__ bool k1_lds_base_ok(const uint8_t* smem) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((k1_lds8_t*)(smem))) == 0;
+}
+
 __device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Stream& t) {
   return min(t.emit + x.chunk, x.total);
 }
@@ -604,6 +616,9 @@ constexpr int kAblLine64 = 64, kAblRolled = 128, kAblDefer = 256;
 // measurement only: every line load reads the batch's first 1 MiB instead
 // (L2-resident), pricing the per-byte work without HBM
 constexpr int kAblNoLoad = 512;
+// measurement only: transitions addressed by pointer arithmetic on the
+// dynamic-LDS pointer (two VALU per byte) instead of the integer LDS address
+constexpr int kAblPtrAddr = 1024;
 // Deferred outputs (kAblDefer): a lane parks each output position of its
 // fast lines as (offset from the chunk start << 16 | state) in its own slots
 // of a global buffer (L2-resident) and handles them when its file or chunk
@@ -664,7 +679,8 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
   uint32_t s = t.s;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 1) + c2[k]);
+    if (kAbl & kAblPtrAddr) s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 1) + c2[k]);
+    else s = k1_lds16((s << 1) + c2[k] + kTabOff);
     st[k] = s;
   }
   t.s = s;
@@ -719,6 +735,10 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
   constexpr uint32_t kTabOff = 256;
+  if (!(kAbl & kAblPtrAddr) && !k1_lds_base_ok(smem)) {   // the integer LDS addresses assume a zero base
+    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
+    return;
+  }
   const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
   const uint32_t meta_off = kTabOff + padded;
   const uint32_t list_off = meta_off;            // output metadata is inline in the table rows
@@ -867,25 +887,22 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
 //    the stream's deferred-output slots as in v3;
 //  * lines of one stream with a file boundary or chunk end, and the tail of
 //    a stream once the other has finished, take v3's single-stream code.
-typedef __attribute__((address_space(3))) const uint16_t k1_lds16_t;
-typedef __attribute__((address_space(3))) const uint8_t k1_lds8_t;
-__device__ __forceinline__ uint32_t k1_lds16(uint32_t a) { return *reinterpret_cast<k1_lds16_t*>(a); }
-__device__ __forceinline__ uint32_t k1_lds8(uint32_t a) { return *reinterpret_cast<k1_lds8_t*>(a); }
+constexpr uint32_t kOutDrainV4 = 8, kOutSlotsV4 = kOutDrainV4 + 64;   // per stream
 
-// park (or, slots full, handle) the outputs among 4 consecutive states of a
-// stream; t.p is the word's first byte, k0 the first state's byte in it
+// park the outputs among 4 consecutive states of a stream in its slots (a
+// line adds at most 64; the slots are drained after any line that leaves
+// more than kOutDrainV4 parked, so kOutSlotsV4 never overflows); t.p is the
+// word's first byte, k0 the first state's byte in it.  No output is handled
+// inside the word loop: the handling code (k1_out_v3) exists only at the
+// few drain sites, which keeps the hot loop small in the instruction cache.
 __device__ __forceinline__ void k1_v4_outs(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t S, const uint32_t st[4],
                                            int k0) {
   if (max(max(st[0], st[1]), max(st[2], st[3])) >= x.first_out) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (st[k] >= x.first_out) {
-        if (ob.n < kOutSlots) {
-          ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k0 + k - t.emit) << 16) | st[k];
-          ++ob.n;
-        } else {
-          k1_out_v3(x, t, st[k], t.p + k0 + k, S);
-        }
+        ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k0 + k - t.emit) << 16) | st[k];
+        ++ob.n;
       }
     }
   }
@@ -980,8 +997,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
   constexpr uint32_t kTabOff = 256;
   constexpr int kW = 4;                          // 16-byte words per 64-byte line
   constexpr uint32_t kL = kW * 16;
-  // the integer LDS addresses assume the dynamic LDS starts at offset 0
-  if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((k1_lds8_t*)(smem))) != 0) {
+  if (!k1_lds_base_ok(smem)) {                   // the integer LDS addresses assume a zero base
     if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
     return;
   }
@@ -1035,7 +1051,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
       k1_init(x, ta, min(ca * chunk, total), warm_lines);
       k1_init(x, tb, min((ca + 1) * chunk, total), warm_lines);
       OutBuf oa{obuf + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
-      OutBuf ob{obuf + static_cast<size_t>(nthreads) * kOutSlots + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
+      OutBuf ob{obuf + static_cast<size_t>(nthreads) * kOutSlotsV4 + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
       v4u la[kW], lb[kW];
       bool ha = false, hb = false;                               // la / lb hold the line at t.p
       // one stream's line holds a file boundary or its chunk end: word by
@@ -1069,6 +1085,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
           if (h) l[i] = k1_load<kAbl>(data, q + 16 * i);
           k1_v4_single(x, t, o, S, w);
         }
+        if (o.n > kOutDrainV4) k1_drain(x, t, o, S);
       };
       for (;;) {
         const bool ra = ta.p < ta.lim || ta.p < k1_end(x, ta);
@@ -1106,6 +1123,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
             if (hb) lb[i] = k1_load<kAbl>(data, qb + 16 * i);
             k1_v4_pair(x, ta, tb, oa, ob, S, wa, wb);
           }
+          if (oa.n > kOutDrainV4) k1_drain(x, ta, oa, S);
+          if (ob.n > kOutDrainV4) k1_drain(x, tb, ob, S);
         } else if (ra && !fa) {
           ha = false;
           slow_line(ta, oa);
@@ -1168,8 +1187,10 @@ const void* k1_kernel_t(uint32_t threads, int ks) {
 // per lane; `abl` selects a measurement build (kAbl*)
 const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int abl = 0) {
   if (variant == 4) {
-    if (!lds || threads != 1024 || ks != 1) return nullptr;
-    return reinterpret_cast<const void*>(&tsg_k1_scan_v4<1024>);
+    if (!lds || ks != 1) return nullptr;
+    if (threads == 1024) return reinterpret_cast<const void*>(&tsg_k1_scan_v4<1024>);
+    if (threads == 512) return reinterpret_cast<const void*>(&tsg_k1_scan_v4<512>);
+    return nullptr;
   }
   if (variant == 3) {
     if (!lds || threads != 1024 || ks != 1) return nullptr;
@@ -1180,6 +1201,7 @@ const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int a
       TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(82) TSG_K1_V3(146) TSG_K1_V3(210) TSG_K1_V3(112) TSG_K1_V3(240)
       TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466)
       TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(912) TSG_K1_V3(784)
+      TSG_K1_V3(1488)
 #undef TSG_K1_V3
       default: return nullptr;
     }
@@ -1536,16 +1558,16 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const long long v = std::atoll(c);
     if (v >= 0) e->segment_tail_ = static_cast<uint64_t>(v);
   }
-  if (const char* cfg = std::getenv("TSG_K1_CFG")) {
-    unsigned t = 0, k = 0;
-    if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k))) {
-      e->k1_threads_ = t;
-      e->k1_streams_ = static_cast<int>(k);
-    }
-  }
   if (const char* c = std::getenv("TSG_K1_VARIANT")) {
     const int v = std::atoi(c);
     if (v == 1 || v == 3 || v == 4) e->k1_variant_ = v;
+  }
+  if (const char* cfg = std::getenv("TSG_K1_CFG")) {
+    unsigned t = 0, k = 0;
+    if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k), e->k1_variant_, 0)) {
+      e->k1_threads_ = t;
+      e->k1_streams_ = static_cast<int>(k);
+    }
   }
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // measurement builds of v3 only
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
@@ -1652,7 +1674,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   if (4 + ngroups > kCntBytes / 4) { *err = "too many scan-DFA groups"; return false; }
   if (!ensure(&ln.d_bh, &ln.d_bh_cap, 2ull * std::max(dt.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
   if (!ensure(&ln.d_ff, &ln.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
-  if (!ensure(&ln.d_ob, &ln.d_ob_cap, 2ull * std::max(dt.sms, 1) * 1024 * kOutSlots, err)) return false;
+  // deferred-output slots: v3 kOutSlots per thread (x2 grid slack), v4 two
+  // streams x kOutSlotsV4 per thread
+  if (!ensure(&ln.d_ob, &ln.d_ob_cap, static_cast<size_t>(std::max(dt.sms, 1)) * 1024 *
+                                          std::max<size_t>(2 * kOutSlots, 2 * kOutSlotsV4), err)) return false;
 
   const uint32_t sms = static_cast<uint32_t>(dt.sms);
   const Prefilter& pf = pf_;
@@ -1678,7 +1703,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     // v3 runs the groups whose table is in LDS (1024 threads, one stream per
     // lane); the others keep v1
     auto k1_var = [&](const K1Group& g) {
-      return (k1_variant_ == 3 || k1_variant_ == 4) && g.in_lds && nthr == 1024 && ks == 1 ? k1_variant_ : 1;
+      if (k1_variant_ == 4 && g.in_lds && ks == 1 && (nthr == 1024 || nthr == 512)) return 4;
+      return k1_variant_ == 3 && g.in_lds && nthr == 1024 && ks == 1 ? 3 : 1;
     };
     auto k1_lds = [&](const K1Group& g) {
       return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
@@ -1733,7 +1759,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     uint64_t nhits = 0;
     uint32_t maxr = 0;
     for (uint32_t r = 0; r < nregions; ++r) { nhits += ln.h_bh[r]; maxr = std::max(maxr, std::min(ln.h_bh[r], region_cap)); }
-    if (ln.h_bh[nregions + 1] != 0) { *err = "K1 v4: dynamic LDS does not start at address 0"; return false; }
+    if (ln.h_bh[nregions + 1] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
     const uint32_t nover = ln.h_bh[nregions];
     if (nover > ln.over_cap) {
       // the overflow pool (shared by every workgroup) was too small: grow it
@@ -2024,9 +2050,10 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     } else {
       for (uint32_t f = 0; f < in.nfiles;) {
         // next cut: the first file boundary at or past segment_ bytes from
-        // here; the batch ends in a short segment (segment_tail_), so the
-        // kernels and confirmation left after the last upload are short while
-        // the other K1 launches stay large
+        // here; optionally (segment_tail_ > 0) the batch ends in a short
+        // segment, so the kernels and confirmation left after the last upload
+        // are shorter (measured: ~1 ms of a 179 ms 10 GB step, while the
+        // short launch runs K1 at ~2.1 TB/s against 3 TB/s for 4 GB)
         const uint64_t rest = total - in.offsets[f];
         const uint64_t tail = std::min(segment_tail_, segment_ / 8);
         uint64_t target;
