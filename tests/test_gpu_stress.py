@@ -79,7 +79,7 @@ def test_largest_k1_chunk_gpu(monkeypatch):
     want = S.Scanner(None).ScanBatch(args)
     monkeypatch.setenv("TSG_K1_CHUNK", str(1 << 20))     # clamped to the hit record's offset range
     got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
-    assert stats["chunk_bytes"] == 32768
+    assert stats["chunk_bytes"] == 8192                  # v3: a wave item spans 64 lanes x 4 chunks
     assert got == want
     assert sum(len(w["Findings"]) for w in want) > 20
 
@@ -103,3 +103,19 @@ def test_k1_variants_agree_gpu(monkeypatch, variant, abl, chunk):
     assert stats["chunk_bytes"] == int(chunk)
     assert got == want
     assert sum(len(w["Findings"]) for w in want) > 20
+
+
+def test_line_numbers_at_chunk_edges_gpu():
+    # K1 stores one '\n' count per chunk while a lane walks a range of
+    # chunks; a file boundary in the last line before a chunk edge sends that
+    # line down the word-by-word path, and the count must still be stored
+    # before the next chunk's first line.  Small files (so boundaries fall in
+    # every position of a chunk) with dense plants, every finding's line
+    # checked against the host confirmer run without the GPU prefilter.
+    c = synth.generate(40_000_000, seed=41, sizes="small", plant_rate=2e-2, layout="src")
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    got = S.Scanner(None).ScanBatch(args)
+    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    assert sum(len(w["Findings"]) for w in want) > 8000
+    for a, g, w in zip(args, got, want):
+        assert g == w, a.FilePath

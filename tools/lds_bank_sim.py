@@ -40,9 +40,6 @@ def dump_dfa():
     rs = _SCANNER._rs
     nx, bc = ctypes.POINTER(ctypes.c_uint16)(), ctypes.POINTER(ctypes.c_uint8)()
     ns, nc, fo = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-    L.tsg_scan_dfa_dump.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint16)),
-                                    ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_uint32),
-                                    ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     _lib.check(L.tsg_scan_dfa_dump(rs, 0, ctypes.byref(nx), ctypes.byref(bc), ctypes.byref(ns), ctypes.byref(nc),
                                    ctypes.byref(fo)))
     n, c = ns.value, nc.value

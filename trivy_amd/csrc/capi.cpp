@@ -386,7 +386,7 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   // per-chunk newline counts over the packed batch, as K1 produces them
   const uint32_t ch = 2048;
   const uint64_t total = nfiles ? offsets[nfiles] : 0;
-  std::vector<uint32_t> chunk_nl((total + ch - 1) / ch, 0);   // exactly K1's chunk count
+  std::vector<uint16_t> chunk_nl((total + ch - 1) / ch, 0);   // exactly K1's chunk count
   for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += data[x] == '\n';
   for (uint32_t f = 0; f < nfiles; ++f) {
     const uint8_t* c = data + offsets[f];

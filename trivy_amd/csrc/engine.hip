@@ -117,6 +117,9 @@ __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
 // state depends only on the last max_pattern_bytes - 1 bytes of the file.
 struct K1Stream {
   unsigned long long p, lim, emit;   // next byte; min(stream end, file end); first byte with outputs
+  unsigned long long end;            // stream end (v1 / v4: one chunk; v3: the lane's range of chunks)
+  unsigned long long cend;           // v3: end of the current chunk (its '\n' count is stored there)
+  unsigned long long ci;             // v3: index of the current chunk
   uint32_t f, s, p12, nl;            // file; DFA row offset; previous two bytes (p1 | p2 << 8); newlines
   unsigned long long kw0, kw1;
 };
@@ -173,9 +176,7 @@ __device__ __forceinline__ bool k1_lds_base_ok(const uint8_t* smem) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((k1_lds8_t*)(smem))) == 0;
 }
 
-__device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Stream& t) {
-  return min(t.emit + x.chunk, x.total);
-}
+__device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Stream& t) { return t.end; }
 
 __device__ __forceinline__ void k1_out(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
   const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
@@ -300,7 +301,10 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
   t.p12 = 0;
   t.nl = 0;
   t.kw0 = t.kw1 = 0;
-  const unsigned long long end = k1_end(x, t);
+  t.end = min(c0 + x.chunk, x.total);
+  t.cend = t.end;
+  t.ci = 0;
+  const unsigned long long end = t.end;
   if (c0 >= end) { t.p = t.lim = end; t.f = 0; return; }
   t.f = file_of(x.offsets, x.nfiles, t.p);
   t.lim = min(end, x.offsets[t.f + 1]);
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ /*item_ctr: v3*/,
+    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ /*item_ctr: v3*/,
     uint32_t* __restrict__ /*obuf: v3*/) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | (scan table | class map |
@@ -464,7 +468,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
         const unsigned long long c = wi * kS + j;
         if (c < nchunks) {
           flush_kw(x.kwmask, kw_words, S[j].f, S[j].kw0, S[j].kw1);
-          if (x.primary) nl_count[c] = S[j].nl;
+          if (x.primary) nl_count[c] = static_cast<uint16_t>(S[j].nl);
         }
       }
     }
@@ -730,7 +734,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
+    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
     uint32_t* __restrict__ obuf) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
@@ -772,7 +776,18 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
   x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
   __syncthreads();
-  const unsigned long long nitems = (nchunks + 63) / 64;       // wave work items (64 chunks)
+  // Guided work schedule.  A wave item gives each of its 64 lanes a range of
+  // kU consecutive chunks, walked as one stream (one warm-up) that stores the
+  // '\n' count of every chunk it crosses.  Items come from one counter in
+  // decreasing range size: kU = 4 for the bulk, then one grid-wide round of
+  // kU = 2 and one of kU = 1, so the waves that take the last items finish
+  // after a short item and the launch has no long tail.
+  const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
+  const unsigned long long n1 = min(nchunks, W * 64);
+  const unsigned long long n2 = min(nchunks - n1, W * 128);
+  const unsigned long long n4 = nchunks - n1 - n2;
+  const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
+  const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
   for (;;) {
     unsigned long long item = 0;
     if (lane == 0) {
@@ -782,11 +797,20 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     item = __shfl(item, 0);
     if (item >= nitems) break;                                 // wave-uniform exit
     __builtin_amdgcn_wave_barrier();
-    x.item_base = item * 64 * static_cast<unsigned long long>(chunk);
-    const unsigned long long c = item * 64 + lane;
-    if (c < nchunks) {
+    unsigned long long c0, rend;
+    uint32_t kU;
+    if (item < i4) { kU = 4; c0 = item * 256; rend = n4; }
+    else if (item < i4 + i2) { kU = 2; c0 = n4 + (item - i4) * 128; rend = n4 + n2; }
+    else { kU = 1; c0 = n4 + n2 + (item - i4 - i2) * 64; rend = nchunks; }
+    x.item_base = c0 * static_cast<unsigned long long>(chunk);   // hit offsets < 256 chunks (k1_max_chunk(4))
+    const unsigned long long c = c0 + lane * kU;                 // the lane's first chunk
+    if (c < rend) {
       K1Stream t;
       k1_init(x, t, min(c * chunk, total), warm_lines);
+      t.end = min(min(c + kU, rend) * chunk, total);
+      t.cend = min(t.emit + chunk, t.end);
+      t.ci = c;
+      if (t.p < t.end) t.lim = min(t.end, x.offsets[t.f + 1]);
       OutBuf ob{obuf + blockIdx.x * kThreads + threadIdx.x, gridDim.x * kThreads, 0};
       constexpr int kW = (kAbl & kAblLine64) ? 4 : 8;     // words per line
       constexpr uint32_t kL = kW * 16;
@@ -794,6 +818,12 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
       bool have = false;
       for (;;) {
         if (!(t.p < t.lim || t.p < k1_end(x, t))) break;
+        if (t.p >= t.cend && t.cend < t.end) {                // a chunk of the range is done: store its
+          if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);   // count before any byte of the next
+          t.nl = 0;
+          ++t.ci;
+          t.cend = min(t.cend + chunk, t.end);
+        }
         if (t.p + kL <= t.lim) {
           if (!have) {
 #pragma unroll
@@ -828,6 +858,12 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
           have = false;
           if (kAbl & kAblDefer) k1_drain(x, t, ob, S);     // parked outputs belong to file t.f
           for (int i = 0; i < kW && t.p < k1_end(x, t); ++i) {
+            if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
+              if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+              t.nl = 0;
+              ++t.ci;
+              t.cend = min(t.cend + chunk, t.end);
+            }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             k1_word_slow<true>(x, t, w, S);
@@ -840,7 +876,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
         t.kw1 = 0;
       }
       flush_kw(x.kwmask, kw_words, t.f, t.kw0, t.kw1);
-      if (x.primary) nl_count[c] = t.nl;
+      if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);   // the range's last chunk
     }
     // flush this wave's hit buffer (the wave has reconverged here)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -989,7 +1025,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint32_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
+    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
     uint32_t* __restrict__ obuf) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int kAbl = kAblTemporal | kAblLine64 | kAblDefer;   // v3's single-stream code for the odd lines
@@ -1142,8 +1178,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
       flush_kw(x.kwmask, kw_words, ta.f, ta.kw0, ta.kw1);
       flush_kw(x.kwmask, kw_words, tb.f, tb.kw0, tb.kw1);
       if (x.primary) {
-        nl_count[ca] = ta.nl;
-        if (ca + 1 < nchunks) nl_count[ca + 1] = tb.nl;
+        nl_count[ca] = static_cast<uint16_t>(ta.nl);
+        if (ca + 1 < nchunks) nl_count[ca + 1] = static_cast<uint16_t>(tb.nl);
       }
     }
     // flush this wave's hit buffer (the wave has reconverged here)
@@ -1233,7 +1269,10 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // launch, 1-4 KiB.  Measured on MI355X (r2g, v3 K1): a 1 GB launch 0.52 ms
 // at 1 KiB vs 0.56 at 4 KiB (shorter wave items, shorter tail); 2 GB best at
 // 2 KiB; 4 GB and more best at 4 KiB (less warm-up per byte).
-uint32_t k1_chunk_for(uint64_t bytes) {
+// v3 walks ranges of 1-4 chunks per lane (guided schedule): its chunk is
+// the '\n'-count granularity and the last round's range, 1 KiB.
+uint32_t k1_chunk_for(uint64_t bytes, int variant) {
+  if (variant == 3) return 1024;
   uint32_t c = 1024;
   while (c < 4096 && static_cast<uint64_t>(c) * (1u << 20) < bytes) c <<= 1;
   return c;
@@ -1292,7 +1331,7 @@ struct Lane {
   unsigned long long* d_over = nullptr; size_t d_over_cap = 0;   // hits past a full region (any workgroup)
   uint32_t* d_bh = nullptr; size_t d_bh_cap = 0;    // hits written per K1 workgroup (its region of d_hits)
   CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
-  uint32_t* d_nl = nullptr; size_t d_nl_cap = 0;
+  uint16_t* d_nl = nullptr; size_t d_nl_cap = 0;   // '\n' per K1 chunk (chunk <= 32 KiB)
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   uint32_t* d_ob = nullptr; size_t d_ob_cap = 0;    // K1 v3 deferred-output slots (kOutSlots per thread)
   unsigned int* d_cnt = nullptr;
@@ -1305,7 +1344,7 @@ struct Lane {
 // host confirmer.
 struct GpuOut {
   std::vector<CandDev> cands;   // (file, rule, start) candidates, unsorted
-  std::vector<uint32_t> nl;     // '\n' count per K1 chunk
+  std::vector<uint16_t> nl;     // '\n' count per K1 chunk
   std::vector<uint32_t> ff;     // per-file flags (fold-special content)
   uint32_t chunk = 0;           // K1 chunk bytes of this segment (nl[] granularity)
 };
@@ -1654,7 +1693,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
-  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total);
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, k1_variant_);
   if (kChunk > k1_max_chunk(k1_item_chunks()) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   if ((k1_abl_ & kAblNoLoad) && total < (1u << 20) + 64) { *err = "TSG_K1_ABL no-load build needs a batch of >= 1 MiB"; return false; }
   st->chunk_bytes = kChunk;
@@ -1805,7 +1844,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       out->ff.resize(in.nfiles);
       if (in.nfiles) HIP_OK(hipMemcpyAsync(out->ff.data(), ln.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       out->nl.resize(nchunks);
-      if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), ln.d_nl, nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), ln.d_nl, nchunks * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
       st->d2h_ms += ms_since(t_d2h);
       st->candidates += c2;

@@ -101,7 +101,7 @@ struct FilePlan {
 // Newline counts for findLocation without rescanning a file: K1's per-chunk
 // '\n' counts over the packed batch (chunk c covers data[c*chunk, (c+1)*chunk)).
 struct NlSource {
-  const uint32_t* chunk_nl = nullptr;
+  const uint16_t* chunk_nl = nullptr;
   const uint8_t* data = nullptr;      // packed batch (host)
   uint64_t file_off = 0;              // global offset of this file in data
   uint32_t chunk = 0;
