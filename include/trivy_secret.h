@@ -224,6 +224,29 @@ int tsg_prepare_batch(const tsg_ruleset* rs, const char* config_path, const uint
 int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_t** offsets, const uint32_t** index,
                       const uint8_t** binary, uint32_t* nkept);
 void tsg_prepared_free(tsg_prepared* p);
+/* A container layer: walker.LayerTar.Walk (pkg/fanal/walker/tar.go:35-103)
+ * over an uncompressed layer tar in memory -- Go archive/tar's reading of
+ * ustar / GNU / PAX headers (long names, PAX path and size), header checksum,
+ * TypeRegA normalisation; opaque-directory (".wh..wh..opq") and whiteout
+ * (".wh.<name>") entries recorded, not analyzed; skip_files / skip_dirs as
+ * walker.Option (utils.CleanSkipPaths + doublestar.Match, utils.go:88-109),
+ * files under a skipped directory dropped (underSkippedDir) -- then the same
+ * preparation as tsg_prepare_batch for every regular file, with Required
+ * seeing the walker's path (no leading '/', analyzer.go:407-408).  pinned != 0
+ * packs the kept contents into pinned host memory (tsg_alloc_pinned; heap
+ * when no device is present, reported as "pinned": false) so the batch goes
+ * to tsg_scan_batch as prepared.  A malformed tar fails with Walk's
+ * "failed to extract the archive: ..." error. */
+int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const uint8_t* tar, size_t len,
+                          const char* const* skip_files, uint32_t nskip_files, const char* const* skip_dirs,
+                          uint32_t nskip_dirs, int threads, int pinned, tsg_prepared** out);
+/* The kept files' ScanArgs.FilePath: "/" + the walker's path (image files,
+ * secret.go:131-135); only for batches made by tsg_prepare_layer_tar. */
+int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens);
+/* {"files": [every regular file the walk hands to the analyzers], "opq_dirs":
+ * [...], "wh_files": [...], "pinned": bool} (Walk's return values, tar.go:90);
+ * owned by p. */
+const char* tsg_prepared_walk_json(const tsg_prepared* p);
 
 /* Test hook: Regexp.MatchString(text) for `pattern` with the required-literal
  * gate the ruleset compiler sets on path / allow regexes (*gated) and without

@@ -66,6 +66,7 @@ def main():
                 os.environ.pop("TSG_K1_CFG", None)
         sc = S.Scanner(S.ParseConfig(cfg) if cfg else None)
         probe(args, sc, c, d, L)
+        del sc                                    # engine destroyed here (TSG_K2_STATS prints its counters)
 
 
 def probe(args, sc, c, d, L):

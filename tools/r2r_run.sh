@@ -12,3 +12,5 @@ timeout -k 10 400 python -u tools/diff_paths.py > $OUT/diff.log 2>&1 || exit $?
 grep -v amdgpu.ids $OUT/diff.log | head -20
 timeout -k 10 300 python -u tools/k1_probe.py --gb 4 --reps 3 --variants 3:464,3:464:2048 > $OUT/probe4g.log 2>&1 || exit $?
 grep -v amdgpu.ids $OUT/probe4g.log
+TSG_K2_STATS=1 timeout -k 10 300 python -u tools/k1_probe.py --gb 4 --reps 1 > $OUT/k2_stats.log 2>&1 || exit $?
+grep k2_stats $OUT/k2_stats.log | cut -c1-600

@@ -86,6 +86,12 @@ SIGNATURES = [
                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32)]),
     ("tsg_prepared_free", None, [ctypes.c_void_p]),
+    ("tsg_prepare_layer_tar", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t,
+                                             c_char_pp, ctypes.c_uint32, c_char_pp, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prepared_paths", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p)),
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))]),
+    ("tsg_prepared_walk_json", ctypes.c_char_p, [ctypes.c_void_p]),
     ("tsg_regex_match_probe", ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                              ctypes.POINTER(ctypes.c_int)]),

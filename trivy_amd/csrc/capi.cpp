@@ -12,6 +12,7 @@
 
 #include "engine.h"
 #include "feed.h"
+#include "tar.h"
 #include "prefilter.h"
 #include "report.h"
 #include "scanner.h"
@@ -37,6 +38,11 @@ struct tsg_engine {
 
 struct tsg_prepared {
   PreparedBatch b;
+  // layer-tar batches: the kept files' ScanArgs.FilePath and the walk summary
+  std::vector<std::string> scan_paths;
+  std::vector<const char*> path_ptrs;
+  std::vector<uint32_t> path_lens;
+  std::string walk_json;
 };
 
 struct tsg_result {
@@ -722,3 +728,76 @@ int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_
 }
 
 void tsg_prepared_free(tsg_prepared* p) { delete p; }
+
+namespace {
+uint8_t* pinned_alloc(size_t bytes, void (**free_fn)(uint8_t*)) {
+  void* p = nullptr;
+  if (tsg_alloc_pinned(bytes, &p) != 0 || !p) return nullptr;
+  *free_fn = [](uint8_t* q) { tsg_free_pinned(q); };
+  return static_cast<uint8_t*>(p);
+}
+
+void json_str_array(std::string* js, const std::vector<std::string>& v) {
+  *js += "[";
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (i) *js += ", ";
+    go_json_string(js, v[i], false);
+  }
+  *js += "]";
+}
+}  // namespace
+
+int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const uint8_t* tar, size_t len,
+                          const char* const* skip_files, uint32_t nskip_files, const char* const* skip_dirs,
+                          uint32_t nskip_dirs, int threads, int pinned, tsg_prepared** out) {
+  if (!rs || !out || (len && !tar) || (nskip_files && !skip_files) || (nskip_dirs && !skip_dirs))
+    return fail(TSG_ERR_INVALID, "NULL argument");
+  std::vector<std::string> sf, sd;
+  for (uint32_t i = 0; i < nskip_files; ++i) sf.emplace_back(skip_files[i]);
+  for (uint32_t i = 0; i < nskip_dirs; ++i) sd.emplace_back(skip_dirs[i]);
+  LayerWalk walk;
+  std::string err;
+  if (!walk_layer_tar(tar, len, sf, sd, &walk, &err)) return fail(TSG_ERR_INVALID, err);
+  std::vector<uint64_t> starts, sizes;
+  std::vector<std::string> paths;   // Required's path: the walker's (no leading '/') (analyzer.go:407-408)
+  for (const TarFile& f : walk.files) {
+    starts.push_back(f.offset);
+    sizes.push_back(f.size);
+    paths.push_back(f.path);
+  }
+  auto* p = new tsg_prepared();
+  const int nt = threads > 0 ? threads : static_cast<int>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (!prepare_files(*rs->rs, config_path ? config_path : "", tar, starts.data(), sizes.data(), paths, nt, &p->b, &err,
+                     pinned ? pinned_alloc : nullptr)) {
+    delete p;
+    return fail(TSG_ERR_INVALID, err);
+  }
+  // files extracted from an image get a leading '/' for Scan (secret.go:131-135)
+  for (uint32_t i : p->b.index) p->scan_paths.push_back("/" + paths[i]);
+  for (const auto& sp : p->scan_paths) {
+    p->path_ptrs.push_back(sp.c_str());
+    p->path_lens.push_back(static_cast<uint32_t>(sp.size()));
+  }
+  std::string& js = p->walk_json;
+  js = "{\"files\": ";
+  json_str_array(&js, paths);
+  js += ", \"opq_dirs\": ";
+  json_str_array(&js, walk.opq_dirs);
+  js += ", \"wh_files\": ";
+  json_str_array(&js, walk.wh_files);
+  js += ", \"pinned\": ";
+  js += p->b.pinned ? "true" : "false";
+  js += "}";
+  *out = p;
+  return TSG_OK;
+}
+
+int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens) {
+  if (!p || !paths || !lens) return fail(TSG_ERR_INVALID, "NULL argument");
+  if (p->path_ptrs.size() != p->b.index.size()) return fail(TSG_ERR_INVALID, "not a layer-tar batch");
+  *paths = p->path_ptrs.data();
+  *lens = p->path_lens.data();
+  return TSG_OK;
+}
+
+const char* tsg_prepared_walk_json(const tsg_prepared* p) { return p ? p->walk_json.c_str() : nullptr; }

@@ -103,6 +103,11 @@ class Engine {
   // rolled word loop + 64-byte lines + temporal loads (layout bits, results
   // valid); the other bits are measurement builds whose results are invalid.
   int k1_abl_ = 464;
+  uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
+  uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
+  bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
+  std::mutex k2s_mu_;
+  std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
   uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)
   double first_piece_ = 0.7;            // resident data: share of the first piece (TSG_FIRST_PIECE)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)

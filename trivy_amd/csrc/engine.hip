@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
     uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ /*item_ctr: v3*/,
-    uint32_t* __restrict__ /*obuf: v3*/) {
+    uint32_t* __restrict__ /*obuf: v3*/, uint32_t /*tail_rounds: v3*/) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | (scan table | class map |
   //              output meta | output list)]
@@ -502,6 +502,10 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
   if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
 }
 
+// kStats (TSG_K2_STATS, measurement): per rule, atomically count the hits,
+// the hits past the keyword gate, the verify starts walked and the bytes
+// walked (k2s[4 * rule + 0..3]).
+template <bool kStats>
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const unsigned long long* __restrict__ hits, const uint32_t* __restrict__ block_hits, uint32_t region_cap,
@@ -509,7 +513,8 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint32_t* __restrict__ rule_kw, const uint32_t* __restrict__ kwbits, uint32_t kw_words,
     const VDfaDev* __restrict__ vd, const uint16_t* __restrict__ v_next,
     const uint8_t* __restrict__ v_acc, const uint8_t* __restrict__ v_cls,
-    CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap) {
+    CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap,
+    unsigned long long* __restrict__ k2s) {
   // K2 workgroup (r, k) verifies region r's hits k*256+tid, stride 256*(grid/nregions)
   const uint32_t r = blockIdx.x % nregions;
   const uint32_t nsub = gridDim.x / nregions;
@@ -521,6 +526,7 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     const AnchorDev an = anchors[h & 0xffffffu];
     const RuleDev r = rules[an.rule];
     const uint32_t f = file_of(offsets, nfiles, q);
+    if (kStats) atomicAdd(&k2s[4 * an.rule], 1ull);
     if (r.mode == 3) {
       // presence anchor of a rule evaluated in full on the host: the hit is
       // the candidate (any one per file suffices)
@@ -540,6 +546,7 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
       }
       if (!g) continue;
     }
+    if (kStats) atomicAdd(&k2s[4 * an.rule + 1], 1ull);
     const long long fstart = static_cast<long long>(offsets[f]);
     const long long fend = static_cast<long long>(offsets[f + 1]);
     const VDfaDev d = vd[r.verify_dfa];
@@ -565,6 +572,10 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
         st = nx[st * d.nclasses + cl[data[p]]];
         if (acc[st]) ok = true;
         else if (st == d.dead) break;
+      }
+      if (kStats) {
+        atomicAdd(&k2s[4 * an.rule + 2], 1ull);
+        atomicAdd(&k2s[4 * an.rule + 3], static_cast<unsigned long long>(p - s + 1));
       }
       if (!ok && st != d.dead && p < fend && p >= lim) ok = true;   // gave up: conservative
       return ok;
@@ -735,7 +746,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
     uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
-    uint32_t* __restrict__ obuf) {
+    uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
   constexpr uint32_t kTabOff = 256;
@@ -779,12 +790,14 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   // Guided work schedule.  A wave item gives each of its 64 lanes a range of
   // kU consecutive chunks, walked as one stream (one warm-up) that stores the
   // '\n' count of every chunk it crosses.  Items come from one counter in
-  // decreasing range size: kU = 4 for the bulk, then one grid-wide round of
-  // kU = 2 and one of kU = 1, so the waves that take the last items finish
-  // after a short item and the launch has no long tail.
+  // decreasing range size: kU = 4 for the bulk, then `tail_rounds` grid-wide
+  // rounds of kU = 2 and as many of kU = 1, so the waves that take the last
+  // items finish after a short item and the launch has no long tail
+  // (measured r2u, 4 GB: 1.29 ms without the short rounds, 1.21 with one
+  // round each, 1.24 / 1.27 with two / four).
   const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
-  const unsigned long long n1 = min(nchunks, W * 64);
-  const unsigned long long n2 = min(nchunks - n1, W * 128);
+  const unsigned long long n1 = min(nchunks, W * 64 * tail_rounds);
+  const unsigned long long n2 = min(nchunks - n1, W * 128 * tail_rounds);
   const unsigned long long n4 = nchunks - n1 - n2;
   const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
   const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
@@ -1026,7 +1039,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
     uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
-    uint32_t* __restrict__ obuf) {
+    uint32_t* __restrict__ obuf, uint32_t /*tail_rounds: v3*/) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int kAbl = kAblTemporal | kAblLine64 | kAblDefer;   // v3's single-stream code for the odd lines
   constexpr uint32_t kWaves = kThreads / 64;
@@ -1270,9 +1283,10 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // at 1 KiB vs 0.56 at 4 KiB (shorter wave items, shorter tail); 2 GB best at
 // 2 KiB; 4 GB and more best at 4 KiB (less warm-up per byte).
 // v3 walks ranges of 1-4 chunks per lane (guided schedule): its chunk is
-// the '\n'-count granularity and the last round's range, 1 KiB.
+// the '\n'-count granularity and the last round's range: 2 KiB for launches
+// of 2 GiB and more (measured r2r: 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB.
 uint32_t k1_chunk_for(uint64_t bytes, int variant) {
-  if (variant == 3) return 1024;
+  if (variant == 3) return bytes >= (2ull << 30) ? 2048 : 1024;
   uint32_t c = 1024;
   while (c < 4096 && static_cast<uint64_t>(c) * (1u << 20) < bytes) c <<= 1;
   return c;
@@ -1334,6 +1348,7 @@ struct Lane {
   uint16_t* d_nl = nullptr; size_t d_nl_cap = 0;   // '\n' per K1 chunk (chunk <= 32 KiB)
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   uint32_t* d_ob = nullptr; size_t d_ob_cap = 0;    // K1 v3 deferred-output slots (kOutSlots per thread)
+  unsigned long long* d_k2s = nullptr;              // TSG_K2_STATS: per-rule K2 counters (4 per rule)
   unsigned int* d_cnt = nullptr;
   std::vector<uint32_t> h_bh;
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
@@ -1378,7 +1393,7 @@ Lane::~Lane() {
   hipSetDevice(device);
   if (compute) hipStreamSynchronize(compute);
   if (copy) hipStreamSynchronize(copy);
-  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt};
+  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
@@ -1609,6 +1624,15 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     }
   }
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // measurement builds of v3 only
+  if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
+    const int v = std::atoi(c);
+    if (v >= 0 && v <= 16) e->k1_tail_rounds_ = static_cast<uint32_t>(v);
+  }
+  if (const char* c = std::getenv("TSG_K2_HITS_PER_THREAD")) {
+    const int v = std::atoi(c);
+    if (v >= 1 && v <= 64) e->k2_hits_per_thread_ = static_cast<uint32_t>(v);
+  }
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
     // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
     // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
@@ -1626,6 +1650,24 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
 }
 
 Engine::~Engine() {
+  if (k2_stats_ && !k2s_.empty()) {
+    // TSG_K2_STATS: per-rule K2 work of every scan of this engine, busiest first
+    std::vector<size_t> order(k2s_.size() / 4);
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return k2s_[4 * a + 3] > k2s_[4 * b + 3]; });
+    std::string js = "{\"k2_stats\": [";
+    bool first = true;
+    for (size_t i : order) {
+      if (k2s_[4 * i] == 0) continue;
+      const std::string id = i < rs_->rules.size() ? rs_->rules[i].id : "exclude-" + std::to_string(i - rs_->rules.size());
+      js += std::string(first ? "" : ", ") + "{\"rule\": \"" + id + "\", \"hits\": " + std::to_string(k2s_[4 * i]) +
+            ", \"gated\": " + std::to_string(k2s_[4 * i + 1]) + ", \"starts\": " + std::to_string(k2s_[4 * i + 2]) +
+            ", \"bytes\": " + std::to_string(k2s_[4 * i + 3]) + "}";
+      first = false;
+    }
+    js += "]}";
+    std::fprintf(stderr, "%s\n", js.c_str());
+  }
   dev_.clear();
   calls_.clear();
 }
@@ -1647,6 +1689,13 @@ Lane* Engine::acquire_lane(DeviceTables& dt, std::string* err) {
     return nullptr;
   }
   for (auto& ev : l->ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
+  if (k2_stats_) {
+    const size_t n = 4 * std::max<size_t>(pf_.rules.size(), 1) * sizeof(unsigned long long);
+    if (hipMalloc(&l->d_k2s, n) != hipSuccess || hipMemset(l->d_k2s, 0, n) != hipSuccess) {
+      *err = "K2 stats buffer";
+      return nullptr;
+    }
+  }
   for (int i = 0; i < 2; ++i) {
     if (hipEventCreate(&l->up_begin[i]) != hipSuccess || hipEventCreate(&l->up_done[i]) != hipSuccess) {
       *err = "hipEventCreate failed";
@@ -1779,10 +1828,11 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t* a_ocnt = ln.d_cnt + 2;
       uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
       uint32_t a_rcap = region_cap;
+      uint32_t a_tail = k1_tail_rounds_;
       void* args[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
-                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob};
+                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
       HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, s));
       ++launches;
     }
@@ -1815,18 +1865,33 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       HIP_OK(hipMemsetAsync(ln.d_cnt + 1, 0, 4, s));
       HIP_OK(hipEventRecord(ln.ev[2], s));
       if (nhits > 0) {
-        // (region, sub-block) grid: enough sub-blocks that the fullest region is done in ~4 strides
-        const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(64, (maxr + 1023) / 1024)));
-        hipLaunchKernelGGL(tsg_k2_verify, dim3(nregions * nsub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
-                           ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words,
-                           dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, static_cast<uint32_t>(ln.cand_cap));
+        // (region, sub-block) grid: k2_hits_per_thread_ hits of the fullest
+        // region per thread (K2 is latency-bound: more threads in flight)
+        const uint64_t per_block = 256ull * k2_hits_per_thread_;
+        const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(256, (maxr + per_block - 1) / per_block)));
+        if (ln.d_k2s)
+          hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+                             ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
+                             dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt,
+                             static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
+        else
+          hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+                             ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
+                             dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt,
+                             static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
         HIP_OK(hipGetLastError());
         if (nover > 0) {                               // the overflow pool as one more region
           const uint32_t osub = static_cast<uint32_t>(std::min<uint64_t>(4096, (nover + 1023) / 1024));
-          hipLaunchKernelGGL(tsg_k2_verify, dim3(osub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
-                             ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
-                             dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
-                             ln.d_cnt, static_cast<uint32_t>(ln.cand_cap));
+          if (ln.d_k2s)
+            hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(osub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+                               ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
+                               dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
+                               ln.d_cnt, static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
+          else
+            hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(osub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+                               ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
+                               dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
+                               ln.d_cnt, static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
           HIP_OK(hipGetLastError());
         }
       }
@@ -1848,6 +1913,14 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       HIP_OK(hipStreamSynchronize(s));
       st->d2h_ms += ms_since(t_d2h);
       st->candidates += c2;
+      if (ln.d_k2s) {
+        std::vector<unsigned long long> h(4 * pf_.rules.size());
+        HIP_OK(hipMemcpy(h.data(), ln.d_k2s, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemset(ln.d_k2s, 0, h.size() * sizeof(unsigned long long)));
+        std::lock_guard<std::mutex> lk(k2s_mu_);
+        if (k2s_.size() < h.size()) k2s_.resize(h.size(), 0);
+        for (size_t i = 0; i < h.size(); ++i) k2s_[i] += h[i];
+      }
       return true;
     }
     *err = "candidate buffer overflow persisted";

@@ -83,22 +83,19 @@ void parallel_for(uint32_t n, int threads, F&& fn) {
   for (auto& th : ts) th.join();
 }
 
-}  // namespace
-
-bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,
-                   uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
-                   PreparedBatch* out, std::string* err) {
-  for (uint32_t i = 0; i < nfiles; ++i) {
-    if (raw_off[i + 1] < raw_off[i]) { *err = "offsets must be non-decreasing"; return false; }
-  }
+// The two passes over nfiles files; file(i) gives (content, size, path).
+template <typename File>
+bool prepare_core(const Ruleset& rs, const std::string& config_path, uint32_t nfiles, File&& file, int threads,
+                  PreparedBatch* out, FeedAlloc alloc) {
   const std::string cfg_base = go_base(config_path);
   // pass 1: keep decision, binary flag and prepared size per file
   std::vector<uint8_t> keep(nfiles), bin(nfiles);
   std::vector<uint64_t> size(nfiles);
   parallel_for(nfiles, threads, [&](uint32_t i) {
-    const std::string path = path_lens ? std::string(paths[i], path_lens[i]) : std::string(paths[i]);
-    const uint8_t* c = raw + raw_off[i];
-    const uint64_t n = raw_off[i + 1] - raw_off[i];
+    const uint8_t* c;
+    uint64_t n;
+    std::string path;
+    file(i, &c, &n, &path);
     keep[i] = 0;
     if (!required(rs, path, n, cfg_base)) return;
     const bool binary = go_is_binary(c, n);                        // secret.go:104-108
@@ -122,13 +119,19 @@ bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint
   }
   // not zero-filled (every byte below offsets[nk] is written in pass 2); only
   // the pad K1 may read past the last file is cleared
-  out->data.reset(new uint8_t[out->offsets[nk] + 64]);
+  const size_t bytes = out->offsets[nk] + 64;
+  void (*free_fn)(uint8_t*) = nullptr;
+  uint8_t* buf = alloc ? alloc(bytes, &free_fn) : nullptr;
+  out->pinned = buf != nullptr;
+  if (buf) out->data = std::shared_ptr<uint8_t>(buf, free_fn);
+  else out->data = std::shared_ptr<uint8_t>(new uint8_t[bytes], std::default_delete<uint8_t[]>());
   std::memset(out->data.get() + out->offsets[nk], 0, 64);
   // pass 2: write ScanArgs.Content (CR stripped, or the printable runs of a .pyc)
   parallel_for(nk, threads, [&](uint32_t k) {
-    const uint32_t i = out->index[k];
-    const uint8_t* c = raw + raw_off[i];
-    const uint64_t n = raw_off[i + 1] - raw_off[i];
+    const uint8_t* c;
+    uint64_t n;
+    std::string path;
+    file(out->index[k], &c, &n, &path);
     uint8_t* d = out->data.get() + out->offsets[k];
     if (out->binary[k]) {
       const std::string p = go_extract_printable(c, n);
@@ -139,6 +142,33 @@ bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint
     for (uint64_t x = 0; x < n; ++x) if (c[x] != '\r') *d++ = c[x];
   });
   return true;
+}
+
+}  // namespace
+
+bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,
+                   uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
+                   PreparedBatch* out, std::string* err, FeedAlloc alloc) {
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    if (raw_off[i + 1] < raw_off[i]) { *err = "offsets must be non-decreasing"; return false; }
+  }
+  return prepare_core(rs, config_path, nfiles, [&](uint32_t i, const uint8_t** c, uint64_t* n, std::string* path) {
+    *c = raw + raw_off[i];
+    *n = raw_off[i + 1] - raw_off[i];
+    *path = path_lens ? std::string(paths[i], path_lens[i]) : std::string(paths[i]);
+  }, threads, out, alloc);
+}
+
+bool prepare_files(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* starts,
+                   const uint64_t* sizes, const std::vector<std::string>& paths, int threads, PreparedBatch* out,
+                   std::string* err, FeedAlloc alloc) {
+  (void)err;
+  return prepare_core(rs, config_path, static_cast<uint32_t>(paths.size()),
+                      [&](uint32_t i, const uint8_t** c, uint64_t* n, std::string* path) {
+                        *c = raw + starts[i];
+                        *n = sizes[i];
+                        *path = paths[i];
+                      }, threads, out, alloc);
 }
 
 }  // namespace tsg

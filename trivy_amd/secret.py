@@ -228,6 +228,58 @@ def PrepareBatch(scanner, files, config_path="", image=False, threads=0):
     return out, idx
 
 
+class WalkError(Exception):
+    """walker.LayerTar.Walk's error ("failed to extract the archive: ...")."""
+
+
+def PrepareLayerTar(scanner, tar, skip_files=(), skip_dirs=(), config_path="", threads=0, pinned=False,
+                    scan=False):
+    """One container layer: walker.LayerTar.Walk (pkg/fanal/walker/tar.go:35-103)
+    over the uncompressed layer tar `tar` (bytes), then SecretAnalyzer.Required
+    + Analyze content prep for every regular file (tsg_prepare_layer_tar).
+    Returns (ScanArgs list with "/"-prefixed image paths, walk dict with
+    "files", "opq_dirs", "wh_files").  scan=True also runs the prepared batch
+    through tsg_scan_batch straight from the prepared (pinned when `pinned`)
+    buffer and returns (ScanArgs list, walk dict, [types.Secret])."""
+    L = _lib.lib()
+    buf = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
+    sf = [s.encode() for s in skip_files]
+    sd = [s.encode() for s in skip_dirs]
+    sfa = (ctypes.c_char_p * max(1, len(sf)))(*sf)
+    sda = (ctypes.c_char_p * max(1, len(sd)))(*sd)
+    h = ctypes.c_void_p()
+    rc = L.tsg_prepare_layer_tar(scanner._rs, (config_path or "").encode(), buf.ctypes.data, len(tar), sfa, len(sf),
+                                 sda, len(sd), threads, 1 if pinned else 0, ctypes.byref(h))
+    if rc != 0:
+        raise WalkError(L.tsg_last_error().decode("utf-8", "replace"))
+    try:
+        walk = json.loads(L.tsg_prepared_walk_json(h).decode("utf-8", "surrogateescape"))
+        d, o, ix, b = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        nk = ctypes.c_uint32()
+        _lib.check(L.tsg_prepared_view(h, ctypes.byref(d), ctypes.byref(o), ctypes.byref(ix), ctypes.byref(b),
+                                       ctypes.byref(nk)))
+        n = nk.value
+        pp, pl = ctypes.POINTER(ctypes.c_char_p)(), ctypes.POINTER(ctypes.c_uint32)()
+        _lib.check(L.tsg_prepared_paths(h, ctypes.byref(pp), ctypes.byref(pl)))
+        offs = np.ctypeslib.as_array(ctypes.cast(o, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy() \
+            if n else np.zeros(1, np.uint64)
+        binf = np.ctypeslib.as_array(ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)), shape=(n,)).tolist() if n else []
+        data = ctypes.string_at(d, int(offs[-1])) if n else b""
+        out = [ScanArgs(ctypes.string_at(pp[k], pl[k]).decode("utf-8", "surrogateescape"),
+                        data[int(offs[k]):int(offs[k + 1])], bool(binf[k])) for k in range(n)]
+        if not scan:
+            return out, walk
+        res = ctypes.c_void_p()
+        _lib.check(L.tsg_scan_batch(scanner.engine(), d, o, n, pp, ctypes.cast(pl, ctypes.c_void_p), b, ctypes.byref(res)))
+        try:
+            secrets = _lib.result_json(res)
+        finally:
+            L.tsg_result_free(res)
+        return out, walk, secrets
+    finally:
+        L.tsg_prepared_free(h)
+
+
 # ---------------------------------------------------------------- test hooks
 def scan_host_reference(scanner, args_list, threads=1):
     """The C++ confirmer on every (file, rule) pair, no prefilter (tests only)."""
