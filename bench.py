@@ -115,6 +115,65 @@ class PinnedBatch:
             self.ptr = ctypes.c_void_p()
 
 
+def layer_tar_rate(L, sc, batch, target_bytes, threads):
+    """tsg_prepare_layer_tar over one PAX layer tar built from the batch's files
+    (rate in tar bytes per second, pinned output)."""
+    import io
+    import tarfile
+    from trivy_amd import _lib
+    buf = io.BytesIO()
+    nfiles, tot = 0, 0
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        for i in range(batch.nfiles):
+            c = batch.file(i)
+            ti = tarfile.TarInfo(batch.paths[i].lstrip("/"))
+            ti.size = len(c)
+            tf.addfile(ti, io.BytesIO(c))
+            nfiles += 1
+            tot += len(c)
+            if tot >= target_bytes:
+                break
+    tar = np.frombuffer(buf.getvalue(), dtype=np.uint8)
+    best, kept = None, 0
+    for _ in range(3):
+        h = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        _lib.check(L.tsg_prepare_layer_tar(sc._rs, b"", tar.ctypes.data, len(tar), None, 0, None, 0, threads, 1,
+                                           ctypes.byref(h)))
+        dt = time.perf_counter() - t0
+        d_, o_, i_, b_, nk = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(),
+                              ctypes.c_uint32())
+        _lib.check(L.tsg_prepared_view(h, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_), ctypes.byref(b_),
+                                       ctypes.byref(nk)))
+        kept = nk.value
+        L.tsg_prepared_free(h)
+        best = dt if best is None else min(best, dt)
+    return len(tar) / best / 1e9, nfiles, kept, best
+
+
+def numa_bind(device):
+    """Pin this rank to the CPUs of its GPU's NUMA node (before the corpus and
+    the pinned batch are allocated, so both are first-touched there and each
+    GPU's DMA reads node-local memory).  Returns what was done, or None."""
+    try:
+        import torch
+        pr = torch.cuda.get_device_properties(device)
+        bdf = "%04x:%02x:%02x.0" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        base = "/sys/bus/pci/devices/" + bdf
+        node = int(open(base + "/numa_node").read().strip())
+        cpus = set()
+        for part in open(base + "/local_cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if node < 0 or len(cpus) < 8:
+            return None
+        os.sched_setaffinity(0, cpus)
+        return {"pci": bdf, "numa_node": node, "cpus": len(cpus)}
+    except Exception:
+        return None
+
+
 def _segment_bytes():
     v = os.environ.get("TSG_SEGMENT_BYTES")
     return int(v) if v and int(v) >= 4096 else 4 << 30
@@ -125,10 +184,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 5],
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="BASELINE.json config: 1 = 1 GB source tree (log-normal sizes), 2 = 10 GB source "
                          "corpus (the metric's workload), 3 = extracted image layers (small files; bytes counted "
-                         "after Required), 5 = 500 custom rules + allow rules + exclude blocks")
+                         "after Required), 4 = 200 GB as 20 config-2 shards split over the ranks (one step streams "
+                         "the rank's shards), 5 = 500 custom rules + allow rules + exclude blocks")
+    ap.add_argument("--distinct-shards", type=int, default=2,
+                    help="config 4: distinct generated shards per rank, cycled over its shards (generation of a "
+                         "10 GB shard takes ~5 s, 20 of them would dominate the run)")
     ap.add_argument("--gb", type=float, default=None, help="corpus GB per GPU (default: 1 for config 1, else 10)")
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--threads", type=int, default=16, help="host confirm threads per rank")
@@ -161,11 +224,12 @@ def main():
     L = _lib.lib()
     device = local_rank
     torch.cuda.set_device(device)
+    numa = numa_bind(device)
 
     # ---------------------------------------------------------------- workload
     t_gen = time.perf_counter()
     cfg_path = None
-    sizes = {1: "lognormal", 2: "loguniform", 3: "small", 5: "lognormal"}[args.config]
+    sizes = {1: "lognormal", 2: "loguniform", 3: "small", 4: "loguniform", 5: "lognormal"}[args.config]
     corpus = synth.generate(int(gb * 1e9), seed=args.seed + rank, sizes=sizes,
                             layout="image" if args.config == 3 else "src")
     if args.config == 5:      # 500 custom rules + allow rules + exclude blocks (+ builtins)
@@ -211,16 +275,49 @@ def main():
     del corpus, paths, lens, _keep
     nfiles, nbytes = batch.nfiles, batch.nbytes
     bin_ptr = batch.binary.ctypes.data if batch.binary is not None else None
+    # config 4: this rank's share of 20 config-2 shards, streamed one after
+    # another from pinned memory (the distinct shards cycled)
+    shard_batches, nshards = [batch], 1
+    if args.config == 4:
+        nshards = -(-20 // world)
+        for j in range(1, min(args.distinct_shards, nshards)):
+            c2 = synth.generate(int(gb * 1e9), seed=args.seed + 1000 * j + rank, sizes=sizes, layout="src")
+            shard_batches.append(PinnedBatch(L, c2.data, c2.offsets, c2.paths))
+            del c2
+        nbytes = sum(shard_batches[k % len(shard_batches)].nbytes for k in range(nshards))
+        log("config 4: %d shards per rank (%d distinct), %.1f GB per rank per step" % (
+            nshards, len(shard_batches), nbytes / 1e9))
+
+    def scan_one(b):
+        res = ctypes.c_void_p()
+        _lib.check(L.tsg_scan_batch(eng, b.ptr, b.offsets.ctypes.data, b.nfiles, b.cpaths, b.clens,
+                                    b.binary.ctypes.data if b.binary is not None else None, ctypes.byref(res)))
+        return res
 
     def step():
-        res = ctypes.c_void_p()
-        _lib.check(L.tsg_scan_batch(eng, batch.ptr, batch.offsets.ctypes.data, nfiles, batch.cpaths, batch.clens,
-                                    bin_ptr, ctypes.byref(res)))
-        return res
+        """One step: the rank's batch (config 4: its shards); returns the last
+        result and the step's stats (summed over shards)."""
+        if nshards == 1:
+            res = scan_one(batch)
+            return res, _lib.result_stats(res)
+        agg = None
+        res = None
+        for k in range(nshards):
+            if res is not None:
+                L.tsg_result_free(res)
+            res = scan_one(shard_batches[k % len(shard_batches)])
+            st = _lib.result_stats(res)
+            if agg is None:
+                agg = dict(st)
+            else:
+                for key in ("k1_ms", "k2_ms", "host_ms", "h2d_ms", "feed_ms", "total_ms", "k1_launches", "pieces",
+                            "hits", "candidates", "confirm_files"):
+                    agg[key] += st[key]
+        return res, agg
 
     # ------------------------------------------------------- timed (pinned host)
     for _ in range(args.warmup):
-        L.tsg_result_free(step())
+        L.tsg_result_free(step()[0])
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -228,8 +325,8 @@ def main():
     last = None
     t0 = time.perf_counter()
     for k in range(args.steps):
-        res = step()
-        stats.append(_lib.result_stats(res))
+        res, st = step()
+        stats.append(st)
         if k == args.steps - 1:
             last = res
         else:
@@ -252,6 +349,9 @@ def main():
     launches = max(1, int(stats[-1]["k1_launches"]))
     segments = max(1, int(stats[-1]["pieces"]))
     groups = max(1, launches // segments)
+    if nshards > 1:                    # config 4: the parity legs below check the first shard's batch
+        L.tsg_result_free(last)
+        last = scan_one(batch)
     gpu_results = _lib.result_json(last)
     L.tsg_result_free(last)
     findings = sum(len(s["Findings"]) for s in gpu_results)
@@ -281,6 +381,9 @@ def main():
            "secrets (87 builtin rules), builtin rules" % gb,
         3: "config3: %.0f GB of extracted-image-layer small files per GPU (mean ~25 KB, rootfs paths), scanned "
            "after Required/IsBinary/CR strip (tsg_prepare_batch), '/'-prefixed image paths, builtin rules" % gb,
+        4: "config4: 200 GB = 20 config-2 shards (%.0f GB each, log-uniform 64 B-64 MB files), %d per GPU streamed "
+           "one after another from pinned memory (%d distinct generated shards cycled), builtin rules" % (
+               gb, nshards, len(shard_batches)),
         5: "config5: %.0f GB synthetic source corpus per GPU, trivy-secret.yaml with 500 custom rules + 87 "
            "builtins, 20 allow rules, 5 exclude blocks" % gb,
     }[args.config]
@@ -308,6 +411,7 @@ def main():
             "host_confirm_threads": args.threads,
             "segment_bytes": _segment_bytes(),
             "config_id": args.config,
+            "numa": numa,
         },
         "roofline": {
             "bound": "hbm",
@@ -341,15 +445,23 @@ def main():
 
     # host-feed ceiling: the same segmented upload with no kernels
     fms = ctypes.c_double()
-    _lib.check(L.tsg_feed_probe(eng, batch.ptr, nbytes, ctypes.byref(fms)))
-    out["host_feed"]["ceiling_gbps"] = round(nbytes / (fms.value / 1e3) / 1e9, 2)
+    _lib.check(L.tsg_feed_probe(eng, batch.ptr, batch.nbytes, ctypes.byref(fms)))
+    out["host_feed"]["ceiling_gbps"] = round(batch.nbytes / (fms.value / 1e3) / 1e9, 2)
     out["host_feed"]["note"] = ("ceiling_gbps: tsg_feed_probe, the step's segmented pinned upload with no kernels; "
                                 "prepare_gbps: tsg_prepare_batch over the raw files")
     log("host-feed ceiling (segmented pinned upload, no kernels): %.1f GB/s" % out["host_feed"]["ceiling_gbps"])
+    if args.config == 3 and rank == 0:
+        # the image path's host feed from a layer tar: walker.LayerTar.Walk +
+        # Required + content prep into pinned memory (tsg_prepare_layer_tar)
+        tgb, tfiles, tkept, tdt = layer_tar_rate(L, sc, batch, 512e6, args.threads)
+        out["host_feed"]["layer_tar_gbps"] = round(tgb, 2)
+        out["host_feed"]["layer_tar_sample"] = "%d files / %.0f MB of this batch written as one PAX layer tar, %d " \
+                                               "kept, best of 3: %.1f ms" % (tfiles, tgb * tdt * 1e3, tkept, tdt * 1e3)
+        log("layer-tar feed (walk + Required + prep into pinned memory, %d threads): %.1f GB/s" % (args.threads, tgb))
 
     if not args.no_resident:
         # the same batch already resident in HBM (reported, never `value`)
-        d_data = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda:%d" % device)
+        d_data = torch.empty(batch.nbytes + 64, dtype=torch.uint8, device="cuda:%d" % device)
         d_data.copy_(torch.from_numpy(batch.view), non_blocking=False)
         torch.cuda.synchronize()
 
@@ -370,8 +482,8 @@ def main():
             L.tsg_result_free(res)
         rdt = (time.perf_counter() - t0) / len(rst)
         rk1 = float(np.mean([s["k1_ms"] for s in rst]))
-        out["resident"] = {"gbps": round(nbytes / rdt / 1e9, 2), "ms_per_step": round(rdt * 1e3, 3),
-                           "k1_ms": round(rk1, 3), "k1_gbps": round(nbytes / (rk1 / 1e3) / 1e9, 2),
+        out["resident"] = {"gbps": round(batch.nbytes / rdt / 1e9, 2), "ms_per_step": round(rdt * 1e3, 3),
+                           "k1_ms": round(rk1, 3), "k1_gbps": round(batch.nbytes / (rk1 / 1e3) / 1e9, 2),
                            "k1_launches": int(rst[-1]["k1_launches"]), "pieces": int(rst[-1]["pieces"]),
                            "k2_ms": round(float(np.mean([s["k2_ms"] for s in rst])), 3),
                            "host_confirm_ms": round(float(np.mean([s["host_ms"] for s in rst])), 3),
@@ -416,7 +528,8 @@ def main():
             "parity diff files: %d (findings in sample: %d)" % (
                 gbps, args.cpu_procs, nb / cdt / 1e9, args.cpu_procs, len(diff), ofind))
 
-    batch.free()
+    for b in shard_batches:
+        b.free()
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -119,3 +119,18 @@ def test_line_numbers_at_chunk_edges_gpu():
     assert sum(len(w["Findings"]) for w in want) > 8000
     for a, g, w in zip(args, got, want):
         assert g == w, a.FilePath
+
+
+def test_geometric_tail_segments_gpu(monkeypatch):
+    # a batch of many small files (image-layer sizes) is uploaded in segments
+    # whose sizes halve toward the end (the confirm work left after the last
+    # upload stays small); every file equals the host confirmer's result
+    c = synth.generate(60_000_000, seed=43, sizes="small", plant_rate=3e-3, layout="image")
+    args = [S.ScanArgs("/" + c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    monkeypatch.setenv("TSG_SEGMENT_MIN", str(4 << 20))
+    got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
+    assert stats["pieces"] >= 4                          # 30, 15, 7.5, 3.75 + rest (MB)
+    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    assert sum(len(w["Findings"]) for w in want) > 100
+    for a, g, w in zip(args, got, want):
+        assert g == w, a.FilePath

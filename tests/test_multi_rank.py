@@ -19,17 +19,19 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, engine=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from trivy_amd import secret as S
     from workload import synth
-    c = synth.generate(300_000, seed=11, sizes="lognormal", plant_rate=2e-3, base_bytes=1 << 20)
+    c = synth.generate(300_000 if not engine else 8_000_000, seed=11, sizes="lognormal", plant_rate=2e-3,
+                       base_bytes=1 << 20)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
-    sc = S.Scanner(None)
-    mine, res, full = shard.scan_sharded(args, lambda a: S.scan_table_model(sc, a), rank, world)
+    sc = S.Scanner(None, device=0) if engine else S.Scanner(None)
+    scan = (lambda a: sc.ScanBatch(a)) if engine else (lambda a: S.scan_table_model(sc, a))
+    mine, res, full = shard.scan_sharded(args, scan, rank, world)
     if rank == 0:
         q.put(full)
     dist.barrier()
@@ -63,3 +65,28 @@ def test_two_gloo_ranks_match_single_process():
     want = S.scan_table_model(S.Scanner(None), args)
     assert full == want
     assert sum(len(w["Findings"]) for w in want) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_gloo_ranks_engines_gpu():
+    # bench.py's N>1 layout on one card: two processes, each with its own
+    # engine (both on device 0 here, one per GPU on a node), LPT shards, no
+    # collective on file data; the gathered result equals one process's scan
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, True)) for r in range(2)]
+    for p in ps:
+        p.start()
+    full = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from trivy_amd import secret as S
+    from workload import synth
+    c = synth.generate(8_000_000, seed=11, sizes="lognormal", plant_rate=2e-3, base_bytes=1 << 20)
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    want = S.Scanner(None).ScanBatch(args)
+    assert full == want
+    assert sum(len(w["Findings"]) for w in want) > 20

@@ -68,6 +68,7 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
 constexpr uint32_t kWaveHits = kK1WaveHits;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
+constexpr double kDenseFilesPerGB = 8000.0;   // upload segmentation: "many small files" (image layers: ~48k/GB)
 constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [2] overflow, [3] v4 LDS-base error, [4 + g] v3/v4 items of group g
 
 // Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
@@ -1608,6 +1609,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const long long v = std::atoll(c);
     if (v >= 4096) e->segment_ = static_cast<uint64_t>(v);
   }
+  if (const char* c = std::getenv("TSG_SEGMENT_MIN")) {
+    const long long v = std::atoll(c);
+    if (v >= 4096) e->segment_min_ = static_cast<uint64_t>(v);
+  }
   if (const char* c = std::getenv("TSG_SEGMENT_TAIL")) {
     const long long v = std::atoll(c);
     if (v >= 0) e->segment_tail_ = static_cast<uint64_t>(v);
@@ -2160,6 +2165,16 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         if (f > cut.back() && f < in.nfiles) cut.push_back(f);
       }
     } else {
+      // Geometric tail: the work left after the last upload is the last
+      // segment's K1/K2 and host confirmation.  For batches whose confirm
+      // cost per byte is high (many small files: image layers, config 5) or
+      // that are too small for several full segments, the rest after the full
+      // segments is cut in halves down to segment_min_, so the last segment
+      // is small and every upload overlaps the previous segment's work.
+      // Large-file batches keep full segments (K1 runs at its large-launch
+      // rate and their confirmation is cheap).
+      const bool dense = static_cast<double>(in.nfiles) * 1e9 > kDenseFilesPerGB * static_cast<double>(total);
+      const bool geometric = dense || total < 2 * segment_;
       for (uint32_t f = 0; f < in.nfiles;) {
         // next cut: the first file boundary at or past segment_ bytes from
         // here; optionally (segment_tail_ > 0) the batch ends in a short
@@ -2170,6 +2185,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         const uint64_t tail = std::min(segment_tail_, segment_ / 8);
         uint64_t target;
         if (rest > segment_ + tail) target = in.offsets[f] + segment_;
+        else if (geometric && rest / 2 >= segment_min_) target = in.offsets[f] + rest / 2;
         else if (tail > 0 && rest > 2 * tail) target = total - tail;
         else break;
         uint32_t g = static_cast<uint32_t>(std::lower_bound(in.offsets + f, in.offsets + in.nfiles, target) - in.offsets);
