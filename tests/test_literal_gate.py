@@ -87,3 +87,37 @@ def test_builtin_allow_paths_gated(p):
     for t in PATHS:
         g, pl, h = _probe(p, t)
         assert h > 0 and g == pl, (p, t)
+
+
+@pytest.mark.parametrize("cfg", ["builtin", "config5"])
+def test_indexed_allow_path_equals_oracle(tmp_path, cfg):
+    # Scanner.AllowPath through the first-byte index of the global allow
+    # rules' gate literals (global_allow_path) equals the oracle's loop over
+    # every allow rule, on image / source paths built around each rule's
+    # literals, with case variants and near misses
+    import random
+
+    from oracle import secret_oracle as so
+    from trivy_amd import secret as S
+    from workload import synth
+    cfg_path = None
+    if cfg == "config5":
+        c5, _ = synth.config5(500, seed=3)
+        cfg_path = str(tmp_path / "c5.yaml")
+        synth.write_yaml(c5, cfg_path)
+    sc = S.Scanner(S.ParseConfig(cfg_path) if cfg_path else None)
+    ref = so.Scanner(so.parse_config(cfg_path) if cfg_path else None)
+    rng = random.Random(9)
+    parts = ["usr", "share", "include", "lib", "local", "go", "python3.11", "gems", "src", "wordpress", "var", "log",
+             "anaconda", "opt", "yarn-v1.22.19", "vendor", "locale", "locales", "test", "Test", "TEST", "example",
+             "EXAMPLE", "app", "a_test", "x-test", "y.test", "README.md", "doc.MD", "main.go", "node_modules", "tmp"]
+    paths = []
+    for _ in range(4000):
+        p = "/".join(rng.choice(parts) for _ in range(rng.randrange(1, 6)))
+        if rng.random() < 0.5:
+            p = "/" + p
+        paths.append(p)
+    paths += ["usr/share/x", "/usr/share/x", "opt/yarn-v1.2/x", "usr/local/lib/python3.11/x", "a.md", "a.mdx", "",
+              "test", "atest", "/test", "examplE", "x/vendor/y", "x/vendorz/y"]
+    for p in paths:
+        assert sc.AllowPath(p) == ref.allow_path(p), p

@@ -9,7 +9,9 @@ import json
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrivysecret.so")
+# TSG_LIB (measurement only): an alternative in-tree build, e.g.
+# trivy_amd/libtrivysecret_a.so, to compare two builds on one box
+LIB_PATH = os.path.join(_HERE, os.environ.get("TSG_LIB", "libtrivysecret.so"))
 
 c_char_pp = ctypes.POINTER(ctypes.c_char_p)
 

@@ -86,10 +86,7 @@ const char* tsg_ruleset_rule_id(const tsg_ruleset* rs, int i) {
 
 int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len) {
   if (!rs) return fail(TSG_ERR_INVALID, "ruleset is NULL");
-  for (const auto& a : rs->rs->allow_rules) {
-    if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path), len)) return 1;
-  }
-  return 0;
+  return global_allow_path(*rs->rs, reinterpret_cast<const uint8_t*>(path), len) ? 1 : 0;
 }
 
 int tsg_device_count(void) { return device_count(); }

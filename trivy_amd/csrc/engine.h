@@ -105,7 +105,8 @@ class Engine {
   int k1_abl_ = 464;
   uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
   uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
-  bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
+  bool k2_stats_ = false;
+  bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
   std::mutex k2s_mu_;
   std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
   uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)

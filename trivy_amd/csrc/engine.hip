@@ -1630,6 +1630,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   }
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // measurement builds of v3 only
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
     const int v = std::atoi(c);
     if (v >= 0 && v <= 16) e->k1_tail_rounds_ = static_cast<uint32_t>(v);
@@ -1988,6 +1989,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
   const Ruleset& rs = *rs_;
   const size_t nr = rs.rules.size();
   const size_t nplan = pf_.rules.size();   // rules + exclude-block pseudo-rules
+  const auto t_begin = std::chrono::steady_clock::now();
   // group candidates per file (counting sort by file, then sort each file's list)
   std::vector<uint32_t> per_file(in.nfiles + 1, 0);
   for (const CandDev& c : g.cands) per_file[c.file + 1]++;
@@ -2019,7 +2021,6 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
   std::atomic<uint32_t> next{0};
   std::atomic<uint64_t> nfind{0}, nconf{0};
   auto light_files = [&]() {
-    std::string path;
     for (;;) {
       const uint32_t b = next_light.fetch_add(1);
       if (b >= nlight_blocks) break;
@@ -2027,13 +2028,9 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
       for (size_t k = static_cast<size_t>(b) * kLightBlock; k < e; ++k) {
         const uint32_t f = light[k];
         // no candidates, no host-evaluated rule: only the global allow-path outcome remains
-        if (in.path_lens) path.assign(in.paths[f], in.path_lens[f]); else path.assign(in.paths[f]);
-        for (const auto& a : rs.allow_rules) {
-          if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) {
-            results[f].file_path = path;
-            break;
-          }
-        }
+        const char* p = in.paths[f];
+        const size_t pn = in.path_lens ? in.path_lens[f] : std::strlen(p);
+        if (global_allow_path(rs, reinterpret_cast<const uint8_t*>(p), pn)) results[f].file_path.assign(p, pn);
       }
     }
   };
@@ -2099,11 +2096,21 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
   // while GPU passes are in flight one core stays with each thread driving
   // them (a preempted driver thread stalls its GPU)
   const int active = gpu_in_flight && nt > 1 ? nt - 1 : nt;
+  const double t_setup = ms_since(t_begin);
+  std::atomic<uint64_t> work_us{0}, light_us{0};
   cc.pool->run([&](int idx) {
     if (idx >= active) return;
+    auto a = std::chrono::steady_clock::now();
     worker();
+    auto b = std::chrono::steady_clock::now();
     light_files();
+    work_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(b - a).count());
+    light_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - b).count());
   });
+  if (host_profile_)
+    std::fprintf(stderr, "[tsg host] files %u (work %zu, light %zu) cands %zu: setup %.2f ms, wall %.2f ms, "
+                 "work %.1f + light %.1f thread-ms on %d threads\n", in.nfiles, work.size(), light.size(),
+                 g.cands.size(), t_setup, ms_since(t_begin), work_us.load() / 1e3, light_us.load() / 1e3, active);
   *nconf_out += nconf.load();
   *nfind_out += nfind.load();
 }

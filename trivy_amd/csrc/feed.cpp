@@ -57,9 +57,7 @@ bool required(const Ruleset& rs, const std::string& path, uint64_t size, const s
   if (cfg_base == path) return false;                              // secret.go:178-180
   const std::string ext = go_ext(name);
   for (const char* se : kSkipExts) if (ext == se) return false;
-  for (const auto& a : rs.allow_rules)                             // scanner.AllowPath (scanner.go:205-212)
-    if (a.path && a.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) return false;
-  return true;
+  return !global_allow_path(rs, path);                             // scanner.AllowPath (scanner.go:205-212)
 }
 
 // fn(i) for i in [0, n) on `threads` threads, files handed out dynamically

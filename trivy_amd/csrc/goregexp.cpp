@@ -1240,6 +1240,8 @@ int span_shape(const Node& ast, std::string* l1, std::string* l2) {
 
 }  // namespace
 
+static bool begins_with_text_start(const Node& n);
+
 std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string* err) {
   static std::atomic<uint64_t> next_id{1};
   auto re = std::unique_ptr<Regexp>(new Regexp());
@@ -1258,28 +1260,26 @@ std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string*
   re->nullable_ = f.nullable;
   compute_first(&re->prog_);
   re->span_shape_ = span_shape(*re->ast_, &re->span_l1_, &re->span_l2_);
+  re->start_anchored_ = begins_with_text_start(*re->ast_);
   return re;
 }
 
 bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored, int ncap_wanted,
                       Cap* caps) const {
   if (prog_.start == 0) return false;
-  // one Machine per (thread, Regexp): keyed by the Regexp's unique id
-  thread_local std::vector<std::pair<uint64_t, std::unique_ptr<Machine>>> cache;
-  Machine* m = nullptr;
-  for (auto& e : cache) {
-    if (e.first == id_) { m = e.second.get(); break; }
-  }
+  // one Machine per (thread, Regexp): a direct-mapped per-thread cache keyed
+  // by the Regexp's unique (sequential) id -- one probe per call, where a
+  // scan over every cached regexp cost more than the match itself on the
+  // short paths of image layers
+  constexpr size_t kSlots = 4096;
+  thread_local std::vector<std::pair<uint64_t, std::unique_ptr<Machine>>> cache(kSlots);
+  auto& slot = cache[id_ & (kSlots - 1)];
   (void)ncap_wanted;
-  const int ncap = 2 * (prog_.num_cap + 1);
-  std::unique_ptr<Machine> own;
-  if (!m) {
-    own.reset(new Machine(prog_, ncap));
-    m = own.get();
-    if (cache.size() > 4096) cache.clear();
-    cache.emplace_back(id_, std::move(own));
+  if (slot.first != id_ || !slot.second) {
+    slot.second.reset(new Machine(prog_, 2 * (prog_.num_cap + 1)));
+    slot.first = id_;
   }
-  return m->match(text, len, pos, anchored, caps);
+  return slot.second->match(text, len, pos, anchored, caps);
 }
 
 long Regexp::match_end(const uint8_t* text, size_t len, size_t pos) const {
@@ -1342,31 +1342,73 @@ static size_t seq_at(const std::vector<std::vector<std::string>>& seq, const uin
   return p - i;
 }
 
+// Every match of n starts at the beginning of the text: n begins with
+// BeginText (Go's ^ without (?m), \A) on every alternative.
+static bool begins_with_text_start(const Node& n) {
+  switch (n.op) {
+    case Op::BeginText: return true;
+    case Op::Capture:
+    case Op::Concat: return !n.sub.empty() && begins_with_text_start(*n.sub[0]);
+    case Op::Alternate:
+      if (n.sub.empty()) return false;
+      for (const auto& s : n.sub) if (!begins_with_text_start(*s)) return false;
+      return true;
+    default: return false;
+  }
+}
+
+bool Regexp::gate_hit_at(const uint8_t* text, size_t len, size_t i) const {
+  if (gate_.empty()) return true;
+  if (i >= len || !gate_first_[text[i]]) return false;
+  for (const auto& seq : gate_) if (seq_at(seq, text, len, i)) return true;
+  return false;
+}
+
 bool Regexp::match_string(const uint8_t* text, size_t len) const {
   if (gate_.empty()) {
-    std::vector<Cap> caps(2 * (prog_.num_cap + 1));
-    return match_at(text, len, 0, false, 0, caps.data());
+    thread_local std::vector<Cap> caps0;
+    caps0.resize(2 * (prog_.num_cap + 1));
+    return match_at(text, len, 0, false, 0, caps0.data());
   }
   auto hit_at = [&](size_t i) {
     if (!gate_first_[text[i]]) return false;
     for (const auto& seq : gate_) if (seq_at(seq, text, len, i)) return true;
     return false;
   };
+  if (start_anchored_) {
+    // a match can only start at 0, so its gate literal lies at
+    // gate_dmin_..gate_dmax_ (bounded) or anywhere (unbounded)
+    const size_t hi = gate_bounded_ ? std::min<size_t>(gate_dmax_ + 1, len) : len;
+    bool hit = false;
+    for (size_t i = gate_bounded_ ? gate_dmin_ : 0; i < hi && !hit; ++i) hit = hit_at(i);
+    if (!hit) return false;
+    thread_local std::vector<Cap> caps2;
+    caps2.resize(2 * (prog_.num_cap + 1));
+    return match_at(text, len, 0, true, 0, caps2.data());
+  }
   if (!gate_bounded_) {
     for (size_t i = 0; i < len; ++i) {
       if (hit_at(i)) {
-        std::vector<Cap> caps(2 * (prog_.num_cap + 1));
-        return match_at(text, len, 0, false, 0, caps.data());
+        thread_local std::vector<Cap> caps1;
+        caps1.resize(2 * (prog_.num_cap + 1));
+        return match_at(text, len, 0, false, 0, caps1.data());
       }
     }
     return false;                                  // no gate literal: no match can exist
   }
-  // every match starts gate_dmin_..gate_dmax_ bytes before a gate literal
-  std::vector<uint8_t> tried;
-  std::vector<Cap> caps;
+  // every match starts gate_dmin_..gate_dmax_ bytes before a gate literal;
+  // starts already tried are skipped (a per-thread scratch, no allocation
+  // per call)
+  thread_local std::vector<uint8_t> tried;
+  thread_local std::vector<Cap> caps;
+  bool first = true;
   for (size_t i = gate_dmin_; i < len; ++i) {
     if (!hit_at(i)) continue;
-    if (tried.empty()) { tried.assign(len + 1, 0); caps.resize(2 * (prog_.num_cap + 1)); }
+    if (first) {
+      first = false;
+      tried.assign(len + 1, 0);
+      caps.resize(2 * (prog_.num_cap + 1));
+    }
     const size_t lo = i >= gate_dmax_ ? i - gate_dmax_ : 0, hi = i - gate_dmin_;
     for (size_t s0 = lo; s0 <= hi; ++s0) {
       if (tried[s0]) continue;

@@ -143,6 +143,10 @@ class Regexp {
       for (const auto& alt : seq[0]) gate_first_[static_cast<uint8_t>(alt[0])] = 1;
   }
   const LitGate& gate() const { return gate_; }
+  bool has_gate() const { return !gate_.empty(); }
+  const uint8_t* gate_first() const { return gate_first_; }   // first bytes of the gate literals
+  // Some gate literal occurs at text[i..] (always true without a gate).
+  bool gate_hit_at(const uint8_t* text, size_t len, size_t i) const;
   // Regexp.FindAll(Submatch)Index(text, -1): flattened vectors of 2 (or 2*(ncap+1)) ints.
   void find_all(const uint8_t* text, size_t len, bool submatch, std::vector<Cap>* out) const;
   // Minimal byte length of a match (used by the prefilter to reject nullable rules).
@@ -156,6 +160,7 @@ class Regexp {
   bool nullable_ = false;
   uint64_t id_ = 0;
   LitGate gate_;
+  bool start_anchored_ = false;     // every match starts at text offset 0 (leading \A / non-multiline ^)
   uint8_t gate_first_[256] = {};    // first bytes of the gate literals
   bool gate_bounded_ = false;
   uint32_t gate_dmin_ = 0, gate_dmax_ = 0;

@@ -1,5 +1,7 @@
 // Exact restatement of pkg/fanal/secret/scanner.go on the host (see scanner.h).
 #include "scanner.h"
+
+#include <array>
 #include "gosort.h"
 #include "prefilter.h"
 
@@ -135,6 +137,77 @@ void index_excludes(Ruleset* rs) {
 
 }  // namespace
 
+// Ruleset::AllowPathIndex: the literals of every global allow-path regex's
+// gate (each unit's alternatives expanded, at most kMaxLits per regex; a
+// regex past that or without a gate is always run) in one Aho-Corasick DFA.
+static void build_allow_index(Ruleset* rs) {
+  Ruleset::AllowPathIndex& ix = rs->allow_index;
+  ix = Ruleset::AllowPathIndex();
+  if (rs->allow_rules.size() > 64) return;
+  constexpr size_t kMaxLits = 512, kMaxStates = 4096;
+  std::vector<std::array<int32_t, 256>> go(1);
+  go[0].fill(-1);
+  std::vector<uint64_t> out(1, 0);
+  for (size_t j = 0; j < rs->allow_rules.size(); ++j) {
+    const auto& path = rs->allow_rules[j].path;
+    if (!path) continue;
+    std::vector<std::string> lits;
+    bool ok = path->has_gate();
+    for (const auto& seq : path->gate()) {
+      if (!ok) break;
+      std::vector<std::string> cur{""};
+      for (const auto& unit : seq) {
+        std::vector<std::string> nx;
+        for (const auto& c : cur)
+          for (const auto& alt : unit) nx.push_back(c + alt);
+        if (nx.size() > kMaxLits) { ok = false; break; }
+        cur.swap(nx);
+      }
+      if (ok) lits.insert(lits.end(), cur.begin(), cur.end());
+      if (lits.size() > kMaxLits) ok = false;
+    }
+    if (!ok || lits.empty()) { ix.always |= 1ull << j; continue; }
+    for (const auto& l : lits) {
+      int32_t st = 0;
+      for (unsigned char c : l) {
+        if (go[st][c] < 0) {
+          go[st][c] = static_cast<int32_t>(go.size());
+          go.emplace_back();
+          go.back().fill(-1);
+          out.push_back(0);
+        }
+        st = go[st][c];
+      }
+      out[st] |= 1ull << j;
+    }
+    if (go.size() > kMaxStates) return;    // unusable: the plain loop
+  }
+  // BFS: failure links folded into a full DFA
+  const size_t ns = go.size();
+  ix.next.assign(ns * 256, 0);
+  std::vector<int32_t> fail(ns, 0), order;
+  for (int c = 0; c < 256; ++c) {
+    const int32_t t = go[0][c];
+    if (t >= 0) { fail[t] = 0; order.push_back(t); ix.next[c] = static_cast<uint16_t>(t); }
+  }
+  for (size_t k = 0; k < order.size(); ++k) {
+    const int32_t s = order[k];
+    out[s] |= out[fail[s]];
+    for (int c = 0; c < 256; ++c) {
+      const int32_t t = go[s][c];
+      if (t >= 0) {
+        fail[t] = ix.next[static_cast<size_t>(fail[s]) * 256 + c];
+        order.push_back(t);
+        ix.next[static_cast<size_t>(s) * 256 + c] = static_cast<uint16_t>(t);
+      } else {
+        ix.next[static_cast<size_t>(s) * 256 + c] = ix.next[static_cast<size_t>(fail[s]) * 256 + c];
+      }
+    }
+  }
+  ix.out = std::move(out);
+  ix.usable = true;
+}
+
 bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
   std::vector<Rule> b_rules;
   std::vector<AllowRule> b_allow;
@@ -189,7 +262,29 @@ bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
   for (auto& a : custom_allow) if (!contains(disable_allow, a.id)) out->allow_rules.push_back(a);
   out->exclude_block = std::move(excl);
   index_excludes(out);
+  build_allow_index(out);
   return true;
+}
+
+bool global_allow_path(const Ruleset& rs, const uint8_t* p, size_t n) {
+  const Ruleset::AllowPathIndex& ix = rs.allow_index;
+  if (!ix.usable) {
+    for (const auto& r : rs.allow_rules)
+      if (r.path && r.path->match_string(p, n)) return true;
+    return false;
+  }
+  uint64_t cand = ix.always;
+  uint32_t st = 0;
+  for (size_t i = 0; i < n; ++i) {
+    st = ix.next[st * 256u + p[i]];
+    cand |= ix.out[st];
+  }
+  while (cand) {                       // a rule none of whose gate literals occurs cannot match
+    const int j = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    if (rs.allow_rules[j].path->match_string(p, n)) return true;
+  }
+  return false;
 }
 
 // ---------------------------------------------------------------- helpers
@@ -691,7 +786,7 @@ bool keywords_match_raw(const Rule& r, const uint8_t* content, size_t len, Lower
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl) {
   Secret out;
-  if (allow_path(rs.allow_rules, path)) { out.file_path = path; return out; }   // scanner.go:381-386
+  if (global_allow_path(rs, path)) { out.file_path = path; return out; }   // scanner.go:381-386
   std::string lower;
   bool have_lower = false;
   auto lowered = [&]() -> const std::string& {

@@ -41,7 +41,27 @@ struct Ruleset {                         // scanner.go:45-49 (Global)
   // by exclude id.  The prefilter treats exclude id k as pseudo-rule
   // rules.size() + k, so block locations come from GPU candidates too.
   std::vector<const re::Regexp*> excludes;
+  // The global allow-path regexes indexed by the first bytes of their gate
+  // literals: AllowPath over hundreds of thousands of image paths makes one
+  // pass over each path to find the few regexes worth running
+  // (global_allow_path).  Built by build_ruleset.
+  struct AllowPathIndex {
+    // Aho-Corasick DFA over every gate literal (case variants expanded) of
+    // every global allow-path regex: out[s] = rules with a literal ending in
+    // state s (suffix links folded in)
+    std::vector<uint16_t> next;  // nstates x 256
+    std::vector<uint64_t> out;
+    uint64_t always = 0;         // allow rules with a path regex but no (expandable) gate
+    bool usable = false;         // <= 64 allow rules and the automaton fits
+  } allow_index;
 };
+
+// Scanner.AllowPath (scanner.go:205-212): some global allow rule's path regex
+// matches `path`; equals the loop over rs.allow_rules.
+bool global_allow_path(const Ruleset& rs, const uint8_t* path, size_t n);
+inline bool global_allow_path(const Ruleset& rs, const std::string& path) {
+  return global_allow_path(rs, reinterpret_cast<const uint8_t*>(path.data()), path.size());
+}
 
 // ParseConfig (already decoded from YAML to JSON) + NewScanner: builtin rules
 // and allow rules, enable/disable filters, custom rules appended
