@@ -295,9 +295,10 @@ __device__ __forceinline__ void k1_word_emit(const K1Ctx& x, K1Stream& t, uint32
   }
 }
 
-__device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned long long c0, uint32_t warm_lines) {
+// warm_bytes: a multiple of the kernel's line size (v1 / v4: 128 B, v3: 64 B)
+__device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned long long c0, uint32_t warm_bytes) {
   t.emit = c0;
-  t.p = c0 > warm_lines * 128ull ? c0 - warm_lines * 128ull : 0;   // c0 is a multiple of 128
+  t.p = c0 > warm_bytes ? c0 - warm_bytes : 0;   // c0 is a multiple of 128
   t.s = 0;
   t.p12 = 0;
   t.nl = 0;
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan(
     if (wi < nwork) {
       K1Stream S[kS];
 #pragma unroll
-      for (int j = 0; j < kS; ++j) k1_init(x, S[j], min((wi * kS + j) * chunk, total), warm_lines);
+      for (int j = 0; j < kS; ++j) k1_init(x, S[j], min((wi * kS + j) * chunk, total), warm_lines * 128u);
       for (;;) {
         bool any = false, all_fast = true;
 #pragma unroll
@@ -820,7 +821,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const unsigned long long c = c0 + lane * kU;                 // the lane's first chunk
     if (c < rend) {
       K1Stream t;
-      k1_init(x, t, min(c * chunk, total), warm_lines);
+      // v3 warms up over whole lines of its own size (warm_lines counts them)
+      k1_init(x, t, min(c * chunk, total), warm_lines * ((kAbl & kAblLine64) ? 64u : 128u));
       t.end = min(min(c + kU, rend) * chunk, total);
       t.cend = min(t.emit + chunk, t.end);
       t.ci = c;
@@ -1098,8 +1100,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
     const unsigned long long ca = item * 128 + 2 * lane;       // stream a's chunk; b's is ca + 1
     if (ca < nchunks) {
       K1Stream ta, tb;
-      k1_init(x, ta, min(ca * chunk, total), warm_lines);
-      k1_init(x, tb, min((ca + 1) * chunk, total), warm_lines);
+      k1_init(x, ta, min(ca * chunk, total), warm_lines * 128u);
+      k1_init(x, tb, min((ca + 1) * chunk, total), warm_lines * 128u);
       OutBuf oa{obuf + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
       OutBuf ob{obuf + static_cast<size_t>(nthreads) * kOutSlotsV4 + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
       v4u la[kW], lb[kW];
@@ -1306,7 +1308,7 @@ struct K1Group {
   OutMeta* meta = nullptr;
   uint32_t* list = nullptr;
   uint32_t nmeta = 0, nlist = 0, table_words16 = 0, stride = 0, ostride = 0, nclasses = 0, first_out = 0;
-  uint32_t kw_base = 0, warm_lines = 0;
+  uint32_t kw_base = 0, warm_lines = 0, warm_lines64 = 0;
   size_t meta_bytes = 0;
   bool in_lds = false;
 };
@@ -1438,7 +1440,8 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     g.first_out = fo * stride;
     g.kw_base = sd.kw_base;
     const uint32_t warm = sd.max_pattern_bytes > 0 ? sd.max_pattern_bytes - 1 : 0;
-    g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk
+    g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk (v1, v4)
+    g.warm_lines64 = (warm + 63) / 64;          // v3 (64-byte lines): whole 64-byte lines
     // entries hold the next state's row offset: the DFA chain is then one
     // add + one LDS read per byte (no multiply)
     if (k1_table_words16(sd) > 65535) {
@@ -1820,7 +1823,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
       uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
-      uint32_t a_warm = g.warm_lines;
+      const bool v3_line64 = k1_var(g) == 3 && (k1_abl_ & kAblLine64);
+      uint32_t a_warm = v3_line64 ? g.warm_lines64 : g.warm_lines;
       unsigned long long a_nchunks = nchunks;
       uint32_t a_chunk = kChunk;
       uint32_t a_kww = dt.kw_words, a_kwbase = g.kw_base, a_primary = gi == 0;
