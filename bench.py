@@ -491,7 +491,32 @@ def main():
                            "note": "the same batch already in HBM (tsg_scan_batch_resident)"}
         log("HBM-resident: %.1f GB/s (%.2f ms/step, K1 %.2f ms = %.0f GB/s), same findings: %s" % (
             out["resident"]["gbps"], rdt * 1e3, rk1, out["resident"]["k1_gbps"], same))
-        del d_data
+        # GPU-side CR strip (tsg_strip_cr_device) over a copy
+        # of this batch with every '\n' turned into '\r' (CRLF density: the
+        # kernel's work depends on where the CRs are, not on the other bytes);
+        # reported beside the scan, never `value`
+        d_cr = d_data.clone()
+        d_cr.masked_fill_(d_cr == 10, 13)
+        d_off = torch.from_numpy(batch.offsets.astype(np.int64)).to("cuda:%d" % device)
+        cms = []
+        for _ in range(4):
+            d_dst, _noff, stripped, kms = sc.StripCR(d_cr, d_off, nfiles, batch.nbytes)
+            cms.append(kms)
+            del d_dst, _noff
+        cms = float(np.mean(cms[1:]))
+        algo = batch.nbytes + stripped
+        out["cr_strip"] = {
+            "bytes": batch.nbytes, "stripped_bytes": stripped, "ms": round(cms, 3),
+            "gbps": round(batch.nbytes / (cms / 1e3) / 1e9, 1),
+            "roofline": {"bound": "hbm", "achieved": round(algo / (cms / 1e3) / 1e9, 1), "peak": 8000.0,
+                         "unit": "GB/s", "frac": round(algo / (cms / 1e3) / 1e9 / 8000.0, 3),
+                         "design_traffic": batch.nbytes * 2 + stripped},
+            "note": "four kernels (count, first-file, scan, compact), HIP events; algorithmic bytes = read N + write "
+                    "N'; the count pass reads N once more (design_traffic)"}
+        log("GPU CR strip: %.1f GB in %.2f ms = %.0f GB/s of input (%.2f of HBM roofline on N + N')" % (
+            batch.nbytes / 1e9, cms, out["cr_strip"]["gbps"], out["cr_strip"]["roofline"]["frac"]))
+        del d_cr, d_off, d_data
+        torch.cuda.empty_cache()
 
     failed = False
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

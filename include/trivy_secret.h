@@ -163,6 +163,20 @@ int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_d
  * wall time.  Reported beside scan rates, never used by a scan. */
 int tsg_feed_probe(tsg_engine* e, const uint8_t* data, uint64_t bytes, double* ms);
 
+/* GPU-side CR strip of a device-resident batch of TEXT files: the analyzer's
+ *   content = bytes.ReplaceAll(content, []byte("\r"), []byte(""))
+ * (pkg/fanal/analyzer/secret/secret.go:121) for every file at once.  Replaces
+ * the host-side strip of tsg_prepare_batch for a feed that uploads files as
+ * read.  d_src / d_dst: 16-byte aligned device buffers of >= total bytes on
+ * the engine's first device (not overlapping); d_offsets: nfiles + 1 device
+ * uint64, nondecreasing, d_offsets[0] = 0, d_offsets[nfiles] = total (checked);
+ * d_new_offsets: nfiles + 1 device uint64 receiving each file's start in
+ * d_dst.  *out_total = stripped bytes (= d_new_offsets[nfiles]); *ms (may be
+ * NULL) = kernel time.  Synchronous.  Binary files (ExtractPrintableBytes)
+ * stay on the host path. */
+int tsg_strip_cr_device(tsg_engine* e, const void* d_src, const uint64_t* d_offsets, uint32_t nfiles,
+                        uint64_t total, void* d_dst, uint64_t* d_new_offsets, uint64_t* out_total, double* ms);
+
 uint32_t tsg_result_num_files(const tsg_result* r);
 /* types.Secret.FilePath of file i ("" for types.Secret{}) */
 int tsg_result_file_path(const tsg_result* r, uint32_t file, const char** path, size_t* len);

@@ -56,6 +56,9 @@ SIGNATURES = [
                                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_feed_probe", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_double)]),
+    ("tsg_strip_cr_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]),
     ("tsg_result_num_files", ctypes.c_uint32, [ctypes.c_void_p]),
     ("tsg_result_file_path", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
                                              ctypes.POINTER(ctypes.c_size_t)]),

@@ -180,6 +180,16 @@ int tsg_feed_probe(tsg_engine* e, const uint8_t* data, uint64_t bytes, double* m
   return TSG_OK;
 }
 
+int tsg_strip_cr_device(tsg_engine* e, const void* d_src, const uint64_t* d_offsets, uint32_t nfiles, uint64_t total,
+                        void* d_dst, uint64_t* d_new_offsets, uint64_t* out_total, double* ms) {
+  if (!e || !d_offsets || !d_new_offsets || !out_total) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string err;
+  if (!e->eng->strip_cr(d_src, d_offsets, nfiles, total, d_dst, d_new_offsets, out_total, ms, &err))
+    return fail(err.find("CR strip:") == 0 || err.find("aligned") != std::string::npos ? TSG_ERR_INVALID : TSG_ERR_HIP,
+                err);
+  return TSG_OK;
+}
+
 uint32_t tsg_result_num_files(const tsg_result* r) { return r ? static_cast<uint32_t>(r->files.size()) : 0; }
 
 int tsg_result_file_path(const tsg_result* r, uint32_t f, const char** path, size_t* len) {

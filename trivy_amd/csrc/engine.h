@@ -67,6 +67,12 @@ class Engine {
   // returns the wall time in ms.
   bool feed_probe(const uint8_t* h_data, uint64_t bytes, double* ms, std::string* err);
 
+  // GPU-side CR strip of a device-resident batch on the first device
+  // (crstrip.hip): d_dst = d_src without '\r', d_new_off = the files' new
+  // starts; *out_total = stripped bytes, *ms = the kernels' time (HIP events).
+  bool strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles, uint64_t total, void* d_dst,
+                uint64_t* d_new_off, uint64_t* out_total, double* ms, std::string* err);
+
   const Prefilter& prefilter() const { return pf_; }
   std::shared_ptr<const Ruleset> ruleset() const { return rs_; }
   const std::vector<int>& devices() const { return devices_; }
@@ -105,8 +111,8 @@ class Engine {
   int k1_abl_ = 464;
   uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
   uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
-  bool k2_stats_ = false;
-  bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
+  bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
+  bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr
   std::mutex k2s_mu_;
   std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
   uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)

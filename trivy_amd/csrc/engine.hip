@@ -30,6 +30,7 @@
 #include <mutex>
 #include <thread>
 
+#include "crstrip.h"
 #include "engine.h"
 #include "threadpool.h"
 
@@ -1353,6 +1354,7 @@ struct Lane {
   uint32_t* d_ob = nullptr; size_t d_ob_cap = 0;    // K1 v3 deferred-output slots (kOutSlots per thread)
   unsigned long long* d_k2s = nullptr;              // TSG_K2_STATS: per-rule K2 counters (4 per rule)
   unsigned int* d_cnt = nullptr;
+  uint8_t* d_cr = nullptr; size_t d_cr_cap = 0;     // CR strip scratch (crstrip.hip)
   std::vector<uint32_t> h_bh;
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
   ~Lane();
@@ -1396,7 +1398,7 @@ Lane::~Lane() {
   hipSetDevice(device);
   if (compute) hipStreamSynchronize(compute);
   if (copy) hipStreamSynchronize(copy);
-  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s};
+  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s, d_cr};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
@@ -1983,6 +1985,56 @@ bool Engine::feed_probe(const uint8_t* h_data, uint64_t bytes, double* ms, std::
   release_lane(dt, ln);
   if (!ok && err->empty()) *err = "feed probe copy failed";
   return ok;
+}
+
+bool Engine::strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles, uint64_t total, void* d_dst,
+                      uint64_t* d_new_off, uint64_t* out_total, double* ms, std::string* err) {
+  if ((reinterpret_cast<uintptr_t>(d_src) | reinterpret_cast<uintptr_t>(d_dst)) & 15u) {
+    *err = "CR strip buffers must be 16-byte aligned";
+    return false;
+  }
+  if (!d_off || !d_new_off || (total && (!d_src || !d_dst))) { *err = "CR strip: null buffer"; return false; }
+  DeviceTables& dt = *dev_[0];
+  Lane* ln = acquire_lane(dt, err);
+  if (!ln) return false;
+  bool ok = hipSetDevice(dt.device) == hipSuccess;
+  uint64_t ends[2] = {1, 0};
+  ok = ok && hipMemcpyAsync(&ends[0], d_off, 8, hipMemcpyDeviceToHost, ln->compute) == hipSuccess &&
+       hipMemcpyAsync(&ends[1], d_off + nfiles, 8, hipMemcpyDeviceToHost, ln->compute) == hipSuccess &&
+       hipStreamSynchronize(ln->compute) == hipSuccess;
+  if (ok && (ends[0] != 0 || ends[1] != total)) {
+    *err = "CR strip: offsets must run from 0 to the batch size";
+    ok = false;
+  }
+  ok = ok && ensure(&ln->d_cr, &ln->d_cr_cap, cr_strip_scratch_bytes(total), err);
+  static unsigned long long* dbg = nullptr;
+  if (ok && std::getenv("TSG_CR_DEBUG")) {
+    if (!dbg) hipMalloc(&dbg, 64);
+    hipMemsetAsync(dbg, 0, 64, ln->compute);
+    cr_strip_dbg(dbg);
+  }
+  ok = ok && hipEventRecord(ln->ev[0], ln->compute) == hipSuccess;
+  ok = ok && cr_strip_launch(static_cast<const uint8_t*>(d_src), d_off, nfiles, total, static_cast<uint8_t*>(d_dst),
+                             d_new_off, ln->d_cr, ln->compute, err);
+  ok = ok && hipEventRecord(ln->ev[1], ln->compute) == hipSuccess;
+  uint64_t stripped = 0;
+  ok = ok && hipMemcpyAsync(&stripped, ln->d_cr, 8, hipMemcpyDeviceToHost, ln->compute) == hipSuccess &&
+       hipStreamSynchronize(ln->compute) == hipSuccess;
+  float kms = 0;
+  if (ok && ms) ok = hipEventElapsedTime(&kms, ln->ev[0], ln->ev[1]) == hipSuccess;
+  if (ok && dbg && std::getenv("TSG_CR_DEBUG")) {
+    unsigned long long h[8] = {};
+    hipMemcpy(h, dbg, 64, hipMemcpyDeviceToHost);
+    std::fprintf(stderr, "[cr] lookback waits %llu done %llu sum_nr %llu sum_inc %llu\n", h[0], h[1], h[2], h[3]);
+  }
+  release_lane(dt, ln);
+  if (!ok) {
+    if (err->empty()) *err = "CR strip failed on the device";
+    return false;
+  }
+  if (out_total) *out_total = stripped;
+  if (ms) *ms = kms;
+  return true;
 }
 
 // Host confirmation of one segment (files [0, in.nfiles) of sg.in, results

@@ -148,6 +148,29 @@ class Scanner:
     def report(self):
         return _lib.lib().tsg_engine_report(self.engine()).decode("utf-8", "replace")
 
+    def StripCR(self, d_src, d_offsets, nfiles, total):
+        """GPU-side CR strip (tsg_strip_cr_device) of a device-resident batch of
+        text files: every file's bytes.ReplaceAll(content, "\r", "")
+        (pkg/fanal/analyzer/secret/secret.go:121) in one pass.
+
+        d_src: uint8 device tensor holding >= total bytes (16-byte aligned);
+        d_offsets: int64 device tensor of nfiles + 1 file starts (0 ... total).
+        Returns (d_dst, d_new_offsets, stripped_total, kernel_ms); d_dst holds
+        stripped_total bytes (plus 64 bytes of padding for the resident scan).
+        """
+        import torch
+        dev = d_src.device
+        dst = torch.empty(int(total) + 64, dtype=torch.uint8, device=dev)
+        new_off = torch.empty(int(nfiles) + 1, dtype=torch.int64, device=dev)
+        torch.cuda.current_stream(dev).synchronize()     # the engine runs on its own stream
+        out_total, ms = ctypes.c_uint64(), ctypes.c_double()
+        _lib.check(_lib.lib().tsg_strip_cr_device(self.engine(), ctypes.c_void_p(d_src.data_ptr()),
+                                                   ctypes.c_void_p(d_offsets.data_ptr()), int(nfiles), int(total),
+                                                   ctypes.c_void_p(dst.data_ptr()),
+                                                   ctypes.c_void_p(new_off.data_ptr()), ctypes.byref(out_total),
+                                                   ctypes.byref(ms)))
+        return dst, new_off, out_total.value, ms.value
+
     def Scan(self, args):
         return self.ScanBatch([args])[0]
 
