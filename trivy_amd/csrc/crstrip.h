@@ -19,7 +19,4 @@ size_t cr_strip_scratch_bytes(uint64_t total);
 bool cr_strip_launch(const uint8_t* src, const uint64_t* offsets, uint32_t nfiles, uint64_t total, uint8_t* dst,
                      uint64_t* new_off, void* scratch, hipStream_t s, std::string* err);
 
-// measurement: look-back counters (nullptr = off)
-void cr_strip_dbg(unsigned long long* d);
-
 }  // namespace tsg

@@ -5,25 +5,22 @@
 // the batch's stripped image is one stream compaction of the whole batch;
 // each file's new start is the output position of its first input byte.
 //
-// One pass (decoupled look-back, as in single-pass prefix scans): each
-// workgroup takes the next 32 KiB tile from a counter; each of its 8 waves
-// holds 4 KiB in registers (lane l: bytes [16l, 16l + 16) of each 1 KiB
-// sub-tile).  The workgroup publishes its kept-byte count, then reads the
-// status words of the 512 preceding tiles at once (one per thread) back to the
-// nearest published inclusive prefix, publishes its own inclusive prefix and
-// writes the kept bytes and the new start of every file that begins in it.
-// HBM traffic N + N' (read once, write once) plus 8 bytes of status per tile;
-// a small kernel first finds the first file of each 4 KiB wave tile.  With a
-// 512-tile window the prefix frontier moves 16 MB per L2 round trip, well
-// ahead of HBM (a one-wave, one-status-at-a-time look-back measured 1.9 s for
-// 10 GB: the frontier then moved one tile per round trip).
-// Output goes to HBM as aligned dwords through a per-wave LDS staging line
-// (byte stores only at the two partial dwords at a sub-tile's ends, which the
-// neighbouring sub-tiles complete); a sub-tile with no '\r' whose output is
-// 16-byte aligned (every one before the batch's first '\r') is stored directly.
+// Reduce, scan, compact over 64 KiB regions (one wave each):
+//   tsg_cr_count       '\r' count per region                          reads N
+//   tsg_cr_first_file  the first file starting in each region (one thread per file)
+//   tsg_cr_scan        exclusive prefix of the region counts (one workgroup)
+//   tsg_cr_compact     the kept bytes to their output position, and the new
+//                      start of every file beginning in the region    reads N, writes N'
+// HBM traffic 2N + N' for N input bytes (algorithmic N + N').  The compaction
+// works per 1 KiB sub-tile: lane l holds bytes [16l, 16l + 16), a wave prefix
+// sum of the kept counts places them, and the sub-tile's output goes to HBM
+// as aligned dwords through a per-wave LDS staging line (byte stores only at
+// the two partial dwords at its ends, which neighbouring sub-tiles complete).
+// A sub-tile with no '\r' whose output is 16-byte aligned (every one before
+// the batch's first '\r') is stored directly.
+// A single-pass decoupled look-back variant (32 KiB workgroup tiles, 512-tile
+// window) was measured slower: 8.1 ms vs 6.1 ms for 10 GB.
 #include "crstrip.h"
-
-#include <cstdlib>
 
 namespace tsg {
 namespace {
@@ -31,10 +28,8 @@ namespace {
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kCrSub = 1024;            // bytes per wave step (64 lanes x 16 B)
-constexpr uint32_t kCrWaves = 8;             // waves per workgroup
-constexpr uint32_t kCrThreads = 64 * kCrWaves;          // = the look-back window (tiles)
-// tile status word: state in the top two bits, kept-byte count below
-constexpr unsigned long long kCrAggregate = 1ull << 62, kCrInclusive = 2ull << 62, kCrValue = (1ull << 62) - 1;
+constexpr uint32_t kCrRegion = 64 * 1024;    // bytes per wave (one region)
+constexpr uint32_t kCrWaves = 4;             // waves per workgroup (count / compact)
 
 // bit k (k < 4): byte k of d is '\r'
 __device__ __forceinline__ uint32_t cr_bits(uint32_t d) {
@@ -63,19 +58,94 @@ __device__ __forceinline__ v4u cr_load(const uint8_t* __restrict__ src, uint64_t
   return v4u{b[0], b[1], b[2], b[3]};
 }
 
-// first[t] = the first file whose start is >= t * wave_tile (lower_bound)
-__global__ __launch_bounds__(256) void tsg_cr_tile_first(const uint64_t* __restrict__ offsets, uint32_t nfiles,
-                                                         uint32_t ntiles, uint32_t wave_tile,
-                                                         uint32_t* __restrict__ first) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  const uint64_t x = static_cast<uint64_t>(t) * wave_tile;
-  uint32_t lo = 0, hi = nfiles + 1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (offsets[mid] < x) lo = mid + 1; else hi = mid;
+__global__ __launch_bounds__(256) void tsg_cr_count(const uint8_t* __restrict__ src, uint64_t total, uint32_t nregions,
+                                                    uint32_t* __restrict__ region_cr) {
+  const uint32_t lane = threadIdx.x & 63u, r = blockIdx.x * kCrWaves + (threadIdx.x >> 6);
+  if (r >= nregions) return;
+  const uint64_t r0 = static_cast<uint64_t>(r) * kCrRegion;
+  uint32_t n = 0;
+#pragma unroll 8
+  for (uint32_t j = 0; j < kCrRegion / kCrSub; ++j) {
+    uint32_t valid;
+    const v4u w = cr_load(src, r0 + j * kCrSub + lane * 16u, total, &valid);
+    n += __popc(cr_mask16(w) & valid);
   }
-  first[t] = lo;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
+  if (lane == 0) region_cr[r] = n;
+}
+
+// first[r] = the first file whose start is >= r * kCrRegion (files f with
+// offsets[f - 1] < r * kCrRegion <= offsets[f])
+__global__ __launch_bounds__(256) void tsg_cr_first_file(const uint64_t* __restrict__ offsets, uint32_t nfiles,
+                                                         uint32_t nregions, uint32_t* __restrict__ first) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f > nfiles) return;
+  const uint64_t rb = f ? offsets[f - 1] / kCrRegion + 1 : 0;
+  const uint64_t re = offsets[f] / kCrRegion;
+  for (uint64_t r = rb; r <= re && r < nregions; ++r) first[r] = f;
+}
+
+// One workgroup: region_base[r] = '\r' bytes before region r; the files that
+// start at the batch end (trailing empty files, the end sentinel) get the
+// stripped total, which is also stored at *out_total.  Each thread sums a
+// contiguous run of regions with its loads issued in groups of 8 (a
+// one-at-a-time loop waits one L2 round trip per region: 0.29 ms for 10 GB).
+__global__ __launch_bounds__(1024) void tsg_cr_scan(const uint32_t* __restrict__ region_cr, uint32_t nregions,
+                                                    uint64_t* __restrict__ region_base,
+                                                    const uint64_t* __restrict__ offsets, uint32_t nfiles,
+                                                    uint64_t total, uint64_t* __restrict__ new_off,
+                                                    uint64_t* __restrict__ out_total) {
+  __shared__ uint64_t part[1024];
+  __shared__ uint32_t s_lb;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nregions + 1023u) / 1024u;
+  const uint32_t b = min(nregions, t * per), e = min(nregions, b + per);
+  uint64_t s = 0;
+  uint32_t i = b;
+  for (; i + 8 <= e; i += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = region_cr[i + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  for (; i < e; ++i) s += region_cr[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - s;
+  for (i = b; i + 8 <= e; i += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = region_cr[i + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      region_base[i + q] = run;
+      run += v[q];
+    }
+  }
+  for (; i < e; ++i) {
+    region_base[i] = run;
+    run += region_cr[i];
+  }
+  const uint64_t stripped = total - part[1023];
+  if (t == 0) {
+    uint32_t lo = 0, hi = nfiles + 1;      // lower_bound(offsets, total)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (offsets[mid] < total) lo = mid + 1; else hi = mid;
+    }
+    s_lb = lo;
+    *out_total = stripped;
+  }
+  __syncthreads();
+  for (uint32_t k = s_lb + t; k <= nfiles; k += 1024) new_off[k] = stripped;
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
@@ -87,120 +157,45 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
-// status[t] of every tile and status[ntiles] (the tile counter) start at 0.
-template <uint32_t kCrSubs, int kMinWaves>
-__global__ __launch_bounds__(kCrThreads, kMinWaves) void tsg_cr_strip(const uint8_t* __restrict__ src, uint64_t total,
-                                                           uint32_t ntiles, uint32_t nwt,
-                                                           const uint32_t* __restrict__ first,
-                                                           const uint64_t* __restrict__ offsets, uint32_t nfiles,
-                                                           uint8_t* __restrict__ dst, uint64_t* __restrict__ new_off,
-                                                           unsigned long long* __restrict__ status,
-                                                           uint64_t* __restrict__ out_total,
-                                                           unsigned long long* __restrict__ dbg) {
-  constexpr uint32_t kCrWaveTile = kCrSub * kCrSubs;     // bytes per wave
+__global__ __launch_bounds__(256) void tsg_cr_compact(const uint8_t* __restrict__ src, uint64_t total,
+                                                      uint32_t nregions, const uint64_t* __restrict__ region_base,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint64_t* __restrict__ offsets, uint32_t nfiles,
+                                                      uint8_t* __restrict__ dst, uint64_t* __restrict__ new_off) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kCrWaves][kCrSub + 16];
-  __shared__ uint32_t s_tile, s_wt[kCrWaves], s_agg[kCrWaves], s_inc, s_nr;
-  __shared__ unsigned long long s_incval;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t r = blockIdx.x * kCrWaves + wv;
+  if (r >= nregions) return;                 // whole waves only; no workgroup barrier below
   uint8_t* lb = stage[wv];
-  if (threadIdx.x == 0) s_tile = atomicAdd(reinterpret_cast<unsigned int*>(status + ntiles), 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  if (tile >= ntiles) return;                // the whole workgroup
-  const uint32_t wt = tile * kCrWaves + wv;  // this wave's 4 KiB tile
-  const uint64_t t0 = static_cast<uint64_t>(wt) * kCrWaveTile;
-  v4u w[kCrSubs];
-  uint32_t keep[kCrSubs];
-#pragma unroll
-  for (uint32_t j = 0; j < kCrSubs; ++j) {
-    uint32_t valid;
-    w[j] = cr_load(src, t0 + j * kCrSub + lane * 16u, total, &valid);
-    keep[j] = valid;
-  }
-  uint32_t k[kCrSubs], excl[kCrSubs], K[kCrSubs], T = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kCrSubs; ++j) {
-    keep[j] &= ~cr_mask16(w[j]);
-    k[j] = __popc(keep[j]);
-    const uint32_t incl = wave_incl_scan(k[j], lane);
-    excl[j] = incl - k[j];
-    K[j] = __shfl(incl, 63);
-    T += K[j];
-  }
-  if (lane == 0) s_wt[wv] = T;
-  __syncthreads();
-  uint32_t wbase = 0, TT = 0;                // kept bytes of the earlier waves / of the tile
-#pragma unroll
-  for (uint32_t i = 0; i < kCrWaves; ++i) {
-    if (i < wv) wbase += s_wt[i];
-    TT += s_wt[i];
-  }
-  if (threadIdx.x == 0)
-    __hip_atomic_store(status + tile, (tile == 0 ? kCrInclusive : kCrAggregate) | TT, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  // look-back: thread i reads the status of tile p - i; every earlier tile is
-  // held by a running or finished workgroup, and tile 0 publishes at once.
-  // Status words are relaxed device-scope atomics: they carry the counts
-  // themselves and order nothing else (release / acquire at device scope
-  // write back / invalidate the XCD's L2 on every access: measured 64 ms
-  // instead of a few for 10 GB)
-  unsigned long long before = 0;
-  for (long long p = static_cast<long long>(tile) - 1; p >= 0;) {
-    const uint32_t i = threadIdx.x;
-    const unsigned long long v = static_cast<long long>(i) <= p
-        ? __hip_atomic_load(status + (p - i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-        : kCrAggregate;                      // past tile 0: never reached (tile 0 is inclusive)
-    if (i == 0) { s_inc = 0xffffffffu; s_nr = 0xffffffffu; }
-    __syncthreads();
-    if (v & kCrInclusive) atomicMin(&s_inc, i);
-    if (v == 0) atomicMin(&s_nr, i);
-    __syncthreads();
-    const uint32_t inc = s_inc, nr = s_nr;
-    if (dbg && i == 0) atomicAdd(dbg + (nr < inc ? 0 : 1), 1ull);
-    if (dbg && i == 0 && nr < inc) atomicAdd(dbg + 2, static_cast<unsigned long long>(nr));
-    if (dbg && i == 0 && nr >= inc && inc != 0xffffffffu) atomicAdd(dbg + 3, static_cast<unsigned long long>(inc));
-    if (nr < inc) {                          // a nearer tile has not published yet
-      __syncthreads();
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    uint32_t x = i < inc ? static_cast<uint32_t>(v & kCrValue) : 0u;   // aggregates (<= 32 KiB each)
-    if (i == inc) s_incval = v & kCrValue;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-    if (lane == 0) s_agg[wv] = x;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t q = 0; q < kCrWaves; ++q) before += s_agg[q];
-    if (inc != 0xffffffffu) {
-      before += s_incval;
-      break;
-    }
-    __syncthreads();
-    p -= kCrThreads;
-  }
-  if (threadIdx.x == 0 && tile > 0)
-    __hip_atomic_store(status + tile, kCrInclusive | (before + TT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t out = before + wbase;
-  uint32_t f = first[wt];
+  const uint64_t r0 = static_cast<uint64_t>(r) * kCrRegion;
+  const uint64_t r1 = min(r0 + kCrRegion, total);
+  uint64_t out = r0 - region_base[r];
+  uint32_t f = first[r];
   uint64_t next_start = offsets[f];          // wave-uniform: the next file start at or after the sub-tile
-#pragma unroll
-  for (uint32_t j = 0; j < kCrSubs; ++j) {
-    const uint64_t s0 = t0 + j * kCrSub;
-    if (s0 >= total) break;
-    const bool plain = __ballot(keep[j] != 0xffffu) == 0;   // full sub-tile without '\r'
+  uint32_t valid_n;
+  v4u wn = cr_load(src, r0 + lane * 16u, total, &valid_n);
+  for (uint64_t s0 = r0; s0 < r1; s0 += kCrSub) {
+    const v4u w = wn;
+    const uint32_t valid = valid_n;
+    if (s0 + kCrSub < r1) wn = cr_load(src, s0 + kCrSub + lane * 16u, total, &valid_n);   // next sub-tile in flight
+    const uint32_t keep = valid & ~cr_mask16(w);
+    const uint32_t k = __popc(keep);
+    const uint32_t incl = wave_incl_scan(k, lane);
+    const uint32_t excl = incl - k;
+    const uint32_t K = __shfl(incl, 63);
+    const bool plain = __ballot(keep != 0xffffu) == 0;   // full sub-tile without '\r'
     if (plain && (out & 15u) == 0) {
-      __builtin_nontemporal_store(w[j], reinterpret_cast<v4u*>(dst + out + lane * 16u));
-    } else if (K[j]) {
+      __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst + out + lane * 16u));
+    } else if (K) {
       const uint32_t q0 = static_cast<uint32_t>(out & 3u);   // stage byte q holds output byte (out & ~3) + q
       if (plain && q0 == 0) {
-        *reinterpret_cast<v4u*>(lb + lane * 16u) = w[j];
+        *reinterpret_cast<v4u*>(lb + lane * 16u) = w;
       } else {
-        const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
-        uint32_t q = q0 + excl[j];
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        uint32_t q = q0 + excl;
 #pragma unroll
         for (int b = 0; b < 16; ++b) {
-          if ((keep[j] >> b) & 1u) {
+          if ((keep >> b) & 1u) {
             lb[q] = static_cast<uint8_t>(ws[b >> 2] >> ((b & 3) * 8));
             ++q;
           }
@@ -208,7 +203,7 @@ __global__ __launch_bounds__(kCrThreads, kMinWaves) void tsg_cr_strip(const uint
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      const uint64_t a0 = out - q0, e = out + K[j];
+      const uint64_t a0 = out - q0, e = out + K;
       const uint32_t ndw = static_cast<uint32_t>((e - a0 + 3) >> 2);
       for (uint32_t d = lane; d < ndw; d += 64) {
         const uint64_t g = a0 + 4ull * d;
@@ -230,77 +225,43 @@ __global__ __launch_bounds__(kCrThreads, kMinWaves) void tsg_cr_strip(const uint
       const uint64_t o = idx <= nfiles ? offsets[idx] : ~0ull;
       const bool in = o < s1;                // o >= s0: files are sorted and f is past the earlier ones
       const uint32_t wi = in ? static_cast<uint32_t>((o - s0) >> 4) : 0u;
-      const uint32_t pe = __shfl(excl[j], wi), pk = __shfl(keep[j], wi);
+      const uint32_t pe = __shfl(excl, wi), pk = __shfl(keep, wi);
       if (in) new_off[idx] = out + pe + __popc(pk & ((1u << (o & 15u)) - 1u));
       f += static_cast<uint32_t>(__popcll(__ballot(in)));
       next_start = f <= nfiles ? offsets[f] : ~0ull;
     }
-    out += K[j];
-  }
-  if (wt == nwt - 1) {                       // files starting at the batch end, and the stripped total
-    for (uint32_t i = f + lane; i <= nfiles; i += 64) new_off[i] = out;
-    if (lane == 0) *out_total = out;
+    out += K;
   }
 }
 
 }  // namespace
 
-unsigned long long* dbg_ = nullptr;   // TSG_CR_DEBUG: look-back counters (measurement)
-void cr_strip_dbg(unsigned long long* d) { dbg_ = d; }
-
-// TSG_CR_VARIANT (measurement): sub-tiles per wave x minimum waves per SIMD
-int cr_variant_ = 0;
-struct CrVariant { uint32_t subs; const void* fn; };
-CrVariant cr_variant() {
-  switch (cr_variant_) {
-    case 1: return {4, reinterpret_cast<const void*>(&tsg_cr_strip<4, 6>)};
-    case 2: return {2, reinterpret_cast<const void*>(&tsg_cr_strip<2, 1>)};
-    case 3: return {2, reinterpret_cast<const void*>(&tsg_cr_strip<2, 8>)};
-    case 4: return {1, reinterpret_cast<const void*>(&tsg_cr_strip<1, 8>)};
-    default: return {4, reinterpret_cast<const void*>(&tsg_cr_strip<4, 1>)};
-  }
-}
-
 size_t cr_strip_scratch_bytes(uint64_t total) {
-  const uint64_t wave_tile = kCrSub;             // the smallest variant's
-  const uint64_t ntiles = (total + wave_tile * kCrWaves - 1) / (wave_tile * kCrWaves);
-  const uint64_t nwt = (total + wave_tile - 1) / wave_tile;
-  return 64 + (ntiles + 1) * 8 + nwt * 4 + 64;
+  const uint64_t nreg = (total + kCrRegion - 1) / kCrRegion;
+  return 64 + nreg * (4 + 8 + 4) + 64;
 }
 
 bool cr_strip_launch(const uint8_t* src, const uint64_t* offsets, uint32_t nfiles, uint64_t total, uint8_t* dst,
                      uint64_t* new_off, void* scratch, hipStream_t s, std::string* err) {
-  static const bool once = [] {
-    if (const char* c = std::getenv("TSG_CR_VARIANT")) cr_variant_ = std::atoi(c);
-    return true;
-  }();
-  (void)once;
-  const CrVariant v = cr_variant();
-  const uint64_t wave_tile = kCrSub * v.subs, tile = wave_tile * kCrWaves;
-  const uint64_t nt64 = (total + tile - 1) / tile, nwt64 = (total + wave_tile - 1) / wave_tile;
-  if (nwt64 >= 0xffffffffull) { *err = "batch too large for the CR strip"; return false; }
-  const uint32_t ntiles = static_cast<uint32_t>(nt64), nwt = static_cast<uint32_t>(nwt64);
+  const uint64_t nreg64 = (total + kCrRegion - 1) / kCrRegion;
+  if (nreg64 > 0xffffffffull / kCrWaves) { *err = "batch too large for the CR strip"; return false; }
+  const uint32_t nreg = static_cast<uint32_t>(nreg64);
   uint8_t* sp = static_cast<uint8_t*>(scratch);
   uint64_t* d_total = reinterpret_cast<uint64_t*>(sp);
-  unsigned long long* status = reinterpret_cast<unsigned long long*>(sp + 64);
-  uint32_t* first = reinterpret_cast<uint32_t*>(sp + 64 + (nt64 + 1) * 8);
-  if (ntiles == 0) {                         // every file is empty
-    if (hipMemsetAsync(new_off, 0, (static_cast<size_t>(nfiles) + 1) * 8, s) != hipSuccess ||
-        hipMemsetAsync(d_total, 0, 8, s) != hipSuccess) {
-      *err = "CR strip: memset failed";
-      return false;
-    }
-    return true;
+  uint64_t* region_base = reinterpret_cast<uint64_t*>(sp + 64);
+  uint32_t* region_cr = reinterpret_cast<uint32_t*>(sp + 64 + 8 * nreg64);
+  uint32_t* first = region_cr + nreg64;
+  const uint32_t blocks = (nreg + kCrWaves - 1) / kCrWaves;
+  if (nreg) {
+    hipLaunchKernelGGL(tsg_cr_count, dim3(blocks), dim3(256), 0, s, src, total, nreg, region_cr);
+    hipLaunchKernelGGL(tsg_cr_first_file, dim3((nfiles + 1 + 255) / 256), dim3(256), 0, s, offsets, nfiles, nreg,
+                       first);
   }
-  if (hipMemsetAsync(status, 0, (nt64 + 1) * 8, s) != hipSuccess) { *err = "CR strip: memset failed"; return false; }
-  hipLaunchKernelGGL(tsg_cr_tile_first, dim3((nwt + 255) / 256), dim3(256), 0, s, offsets, nfiles, nwt,
-                     static_cast<uint32_t>(wave_tile), first);
-  void* args[] = {&src, &total, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&nwt), &first, &offsets, &nfiles,
-                  &dst, &new_off, &status, &d_total, &dbg_};
-  if (hipLaunchKernel(v.fn, dim3(ntiles), dim3(kCrThreads), args, 0, s) != hipSuccess) {
-    *err = "CR strip launch failed";
-    return false;
-  }
+  hipLaunchKernelGGL(tsg_cr_scan, dim3(1), dim3(1024), 0, s, region_cr, nreg, region_base, offsets, nfiles, total,
+                     new_off, d_total);
+  if (nreg)
+    hipLaunchKernelGGL(tsg_cr_compact, dim3(blocks), dim3(256), 0, s, src, total, nreg, region_base, first, offsets,
+                       nfiles, dst, new_off);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { *err = std::string("CR strip launch: ") + hipGetErrorString(e); return false; }
   return true;

@@ -2007,12 +2007,6 @@ bool Engine::strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles,
     ok = false;
   }
   ok = ok && ensure(&ln->d_cr, &ln->d_cr_cap, cr_strip_scratch_bytes(total), err);
-  static unsigned long long* dbg = nullptr;
-  if (ok && std::getenv("TSG_CR_DEBUG")) {
-    if (!dbg) hipMalloc(&dbg, 64);
-    hipMemsetAsync(dbg, 0, 64, ln->compute);
-    cr_strip_dbg(dbg);
-  }
   ok = ok && hipEventRecord(ln->ev[0], ln->compute) == hipSuccess;
   ok = ok && cr_strip_launch(static_cast<const uint8_t*>(d_src), d_off, nfiles, total, static_cast<uint8_t*>(d_dst),
                              d_new_off, ln->d_cr, ln->compute, err);
@@ -2022,11 +2016,6 @@ bool Engine::strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles,
        hipStreamSynchronize(ln->compute) == hipSuccess;
   float kms = 0;
   if (ok && ms) ok = hipEventElapsedTime(&kms, ln->ev[0], ln->ev[1]) == hipSuccess;
-  if (ok && dbg && std::getenv("TSG_CR_DEBUG")) {
-    unsigned long long h[8] = {};
-    hipMemcpy(h, dbg, 64, hipMemcpyDeviceToHost);
-    std::fprintf(stderr, "[cr] lookback waits %llu done %llu sum_nr %llu sum_inc %llu\n", h[0], h[1], h[2], h[3]);
-  }
   release_lane(dt, ln);
   if (!ok) {
     if (err->empty()) *err = "CR strip failed on the device";
