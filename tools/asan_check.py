@@ -1,4 +1,4 @@
-"""Host-code sanitizer run (ASan + UBSan) over the CPU entry points of the C-ABI.
+"""Host-code sanitizer run (ASan + UBSan, or TSan with --thread) over the CPU entry points of the C-ABI.
 
 Builds tools/asan_driver.cpp against the host sources of libtrivysecret
 compiled with g++ -fsanitize=address,undefined (no recovery), linked with the
@@ -26,11 +26,12 @@ from trivy_amd import build as B  # noqa: E402
 from workload import synth  # noqa: E402
 
 SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1"]
+TSAN = ["-fsanitize=thread", "-fno-omit-frame-pointer", "-g", "-O1"]
 
 
-def build_driver(outdir):
+def build_driver(outdir, san):
     B.build()                                        # HIP objects in trivy_amd/_build
-    common = ["-std=c++17", "-fPIC", "-I", B.CSRC, "-I", os.path.join(ROOT, "include")] + SAN
+    common = ["-std=c++17", "-fPIC", "-I", B.CSRC, "-I", os.path.join(ROOT, "include")] + san
     objs = []
     jobs = []
     for s in B.HOST_SRCS:
@@ -73,11 +74,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=float, default=8.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--thread", action="store_true", help="ThreadSanitizer instead of ASan + UBSan")
     ap.add_argument("--workdir", default="", help="keep the driver and inputs here")
     a = ap.parse_args()
     lines = []
     with (tempfile.TemporaryDirectory() if not a.workdir else _Keep(a.workdir)) as td:
-        exe = build_driver(td)
+        san = TSAN if a.thread else SAN
+        exe = build_driver(td, san)
         nb = int(a.mb * 1e6)
         c2 = synth.generate(nb, seed=11, sizes="lognormal", plant_rate=2e-3, base_bytes=1 << 20)
         write_case(os.path.join(td, "c2"), c2, None)
@@ -86,13 +89,14 @@ def main():
         synth.plant_custom(c5, plants, seed=5, rate=2e-3)
         write_case(os.path.join(td, "c5"), c5, cfg5)
         env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
-                   UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+                   UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+                   TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
         rc_all = 0
         for case in ("c2", "c5"):
             p = subprocess.run([exe, os.path.join(td, case)], capture_output=True, text=True, env=env)
             lines.append("%s rc=%d %s%s" % (case, p.returncode, p.stdout, p.stderr[-4000:]))
             rc_all |= p.returncode
-    text = "sanitizers: %s\n%s" % (" ".join(SAN), "".join(lines))
+    text = "sanitizers: %s\n%s" % (" ".join(san), "".join(lines))
     print(text)
     if a.out:
         with open(a.out, "w") as f:
