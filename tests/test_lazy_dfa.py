@@ -108,3 +108,14 @@ def test_span_shape_end_matches_vm(pattern):
         t = b"".join(rng.choice(parts) for _ in range(rng.randint(0, 30)))
         d, v = _probe(pattern, t)
         assert (d == v).all(), (pattern, t, d, v)
+
+
+def test_nesting_depth_limit():
+    # Go regexp/syntax ErrNestingDepth (maxHeight 1000): 999 nested captures
+    # around an atom parse, 1000 do not; a hostile 100k-deep group nest is an
+    # error, not a stack overflow of the host process.
+    d, v = _probe("(" * 999 + "a" + ")" * 999, b"xa")
+    assert list(d[:2]) == [-1, 2] and list(v[:2]) == [-1, 2]
+    for pat in ("(" * 1000 + "a" + ")" * 1000, "(?:" * 100000 + "a" + ")" * 100000):
+        with pytest.raises(Exception, match="expression nests too deeply"):
+            _probe(pat, b"a")

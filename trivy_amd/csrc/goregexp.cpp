@@ -125,6 +125,7 @@ class Parser {
   size_t i_ = 0;
   std::string err_;
   int ncap_ = 0;
+  int depth_ = 0;  // open groups; Go's maxHeight (regexp/syntax parse.go) bounds nesting at 1000
   std::vector<std::string> names_;
 
   bool eof() const { return i_ >= p_.size(); }
@@ -257,7 +258,18 @@ class Parser {
     return literal(next_rune(), *f);
   }
 
+  // Go rejects trees higher than 1000 (ErrNestingDepth): 1000 nested
+  // capture groups around an atom are 1001 levels.  The cap also bounds this
+  // parser's and compile()'s recursion on hostile configs (Go, whose
+  // non-capturing groups add no level, accepts deeper (?: nesting).
   std::unique_ptr<Node> group(Flags* f) {
+    if (++depth_ >= 1000) { fail("expression nests too deeply: `" + p_ + "`"); --depth_; return nullptr; }
+    auto n = group_body(f);
+    --depth_;
+    return n;
+  }
+
+  std::unique_ptr<Node> group_body(Flags* f) {
     ++i_;  // '('
     std::string name;
     bool named = false;
