@@ -11,5 +11,5 @@ tail -2 $OUT/gpu_tests.log
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
 timeout -k 10 500 python -u bench.py > $OUT/bench.json 2> $OUT/bench.log || { tail -20 $OUT/bench.log; exit 1; }
 cat $OUT/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 3 > $OUT/bench_prof.json 2> $OUT/bench_prof.log || { tail $OUT/bench_prof.log; exit 1; }
+[ -n "$R3N_NOPROF" ] || timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 3 > $OUT/bench_prof.json 2> $OUT/bench_prof.log || { tail $OUT/bench_prof.log; exit 1; }
 echo done
