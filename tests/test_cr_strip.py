@@ -148,3 +148,28 @@ def test_strip_cr_then_resident_scan_gpu():
         assert g == w, p
         nfind += len(w.get("Findings") or [])
     assert nfind > 5
+
+
+@pytest.mark.gpu
+def test_strip_cr_rejects_host_buffers_gpu():
+    """Buffers that are not device memory of one of the engine's devices are
+    refused at the boundary (no kernel gets a host or foreign pointer)."""
+    import torch
+    files = [b"a\r\nb", b"\r\r", b"xyz"]
+    data, off = _pack(files)
+    sc = S.Scanner(None)
+    L = _lib.lib()
+    d_src = torch.from_numpy(data.copy()).to("cuda:0")
+    d_off = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
+    h_off = torch.from_numpy(off.astype(np.int64)).pin_memory()
+    dst = torch.empty(len(data), dtype=torch.uint8, device="cuda:0")
+    new_off = torch.empty(len(files) + 1, dtype=torch.int64, device="cuda:0")
+    tot, ms = ctypes.c_uint64(), ctypes.c_double()
+    for src, offs, out in ((d_src, h_off, dst), (data.ctypes.data, d_off, dst), (d_src, d_off, h_off)):
+        p = lambda t: ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())
+        rc = L.tsg_strip_cr_device(sc.engine(), p(src), p(offs), len(files), int(off[-1]), p(out), p(new_off),
+                                   ctypes.byref(tot), ctypes.byref(ms))
+        assert rc != 0 and "device memory" in L.tsg_last_error().decode()
+    # and the same call with device buffers works
+    got_dst, got_off, stripped, _ = sc.StripCR(d_src, d_off, len(files), int(off[-1]))
+    assert got_dst[:stripped].cpu().numpy().tobytes() == b"".join(f.replace(b"\r", b"") for f in files)

@@ -119,3 +119,18 @@ def test_nesting_depth_limit():
     for pat in ("(" * 1000 + "a" + ")" * 1000, "(?:" * 100000 + "a" + ")" * 100000):
         with pytest.raises(Exception, match="expression nests too deeply"):
             _probe(pat, b"a")
+
+
+def test_nested_repeat_product_limit():
+    # Go regexp/syntax repeatIsValid(re, 1000): counted repeats nested inside
+    # counted repeats may not multiply past 1000 ("invalid repeat count");
+    # without the check simplify would expand ((a{1000}){1000}){1000} into 1e9
+    # nodes.  Products up to 1000, and {n,} counted by its minimum, parse.
+    d, _ = _probe("(?:(?:a{10}){10}){10}", b"a" * 1000)
+    assert d[0] == 1000
+    for ok in ("(a{2}){500}", "(a{1000})*", "(a{0}){1000}", "(?:a{10,}){100}", "(a{2}b){2}c{1000}"):
+        _probe(ok, b"ab")
+    for bad in ("((a{1000}){1000}){1000}", "(a{2}){501}", "(?:a{10,}){101}", "(?:(?:a{10}){10}){11}",
+                "(a{1001,})", "(x{2,3}y{3}){400}"):
+        with pytest.raises(Exception, match="invalid repeat count"):
+            _probe(bad, b"a")

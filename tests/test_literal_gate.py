@@ -121,3 +121,7 @@ def test_indexed_allow_path_equals_oracle(tmp_path, cfg):
               "test", "atest", "/test", "examplE", "x/vendor/y", "x/vendorz/y"]
     for p in paths:
         assert sc.AllowPath(p) == ref.allow_path(p), p
+    # the index is built for the builtins-only ruleset (NewScanner(nil)) too,
+    # not only when a config is given
+    rep = S.prefilter_report(sc)
+    assert "global allow-path index: " in rep and "unused" not in rep.split("global allow-path index: ")[1], rep

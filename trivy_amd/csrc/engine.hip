@@ -1994,7 +1994,16 @@ bool Engine::strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles,
     return false;
   }
   if (!d_off || !d_new_off || (total && (!d_src || !d_dst))) { *err = "CR strip: null buffer"; return false; }
-  DeviceTables& dt = *dev_[0];
+  // every buffer must be memory of one device the engine spans; the kernels
+  // run there (an engine over several devices takes the caller's device)
+  const int dev = device_of(d_off);
+  DeviceTables* dtp = nullptr;
+  for (auto& d : dev_) if (d->device == dev) { dtp = d.get(); break; }
+  if (!dtp || device_of(d_new_off) != dev || (total && (device_of(d_src) != dev || device_of(d_dst) != dev))) {
+    *err = "CR strip buffers must be device memory of one of the engine's devices";
+    return false;
+  }
+  DeviceTables& dt = *dtp;
   Lane* ln = acquire_lane(dt, err);
   if (!ln) return false;
   bool ok = hipSetDevice(dt.device) == hipSuccess;

@@ -218,7 +218,27 @@ class Parser {
       n->max = hi;
       n->sub.push_back(std::move(a));
       a = std::move(n);
+      // regexp/syntax parser.repeat: nested counted repeats may not multiply
+      // past 1000 (simplify would expand them into that many copies)
+      if (op == Op::Repeat && (lo >= 2 || hi >= 2) && !repeat_is_valid(a.get(), kMaxRepeat)) {
+        fail("invalid repeat count: `" + p_.substr(save, i_ - save) + "`");
+        return a;
+      }
     }
+  }
+
+  // regexp/syntax repeatIsValid
+  static bool repeat_is_valid(const Node* re, int n) {
+    if (re->op == Op::Repeat) {
+      int m = re->max;
+      if (m == 0) return true;
+      if (m < 0) m = re->min;
+      if (m > n) return false;
+      if (m > 0) n /= m;
+    }
+    for (const auto& s : re->sub)
+      if (!repeat_is_valid(s.get(), n)) return false;
+    return true;
   }
 
   std::unique_ptr<Node> literal(uint32_t r, const Flags& f) {

@@ -1213,6 +1213,11 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
                std::to_string(pf->groups.size()) + " scan DFA group(s), " + std::to_string(pf->nkw) +
                " keywords, " + std::to_string(pf->anchors.size()) + " anchor literals, max pattern " +
                std::to_string(maxb) + " B\n" + grep + rep;
+  const auto& ix = rs.allow_index;
+  pf->report += "global allow-path index: " +
+                (ix.usable ? std::to_string(ix.out.size()) + " AC states, " +
+                                 std::to_string(__builtin_popcountll(ix.always)) + " ungated regexes"
+                           : std::string("unused (plain loop)")) + "\n";
   return true;
 }
 

@@ -217,6 +217,7 @@ bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
     out->allow_rules = std::move(b_allow);
     out->exclude_block.clear();
     index_excludes(out);
+    build_allow_index(out);
     return true;
   }
   std::vector<std::string> enable = str_list(cfg->get("enable-builtin-rules"));

@@ -90,15 +90,25 @@ bool parse_pax(const uint8_t* p, size_t n, std::string* path, bool* has_path, in
     const size_t eq = rec.find('=');
     if (eq == std::string::npos) return false;
     const std::string key = rec.substr(0, eq), val = rec.substr(eq + 1);
+    // validPAXRecord: a non-empty key; no NUL in a path value or in any other key
+    if (key.empty()) return false;
+    if (key == "path" ? val.find('\0') != std::string::npos : key.find('\0') != std::string::npos) return false;
     if (key == "path") { *path = val; *has_path = true; }
     else if (key == "size") {
+      // strconv.ParseInt(v, 10, 64): optional sign, decimal digits, range
+      // checked; a negative size is rejected later (handleRegularFile)
+      size_t k = 0;
+      bool neg = false;
+      if (k < val.size() && (val[k] == '+' || val[k] == '-')) neg = val[k++] == '-';
+      if (k == val.size()) return false;
       int64_t v = 0;
-      if (val.empty()) return false;
-      for (char c : val) {
+      for (; k < val.size(); ++k) {
+        const char c = val[k];
         if (c < '0' || c > '9') return false;
+        if (v > (INT64_MAX - (c - '0')) / 10) return false;   // out of range: ErrHeader
         v = v * 10 + (c - '0');
       }
-      *size = v;
+      *size = neg ? -v : v;
       *has_size = true;
     }
     i = end;
@@ -321,8 +331,15 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
     }
     if (!checksum_ok(h)) return fail("invalid tar header");
     int64_t size = 0;
-    if (!parse_numeric(h + 124, 12, &size) || size < 0) return fail("invalid tar header");
     const char type = static_cast<char>(h[156]);
+    // the raw header's size goes through handleRegularFile before any PAX
+    // record applies: negative is ErrHeader unless the type carries no data
+    const bool raw_header_only = type == '1' || type == '2' || type == '3' || type == '4' || type == '5' || type == '6';
+    if (!parse_numeric(h + 124, 12, &size)) return fail("invalid tar header");
+    if (size < 0) {
+      if (!raw_header_only) return fail("invalid tar header");
+      size = 0;
+    }
     const bool ustar = std::memcmp(h + 257, "ustar", 5) == 0;
     std::string name = field(h, 100);
     if (ustar && std::memcmp(h + 257, "ustar\0" "00", 8) == 0) {
@@ -332,7 +349,7 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
     const uint64_t data_off = pos + kBlock;
     const uint64_t padded = (static_cast<uint64_t>(size) + kBlock - 1) / kBlock * kBlock;
     if (type == 'x' || type == 'g' || type == 'L' || type == 'K') {
-      if (data_off + static_cast<uint64_t>(size) > len) return fail("unexpected EOF");
+      if (static_cast<uint64_t>(size) > len - data_off) return fail("unexpected EOF");
       const uint8_t* d = tar + data_off;
       if (type == 'x') {
         if (!parse_pax(d, static_cast<size_t>(size), &pax_path, &has_pax_path, &pax_size, &has_pax_size))
@@ -357,7 +374,8 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
     // Reader.handleRegularFile: header-only types (links, devices, dirs,
     // fifos) consume no data whatever their size field says
     const bool has_data = !(tf == '1' || tf == '2' || tf == '3' || tf == '4' || tf == '5' || tf == '6');
-    if (has_data && data_off + static_cast<uint64_t>(size) > len) return fail("unexpected EOF");
+    if (has_data && size < 0) return fail("invalid tar header");   // handleRegularFile: Size < 0 is ErrHeader
+    if (has_data && static_cast<uint64_t>(size) > len - data_off) return fail("unexpected EOF");
     pos = data_off + (has_data ? padded2 : 0);
     // ---- walker.LayerTar.Walk (tar.go:46-90)
     std::string file_path = trim_left_slash(go_path_clean(name));
