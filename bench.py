@@ -65,37 +65,75 @@ def cpu_baseline(items, procs, cfg_path=None):
     ctx = mp.get_context("fork")
     with ctx.Pool(procs, initializer=_oracle_worker_init, initargs=(cfg_path,)) as pool:
         t0 = time.perf_counter()
-        res = pool.map(_oracle_scan, items, chunksize=1)
+        # largest files first (LPT): one 64 MB file is seconds of oracle work
+        order = sorted(range(len(items)), key=lambda j: -len(items[j][1]))
+        got = pool.map(_oracle_scan, [items[j] for j in order], chunksize=1)
+        res = [None] * len(items)
+        for j, r in zip(order, got):
+            res[j] = r
         dt = time.perf_counter() - t0
     return nbytes / dt / 1e9, res, dt, nbytes
 
 
-def pick_sample(offsets, target_bytes, max_file, seed):
+def pick_sample(offsets, target_bytes, seed, large=8 << 20, large_share=0.5):
+    """A seeded sample of files of about target_bytes: files up to `large`
+    bytes fill (1 - large_share) of it, files above `large` (up to the 64 MB
+    maximum) the rest, so the oracle also checks the batch's largest files."""
     rng = np.random.default_rng(seed)
     n = len(offsets) - 1
-    idx, tot = [], 0
+    small_t, large_t = target_bytes * (1 - large_share), target_bytes * large_share
+    idx, st, lt = [], 0, 0
     for i in rng.permutation(n):
         sz = int(offsets[i + 1] - offsets[i])
-        if sz > max_file:
-            continue
+        if sz > large:
+            if lt >= large_t:
+                continue
+            lt += sz
+        else:
+            if st >= small_t:
+                continue
+            st += sz
         idx.append(int(i))
-        tot += sz
-        if tot >= target_bytes:
+        if st >= small_t and lt >= large_t:
             break
     return sorted(idx)
+
+
+def _alloc_pinned(L, n):
+    from trivy_amd import _lib
+    ptr = ctypes.c_void_p()
+    _lib.check(L.tsg_alloc_pinned(n, ctypes.byref(ptr)))
+    return ptr, np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
+
+
+class PinnedAlloc:
+    """synth.generate(alloc=...) hook: the corpus is written straight into
+    pinned host memory (one host copy of the batch per rank, not three)."""
+
+    def __init__(self, L):
+        self.L, self.ptr, self.view = L, None, None
+
+    def __call__(self, n):
+        assert self.ptr is None
+        self.ptr, self.view = _alloc_pinned(self.L, n)
+        return self.view
 
 
 class PinnedBatch:
     """A packed batch in pinned host memory (tsg_alloc_pinned) + offsets, paths, binary flags."""
 
-    def __init__(self, L, data_u8, offsets, paths, binary=None):
+    def __init__(self, L, data_u8, offsets, paths, binary=None, pinned=None):
+        """Copies data_u8 into new pinned memory, or adopts `pinned` (a
+        PinnedAlloc the data was generated into) without a copy."""
         from trivy_amd import _lib
         self.L = L
         self.nbytes = int(offsets[-1])
-        self.ptr = ctypes.c_void_p()
-        _lib.check(L.tsg_alloc_pinned(self.nbytes + 64, ctypes.byref(self.ptr)))
-        self.view = np.ctypeslib.as_array(ctypes.cast(self.ptr, ctypes.POINTER(ctypes.c_uint8)), shape=(self.nbytes + 64,))
-        self.view[:self.nbytes] = data_u8[:self.nbytes]
+        if pinned is not None:
+            self.ptr, self.view = pinned.ptr, pinned.view
+            pinned.ptr = None
+        else:
+            self.ptr, self.view = _alloc_pinned(L, self.nbytes + 64)
+            self.view[:self.nbytes] = data_u8[:self.nbytes]
         self.view[self.nbytes:] = 0
         self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         self.paths = paths
@@ -174,6 +212,75 @@ def numa_bind(device):
         return None
 
 
+def available_cores():
+    """CPUs this process may run on: the affinity set, capped by a cgroup CPU
+    quota (cpu.max) when one is set.  Returns (cores, detail)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except Exception:
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {"affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def rank_envs(n, port, base_env=None):
+    """Environment of each of the n ranks `bench.py --gpus n` starts when it is
+    not already running under torchrun (one process per GPU, rank r on HIP
+    device r, its engine's device_mask = 1 << r)."""
+    env0 = dict(os.environ if base_env is None else base_env)
+    out = []
+    for r in range(n):
+        e = dict(env0)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "TSG_BENCH_LAUNCHED": "1"})
+        out.append(e)
+    return out
+
+
+def launch_ranks(n, argv, dry=False):
+    """`python bench.py --gpus n` without torchrun: start n rank processes
+    (children, never an exec of this process) and return the worst exit code.
+    Fails loudly before starting anything when fewer than n GPUs are visible
+    (torch.cuda.device_count() does not initialise the GPU)."""
+    import socket
+    import subprocess
+    if not dry:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print("[bench] --gpus %d needs %d GPUs, %d visible" % (n, n, have), file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    print("[bench] launcher: %d ranks, one per GPU, rendezvous 127.0.0.1:%d" % (n, port), file=sys.stderr, flush=True)
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e) for e in rank_envs(n, port)]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0:
+                    rc = rc or r
+                    for q in pending:          # one rank failed: the others cannot finish their barriers
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def _segment_bytes():
     v = os.environ.get("TSG_SEGMENT_BYTES")
     return int(v) if v and int(v) >= 4096 else 4 << 30
@@ -181,7 +288,8 @@ def _segment_bytes():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); without torchrun, bench.py starts the ranks itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
@@ -195,23 +303,48 @@ def main():
     ap.add_argument("--gb", type=float, default=None, help="corpus GB per GPU (default: 1 for config 1, else 10)")
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--threads", type=int, default=16, help="host confirm threads per rank")
-    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU baseline workers (default: every core this rank may use, SURVEY 8d's T = nproc)")
     ap.add_argument("--cpu-sample-mb", type=float, default=1200.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident comparison leg")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="ranks only report their wiring (rank, device, device_mask) and exit: the launcher's "
+                         "CPU test")
     args = ap.parse_args()
     gb = args.gb if args.gb is not None else (1.0 if args.config == 1 else 10.0)
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], dry=args.dry_launch))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print("[bench] --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr, flush=True)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    if args.dry_launch:
+        wiring = {"rank": rank, "world": world, "local_rank": local_rank, "device": local_rank,
+                  "device_mask": 1 << local_rank}
+        got = [None] * world
+        if dist:
+            dist.all_gather_object(got, wiring)
+            dist.destroy_process_group()
+        else:
+            got = [wiring]
+        if rank == 0:
+            print(json.dumps({"dry_launch": got}), flush=True)
+        return
 
     import torch
+    if torch.cuda.device_count() <= local_rank:
+        print("[bench] rank %d needs HIP device %d, %d visible" % (rank, local_rank, torch.cuda.device_count()),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
 
     from trivy_amd import _lib
     from trivy_amd import secret as S
@@ -225,13 +358,17 @@ def main():
     device = local_rank
     torch.cuda.set_device(device)
     numa = numa_bind(device)
+    cores, cores_detail = available_cores()
 
     # ---------------------------------------------------------------- workload
     t_gen = time.perf_counter()
     cfg_path = None
     sizes = {1: "lognormal", 2: "loguniform", 3: "small", 4: "loguniform", 5: "lognormal"}[args.config]
+    # configs other than 3 scan the files as generated: generate them straight
+    # into the pinned batch (config 3 scans tsg_prepare_batch's output)
+    palloc = PinnedAlloc(L) if args.config != 3 else None
     corpus = synth.generate(int(gb * 1e9), seed=args.seed + rank, sizes=sizes,
-                            layout="image" if args.config == 3 else "src")
+                            layout="image" if args.config == 3 else "src", alloc=palloc)
     if args.config == 5:      # 500 custom rules + allow rules + exclude blocks (+ builtins)
         cfg5, plants = synth.config5(500, seed=args.seed)
         cfg_path = "/tmp/tsg_bench_config5_%d.yaml" % rank
@@ -247,19 +384,23 @@ def main():
     # host content preparation over the files as read (SecretAnalyzer.Required +
     # IsBinary + CR strip + .pyc extraction, tsg_prepare_batch); for config 3
     # its output IS the scanned batch (bytes counted after gating)
-    paths, lens, _keep = _lib.pack_paths(corpus.paths)
+    # (measured on rank 0 only for configs other than 3: its output is a second
+    # copy of the batch, which every rank of an 8-GPU node need not hold)
+    prep_gbps, nk = None, ctypes.c_uint32()
     hpb = ctypes.c_void_p()
-    t0 = time.perf_counter()
-    _lib.check(L.tsg_prepare_batch(sc._rs, None, corpus.data.ctypes.data, corpus.offsets.ctypes.data, raw_files,
-                                   paths, lens, args.threads, ctypes.byref(hpb)))
-    tprep = time.perf_counter() - t0
-    d_, o_, i_, b_, nk = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(),
-                          ctypes.c_uint32())
-    _lib.check(L.tsg_prepared_view(hpb, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_), ctypes.byref(b_),
-                                   ctypes.byref(nk)))
-    prep_gbps = raw_bytes / tprep / 1e9
-    log("host feed prepare (Required + IsBinary + CR strip, %d threads): %.1f GB/s, %d of %d files kept" % (
-        args.threads, prep_gbps, nk.value, raw_files))
+    if args.config == 3 or rank == 0:
+        paths, lens, _keep = _lib.pack_paths(corpus.paths)
+        t0 = time.perf_counter()
+        _lib.check(L.tsg_prepare_batch(sc._rs, None, corpus.data.ctypes.data, corpus.offsets.ctypes.data,
+                                       raw_files, paths, lens, args.threads, ctypes.byref(hpb)))
+        tprep = time.perf_counter() - t0
+        d_, o_, i_, b_ = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(L.tsg_prepared_view(hpb, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_),
+                                       ctypes.byref(b_), ctypes.byref(nk)))
+        prep_gbps = raw_bytes / tprep / 1e9
+        del paths, lens, _keep
+        log("host feed prepare (Required + IsBinary + CR strip, %d threads): %.1f GB/s, %d of %d files kept" % (
+            args.threads, prep_gbps, nk.value, raw_files))
     if args.config == 3:
         n = nk.value
         offs = np.ctypeslib.as_array(ctypes.cast(o_, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy()
@@ -270,9 +411,10 @@ def main():
         scan_paths = ["/" + corpus.paths[i] for i in index]
         batch = PinnedBatch(L, data, offs, scan_paths, binf)
     else:
-        batch = PinnedBatch(L, corpus.data, corpus.offsets, corpus.paths)
-    L.tsg_prepared_free(hpb)
-    del corpus, paths, lens, _keep
+        batch = PinnedBatch(L, None, corpus.offsets, corpus.paths, pinned=palloc)
+    if hpb:
+        L.tsg_prepared_free(hpb)
+    del corpus
     nfiles, nbytes = batch.nfiles, batch.nbytes
     bin_ptr = batch.binary.ctypes.data if batch.binary is not None else None
     # config 4: this rank's share of 20 config-2 shards, streamed one after
@@ -281,8 +423,10 @@ def main():
     if args.config == 4:
         nshards = -(-20 // world)
         for j in range(1, min(args.distinct_shards, nshards)):
-            c2 = synth.generate(int(gb * 1e9), seed=args.seed + 1000 * j + rank, sizes=sizes, layout="src")
-            shard_batches.append(PinnedBatch(L, c2.data, c2.offsets, c2.paths))
+            pa = PinnedAlloc(L)
+            c2 = synth.generate(int(gb * 1e9), seed=args.seed + 1000 * j + rank, sizes=sizes, layout="src",
+                                alloc=pa)
+            shard_batches.append(PinnedBatch(L, None, c2.offsets, c2.paths, pinned=pa))
             del c2
         nbytes = sum(shard_batches[k % len(shard_batches)].nbytes for k in range(nshards))
         log("config 4: %d shards per rank (%d distinct), %.1f GB per rank per step" % (
@@ -438,7 +582,8 @@ def main():
                          "hits": stats[-1]["hits"], "candidates": stats[-1]["candidates"],
                          "confirm_files": stats[-1]["confirm_files"], "findings": findings,
                          "rules_with_findings": len(rules_hit)},
-        "host_feed": {"prepare_gbps": round(prep_gbps, 2), "prepare_kept_files": nk.value},
+        "host_feed": {"prepare_gbps": None if prep_gbps is None else round(prep_gbps, 2),
+                      "prepare_kept_files": nk.value if prep_gbps is not None else None},
         "cpu_baseline": None,
         "parity": None,
     }
@@ -520,38 +665,42 @@ def main():
 
     failed = False
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        idx = pick_sample(batch.offsets, int(args.cpu_sample_mb * 1e6), 8 << 20, args.seed)
+        procs = args.cpu_procs or cores
+        idx = pick_sample(batch.offsets, int(args.cpu_sample_mb * 1e6), args.seed)
         items = [(batch.paths[i], batch.file(i), bool(batch.binary[i]) if batch.binary is not None else False)
                  for i in idx]
-        gbps, ores, dt, nb = cpu_baseline(items, args.cpu_procs, cfg_path)
+        gbps, ores, dt, nb = cpu_baseline(items, procs, cfg_path)
         diff = [batch.paths[i] for j, i in enumerate(idx) if ores[j] != gpu_results[i]]
         ofind = sum(len(r["Findings"]) for r in ores)
         out["cpu_baseline"] = {
-            "value": round(gbps, 5), "unit": "GB/s", "cores": args.cpu_procs, "kind": "port",
-            "sample": "%d files / %.1f MB of the same batch (files <= 8 MB), oracle/secret_oracle.py "
-                      "(Python restatement of pkg/fanal/secret/scanner.go) in a %d-process pool, %.1f s"
-                      % (len(idx), nb / 1e6, args.cpu_procs, dt),
+            "value": round(gbps, 5), "unit": "GB/s", "cores": procs, "kind": "port",
+            "sample": "%d files / %.1f MB of the same batch (%d files > 8 MB, largest %.1f MB), "
+                      "oracle/secret_oracle.py (Python restatement of pkg/fanal/secret/scanner.go) in a "
+                      "%d-process pool on the %d cores this rank may use, %.1f s"
+                      % (len(idx), nb / 1e6, sum(1 for _, c, _ in items if len(c) > (8 << 20)),
+                         max(len(c) for _, c, _ in items) / 1e6, procs, procs, dt),
+            "cores_detail": cores_detail,
         }
         # the C++ restatement of the reference algorithm (every rule's keyword
         # gate + Go-regexp find-all over every file, no GPU prefilter) on the
         # same sample: a compiled CPU scanner closer to the Go reference's speed
         sargs = [S.ScanArgs(p, c, bf) for p, c, bf in items]
         t0 = time.perf_counter()
-        cres = S.scan_host_reference(sc, sargs, threads=args.cpu_procs)
+        cres = S.scan_host_reference(sc, sargs, threads=procs)
         cdt = time.perf_counter() - t0
         cdiff = sum(1 for j in range(len(idx)) if cres[j] != ores[j])
         out["cpu_baseline_cxx"] = {
-            "value": round(nb / cdt / 1e9, 5), "unit": "GB/s", "cores": args.cpu_procs, "kind": "port",
+            "value": round(nb / cdt / 1e9, 5), "unit": "GB/s", "cores": procs, "kind": "port",
             "sample": "same %d files, C++ Go-regexp restatement of scanner.go on every (file, rule) pair "
                       "(tsg_scan_host_reference), %d threads, %.2f s; diff vs oracle: %d files"
-                      % (len(idx), args.cpu_procs, cdt, cdiff),
+                      % (len(idx), procs, cdt, cdiff),
         }
         out["parity"] = {"sample_files": len(idx), "sample_bytes": nb, "sample_findings": ofind,
                          "diff_files": len(diff), "diff_examples": diff[:5], "cxx_diff_files": cdiff}
         failed = bool(diff) or cdiff > 0
         log("cpu baseline %.4f GB/s (oracle, %d procs), %.4f GB/s (C++ restatement, %d threads); "
             "parity diff files: %d (findings in sample: %d)" % (
-                gbps, args.cpu_procs, nb / cdt / 1e9, args.cpu_procs, len(diff), ofind))
+                gbps, procs, nb / cdt / 1e9, procs, len(diff), ofind))
 
     for b in shard_batches:
         b.free()

@@ -503,8 +503,10 @@ class GoRegexp:
         except UnicodeDecodeError:
             pass
         text = content.decode("utf-8", "surrogateescape")
-        lens = np.fromiter((1 if 0xDC80 <= ord(ch) <= 0xDCFF else len(ch.encode("utf-8"))
-                            for ch in text), dtype=np.int64, count=len(text))
+        # UTF-8 length of each char; an escaped invalid byte (U+DC80-U+DCFF) is 1
+        cp = np.frombuffer(text.encode("utf-32-le", "surrogatepass"), dtype=np.uint32)
+        lens = np.where(cp < 0x80, 1, np.where(cp < 0x800, 2, np.where(cp < 0x10000, 3, 4))).astype(np.int64)
+        lens[(cp >= 0xDC80) & (cp <= 0xDCFF)] = 1
         offs = np.zeros(len(text) + 1, dtype=np.int64)
         np.cumsum(lens, out=offs[1:])
         return text, offs

@@ -24,8 +24,10 @@ cases of scanner_test.go, the analyzer tests and the integration golden
 Strings in results are `str` decoded from Go byte strings with
 'surrogateescape' (an invalid byte survives as one lone surrogate).
 """
+import functools
 import json
 import os
+import re
 import unicodedata  # noqa: F401  (documented dependency of str.lower per char)
 
 import yaml
@@ -57,10 +59,13 @@ class Rule:
         return self.path is None or self.path.match_string(path)
 
     # scanner.go:174-186
-    def match_keywords(self, content):
+    def match_keywords(self, content, lower=None):
+        """`lower`: bytes.ToLower(content) computed once per file by the
+        caller (the same value for every rule)."""
         if not self.keywords:
             return True
-        lower = go_bytes_to_lower(content)
+        if lower is None:
+            lower = go_bytes_to_lower(content)
         for kw in self.keywords:
             if go_str_to_lower(kw).encode("utf-8", "surrogateescape") in lower:
                 return True
@@ -101,13 +106,18 @@ def go_bytes_to_lower(b):
     invalid byte becomes U+FFFD (bytes.Map writes RuneError's encoding)."""
     if b.isascii():
         return b.lower()
-    out = []
-    for ch in b.decode("utf-8", "surrogateescape"):
-        if 0xDC80 <= ord(ch) <= 0xDCFF:
-            out.append("�")
-        else:
-            out.append(_go_rune_lower(ch))
-    return "".join(out).encode("utf-8")
+    # ASCII letters lowered bytewise (a UTF-8 sequence has no ASCII byte), then
+    # every non-ASCII char (or escaped invalid byte) mapped on its own
+    text = b.lower().decode("utf-8", "surrogateescape")
+    return _NON_ASCII.sub(lambda m: _go_lower_nonascii(m.group()), text).encode("utf-8")
+
+
+_NON_ASCII = re.compile("[^\x00-\x7f]")
+
+
+@functools.lru_cache(maxsize=None)
+def _go_lower_nonascii(ch):
+    return "\ufffd" if 0xDC80 <= ord(ch) <= 0xDCFF else _go_rune_lower(ch)
 
 
 def go_str_to_lower(s):
@@ -246,6 +256,7 @@ class Scanner:
             return {"FilePath": file_path, "Findings": []}
         prepared = None
         censored = None
+        lower = None
         matched = []
         gblocks = _Blocks(content, self.exclude_block)
         for rule in self.rules:
@@ -253,7 +264,9 @@ class Scanner:
                 continue
             if rule.allow_path(file_path):
                 continue
-            if not rule.match_keywords(content):
+            if rule.keywords and lower is None:
+                lower = go_bytes_to_lower(content)
+            if not rule.match_keywords(content, lower):
                 continue
             if prepared is None:
                 prepared = GoRegexp.prepare(content)
@@ -269,8 +282,9 @@ class Scanner:
                     censored = bytearray(content)
                 censored = censor_location(loc, censored)
         findings = []
+        lines = _LineIndex(censored) if matched else None
         for rule, loc in matched:
-            f = to_finding(rule, loc, censored)
+            f = to_finding(rule, loc, censored, lines)
             if binary:
                 f["Match"] = 'Binary file %s matches a rule %s' % (go_quote(file_path), go_quote(rule.title))
                 f["Code"] = {"Lines": []}
@@ -347,8 +361,11 @@ def censor_location(loc, buf):          # scanner.go:465-473
     return buf
 
 
-def to_finding(rule, loc, content):     # scanner.go:475-488
-    start_line, end_line, code, match_line = find_location(loc[0], loc[1], content)
+def to_finding(rule, loc, content, lines=None):     # scanner.go:475-488
+    if lines is not None:
+        start_line, end_line, code, match_line = find_location_indexed(loc[0], loc[1], lines)
+    else:
+        start_line, end_line, code, match_line = find_location(loc[0], loc[1], content)
     return {
         "RuleID": rule.id, "Category": rule.category,
         "Severity": "UNKNOWN" if rule.severity == "" else rule.severity,
@@ -382,6 +399,62 @@ def find_location(start, end, content):  # scanner.go:495-558
         else:
             s = _s(raw)
         out.append({"Number": code_start + i + 1, "Content": s, "IsCause": in_cause,
+                    "Annotation": "", "Truncated": False, "Highlighted": s,
+                    "FirstCause": (not found_first) and in_cause, "LastCause": False})
+        found_first = found_first or in_cause
+    for ln in reversed(out):
+        if ln["IsCause"]:
+            ln["LastCause"] = True
+            break
+    return start_line_num + 1, end_line_num + 1, {"Lines": out}, match_line
+
+
+class _LineIndex:
+    """The '\n' positions of one (censored) content, built once per file: every
+    finding of a file is located on the same fully-censored buffer (Scan
+    censors all matches before the first toFinding, scanner.go:437-449), so
+    findLocation's Count / LastIndex / Index / Split (O(n) per finding in the
+    reference, O(n * findings) per file) become binary searches."""
+
+    def __init__(self, content):
+        import numpy as np
+        self.c = bytes(content)
+        self.nl = np.flatnonzero(np.frombuffer(self.c, dtype=np.uint8) == 10)
+        self.np = np
+
+    def line_bounds(self, i):           # lines[i] of bytes.Split(content, "\n")
+        nl = self.nl
+        b = int(nl[i - 1]) + 1 if i > 0 else 0
+        e = int(nl[i]) if i < len(nl) else len(self.c)
+        return b, e
+
+
+def find_location_indexed(start, end, idx):
+    """findLocation (scanner.go:495-558) over a _LineIndex: the same values as
+    find_location, checked against it by tests/test_oracle_regex.py."""
+    content, nl = idx.c, idx.nl
+    k = int(idx.np.searchsorted(nl, start, "left"))        # '\n' before start
+    start_line_num = k
+    line_start = int(nl[k - 1]) + 1 if k > 0 else 0
+    line_end = int(nl[k]) if k < len(nl) else len(content)
+    if line_end - line_start > 100:
+        line_start = line_start if start - line_start - 30 < 0 else start - 30
+        line_end = line_end if end + 20 > line_end else end + 20
+    match_line = _s(content[line_start:line_end])
+    end_line_num = start_line_num + (int(idx.np.searchsorted(nl, end, "left")) - k)
+    nlines = len(nl) + 1
+    code_start = max(start_line_num - 2, 0)
+    code_end = min(end_line_num + 2, nlines)
+    out = []
+    found_first = False
+    for real in range(code_start, code_end):
+        b, e = idx.line_bounds(real)
+        in_cause = start_line_num <= real <= end_line_num
+        if e - b > 100:
+            s = match_line if in_cause else _s(content[b:b + 100])
+        else:
+            s = _s(content[b:e])
+        out.append({"Number": real + 1, "Content": s, "IsCause": in_cause,
                     "Annotation": "", "Truncated": False, "Highlighted": s,
                     "FirstCause": (not found_first) and in_cause, "LastCause": False})
         found_first = found_first or in_cause

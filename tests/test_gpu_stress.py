@@ -16,7 +16,7 @@ import random
 import numpy as np
 import pytest
 
-from oracle import secret_oracle as so
+from _oracle_pool import oracle_scan_many
 from trivy_amd import secret as S
 from workload import synth
 
@@ -42,11 +42,18 @@ def test_config2_loguniform_pieces_gpu(monkeypatch):
     assert sum(len(h["Findings"]) for h in host) > 50
     for a, g, h in zip(args, got, host):
         assert g == h, a.FilePath
-    ref = so.Scanner(None)
+    # independent parity: the oracle on the 64 MB file, every file above
+    # 4 MB and a sample of the rest (host == GPU above is the superset check;
+    # the host confirmer shares code with the product, the oracle does not)
     rng = random.Random(5)
-    small = [i for i, a in enumerate(args) if len(a.Content) <= 1 << 20]
-    for i in rng.sample(small, min(300, len(small))):
-        assert got[i] == ref.scan(args[i].FilePath, args[i].Content), args[i].FilePath
+    large = [i for i, a in enumerate(args) if len(a.Content) > 4 << 20]
+    small = [i for i, a in enumerate(args) if len(a.Content) <= 4 << 20]
+    pick = sorted(large + rng.sample(small, min(300, len(small))))
+    assert any(len(args[i].Content) >= 64 << 20 for i in pick) and len(large) >= 5
+    want = oracle_scan_many([(args[i].FilePath, args[i].Content, False) for i in pick], procs=16)
+    assert sum(len(w["Findings"]) for w in want) > 100
+    for i, w in zip(pick, want):
+        assert got[i] == w, args[i].FilePath
 
 
 def _dense(nbytes):

@@ -263,7 +263,8 @@ def PrepareLayerTar(scanner, tar, skip_files=(), skip_dirs=(), config_path="", t
     Returns (ScanArgs list with "/"-prefixed image paths, walk dict with
     "files", "opq_dirs", "wh_files").  scan=True also runs the prepared batch
     through tsg_scan_batch straight from the prepared (pinned when `pinned`)
-    buffer and returns (ScanArgs list, walk dict, [types.Secret])."""
+    buffer and returns (ScanArgs list, walk dict, [types.Secret]); scan="result"
+    returns a report.ScanResult in place of the list."""
     L = _lib.lib()
     buf = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
     sf = [s.encode() for s in skip_files]
@@ -294,6 +295,9 @@ def PrepareLayerTar(scanner, tar, skip_files=(), skip_dirs=(), config_path="", t
             return out, walk
         res = ctypes.c_void_p()
         _lib.check(L.tsg_scan_batch(scanner.engine(), d, o, n, pp, ctypes.cast(pl, ctypes.c_void_p), b, ctypes.byref(res)))
+        if scan == "result":                 # the C result object, for report assembly
+            from .report import ScanResult
+            return out, walk, ScanResult(res)
         try:
             secrets = _lib.result_json(res)
         finally:

@@ -371,7 +371,10 @@ IMAGE_DIRS = ("usr/share/doc/pkg%d", "usr/lib/python3.%d/site-packages/mod", "us
 
 
 def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4, near_miss=0.1,
-             base_bytes=32 << 20, max_files=None, layout="src"):
+             base_bytes=32 << 20, max_files=None, layout="src", alloc=None):
+    """A seeded Corpus of ~total_bytes.  `alloc(n)` (optional) returns the
+    uint8 array of n bytes the corpus is written into -- e.g. a view of pinned
+    host memory, so a bench holds one copy of its batch instead of two."""
     rng = random.Random(seed)
     samples = load_samples()
     rule_ids = sorted(k for k, v in samples.items() if v)
@@ -384,7 +387,11 @@ def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4,
     offsets = np.zeros(n + 1, dtype=np.uint64)
     np.cumsum(np.array(sz, dtype=np.uint64), out=offsets[1:])
     total = int(offsets[-1])
-    data = np.zeros(total + 64, dtype=np.uint8)
+    if alloc is None:
+        data = np.zeros(total + 64, dtype=np.uint8)
+    else:
+        data = alloc(total + 64)
+        data[total:] = 0
     paths = []
     seg = 1 << 16
     B = len(base)
