@@ -2,8 +2,8 @@
 
 The client/server wire form of the secret results, restated with the Python
 protobuf runtime (an independent proto3 implementation) over a descriptor
-built here from rpc/common/service.proto:152-156 (Secret) and 191-223
-(Layer, Line, Code, SecretFinding; field 9 of SecretFinding is reserved),
+built here from rpc/common/service.proto:152-156 (Layer), 191-204 (Line,
+Code), 206-218 (SecretFinding; field 9 is reserved) and 220-223 (Secret),
 filled exactly as pkg/rpc/convert.go does:
 
   ConvertToRPCSecrets / ConvertToRPCSecretFindings   convert.go:146-175
