@@ -254,8 +254,48 @@ void tsg_prepared_free(tsg_prepared* p);
 int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const uint8_t* tar, size_t len,
                           const char* const* skip_files, uint32_t nskip_files, const char* const* skip_dirs,
                           uint32_t nskip_dirs, int threads, int pinned, tsg_prepared** out);
-/* The kept files' ScanArgs.FilePath: "/" + the walker's path (image files,
- * secret.go:131-135); only for batches made by tsg_prepare_layer_tar. */
+/* Analyzer-group options of the secret feed (pkg/fanal/analyzer/analyzer.go
+ * AnalyzerOptions / walker.Option):
+ *   config_path      SecretAnalyzer.configPath; Required skips its base name;
+ *   file_patterns    --file-patterns entries "fileType:regexPattern"
+ *                    (analyzer.go:332-350: a malformed entry or regexp fails
+ *                    with its error text); "secret:<re>" entries force the
+ *                    secret analyzer on matching paths whatever Required says
+ *                    (filePatternMatch, analyzer.go:417-419,522-530);
+ *   skip_files/dirs  --skip-files / --skip-dirs (walker.Option: doublestar
+ *                    patterns; for tsg_prepare_fs_tree made relative to the
+ *                    root by BuildSkipPaths, fs.go:99-149);
+ *   threads          host threads (0: up to 16); pinned: pack into pinned
+ *                    host memory (tsg_alloc_pinned) for tsg_scan_batch. */
+typedef struct tsg_feed_opts {
+  const char* config_path;
+  const char* const* file_patterns;
+  uint32_t n_file_patterns;
+  const char* const* skip_files;
+  uint32_t n_skip_files;
+  const char* const* skip_dirs;
+  uint32_t n_skip_dirs;
+  int32_t threads;
+  int32_t pinned;
+} tsg_feed_opts;
+/* tsg_prepare_batch with feed options (skip lists unused: the files are given). */
+int tsg_prepare_batch_opts(const tsg_ruleset* rs, const uint8_t* raw, const uint64_t* raw_offsets, uint32_t nfiles,
+                           const char* const* paths, const uint32_t* path_lens, const tsg_feed_opts* opts,
+                           tsg_prepared** out);
+/* tsg_prepare_layer_tar with feed options. */
+int tsg_prepare_layer_tar_opts(const tsg_ruleset* rs, const uint8_t* tar, size_t len, const tsg_feed_opts* opts,
+                               tsg_prepared** out);
+/* `trivy fs` over a directory tree on disk: walker.FS.Walk (pkg/fanal/walker/
+ * fs.go:25-97; filepath.WalkDir order, symlinks not followed, defaultSkipDirs
+ * **\/.git proc sys dev, permission errors ignored), AnalyzeFile's gate before
+ * a file is opened (analyzer.go:403-419), the kept files read by `threads`
+ * readers, then tsg_prepare_batch's preparation.  ScanArgs.FilePath is the
+ * walker's path relative to the root (tsg_prepared_paths).  The walk JSON also
+ * reports "read_bytes", "walk_ms", "read_ms", "prep_ms". */
+int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_opts* opts, tsg_prepared** out);
+/* The kept files' ScanArgs.FilePath: "/" + the walker's path for a layer tar
+ * (image files, secret.go:131-135), the path relative to the root for an fs
+ * tree; only for batches made by tsg_prepare_layer_tar* / tsg_prepare_fs_tree. */
 int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens);
 /* {"files": [every regular file the walk hands to the analyzers], "opq_dirs":
  * [...], "wh_files": [...], "pinned": bool} (Walk's return values, tar.go:90);

@@ -150,3 +150,87 @@ def walk(tar_bytes, skip_files=(), skip_dirs=()):
                 continue
             files.append((file_path, tf.extractfile(m).read()))
     return files, opq, wh
+
+
+# ------------------------------------------------------------ walker.FS.Walk
+def build_skip_paths(base, paths):
+    """walker.FS.BuildSkipPaths (pkg/fanal/walker/fs.go:99-149) + CleanSkipPaths."""
+    import os
+    abs_base = os.path.abspath(base)
+    out = []
+    for p in paths:
+        rel = os.path.relpath(os.path.abspath(p), abs_base)
+        if not os.path.isabs(p) and rel.startswith(".."):
+            r = p                                            # #1: as given
+        else:
+            r = rel                                          # #2, #3
+        out.append(r)
+    return clean_skip_paths(out)
+
+
+DEFAULT_SKIP_DIRS = ["**/.git", "proc", "sys", "dev"]        # walker/walk.go:11-16
+
+
+def walk_fs(root, skip_files=(), skip_dirs=()):
+    """walker.FS.Walk (fs.go:25-97) on Python's os.scandir: filepath.WalkDir's
+    lexical order, directories entered as met, symlinks not followed,
+    permission errors ignored.  Returns [(rel_path, abs_path)] of the regular
+    files handed to the WalkFunc."""
+    import os
+    sf = build_skip_paths(root, skip_files)
+    sd = build_skip_paths(root, skip_dirs) + DEFAULT_SKIP_DIRS
+    out = []
+
+    def rec(path, rel):
+        try:
+            ents = sorted(os.scandir(path), key=lambda e: os.fsencode(e.name))
+        except PermissionError:
+            return
+        for e in ents:
+            crel = e.name if rel == "." else rel + "/" + e.name
+            if e.is_dir(follow_symlinks=False):
+                if skip_path(crel, sd):
+                    continue
+                rec(e.path, crel)
+            elif e.is_file(follow_symlinks=False):
+                if skip_path(crel, sf):
+                    continue
+                out.append((crel, e.path))
+    if os.path.isdir(root) and not os.path.islink(root):
+        if not skip_path(".", sd):
+            rec(root, ".")
+    elif os.path.isfile(root) and not os.path.islink(root) and not skip_path(".", sf):
+        out.append((".", root))
+    return out
+
+
+def fs_feed(analyzer, root, skip_files=(), skip_dirs=(), file_patterns=()):
+    """`trivy fs ROOT` up to Scan: walk, AnalyzeFile's gate (analyzer.go:403-419:
+    a "secret:<re>" --file-patterns match or Required on the path with leading
+    '/' trimmed), Analyze's binary check / CR strip / printable extraction.
+    analyzer: an oracle.secret_oracle.SecretAnalyzer.  Returns
+    [(FilePath, Content, Binary)] in walk order."""
+    import os
+    from .goregex import GoRegexp
+    from . import secret_oracle as so
+    pats = []
+    for p in file_patterns:
+        typ, sep, rx = p.partition(":")
+        if not sep:
+            raise ValueError("invalid file pattern (%s)" % p)
+        r = GoRegexp(rx)
+        if typ == "secret":
+            pats.append(r)
+    out = []
+    for rel, path in walk_fs(root, skip_files, skip_dirs):
+        clean = rel.lstrip("/")
+        size = os.lstat(path).st_size
+        if not any(r.match_string(clean) for r in pats) and not analyzer.required(clean, size):
+            continue
+        raw = open(path, "rb").read()
+        binary = so.is_binary(raw[:300])
+        if binary and so.go_ext(rel) != ".pyc":
+            continue
+        content = so.extract_printable_bytes(raw) if binary else raw.replace(b"\r", b"")
+        out.append((rel, content, binary))
+    return out

@@ -91,10 +91,12 @@ def test_largest_k1_chunk_gpu(monkeypatch):
     assert sum(len(w["Findings"]) for w in want) > 20
 
 
-@pytest.mark.parametrize("variant,abl,chunk", [("1", "0", "4096"), ("3", "464", "2048"), ("3", "16", "4096"),
-                                               ("3", "0", "8192"), ("4", "0", "1024"), ("4", "0", "4096"),
-                                               ("4", "0", "16384")])
-def test_k1_variants_agree_gpu(monkeypatch, variant, abl, chunk):
+@pytest.mark.parametrize("variant,abl,chunk,extra", [
+    ("1", "0", "4096", ""), ("3", "464", "2048", ""), ("3", "16", "4096", ""), ("3", "0", "8192", ""),
+    ("4", "0", "1024", ""), ("4", "0", "4096", ""), ("4", "0", "16384", ""),
+    ("5", "464", "1024", ""), ("5", "464", "2048", "TSG_K1_LINE5=2"), ("5", "464", "8192", "TSG_K1_SINGLE5=1"),
+    ("5", "464", "2048", "TSG_K1_SINGLE5=1+TSG_K1_LINE5=2")])
+def test_k1_variants_agree_gpu(monkeypatch, variant, abl, chunk, extra):
     # every K1 build whose layout bits keep results valid (v1; v3 with
     # deferred outputs / rolled loop / 64-B lines / temporal loads; v4, two
     # streams per lane, up to its largest chunk) gives the default engine's
@@ -106,6 +108,9 @@ def test_k1_variants_agree_gpu(monkeypatch, variant, abl, chunk):
     monkeypatch.setenv("TSG_K1_VARIANT", variant)
     monkeypatch.setenv("TSG_K1_ABL", abl)
     monkeypatch.setenv("TSG_K1_CHUNK", chunk)
+    for kv in filter(None, extra.split("+")):
+        k, _, v = kv.partition("=")
+        monkeypatch.setenv(k, v)
     got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
     assert stats["chunk_bytes"] == int(chunk)
     assert got == want

@@ -104,6 +104,42 @@ SIGNATURES = [
                                         ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
 ]
 
+class TsgFeedOpts(ctypes.Structure):
+    _fields_ = [("config_path", ctypes.c_char_p), ("file_patterns", c_char_pp), ("n_file_patterns", ctypes.c_uint32),
+                ("skip_files", c_char_pp), ("n_skip_files", ctypes.c_uint32), ("skip_dirs", c_char_pp),
+                ("n_skip_dirs", ctypes.c_uint32), ("threads", ctypes.c_int32), ("pinned", ctypes.c_int32)]
+
+
+SIGNATURES += [
+    ("tsg_prepare_batch_opts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(TsgFeedOpts),
+                                              ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prepare_layer_tar_opts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.POINTER(TsgFeedOpts), ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_prepare_fs_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(TsgFeedOpts),
+                                           ctypes.POINTER(ctypes.c_void_p)]),
+]
+
+
+def feed_opts(config_path="", file_patterns=(), skip_files=(), skip_dirs=(), threads=0, pinned=False):
+    """A TsgFeedOpts plus the objects its pointers refer to (keep both alive)."""
+    keep = []
+
+    def arr(v):
+        b = [x.encode("utf-8", "surrogateescape") if isinstance(x, str) else x for x in v]
+        a = (ctypes.c_char_p * max(1, len(b)))(*b)
+        keep.extend([b, a])
+        return ctypes.cast(a, c_char_pp), len(b)
+    o = TsgFeedOpts()
+    o.config_path = (config_path or "").encode("utf-8", "surrogateescape")
+    o.file_patterns, o.n_file_patterns = arr(file_patterns)
+    o.skip_files, o.n_skip_files = arr(skip_files)
+    o.skip_dirs, o.n_skip_dirs = arr(skip_dirs)
+    o.threads = threads
+    o.pinned = 1 if pinned else 0
+    return o, keep
+
+
 class TsgLayer(ctypes.Structure):
     _fields_ = [("digest", ctypes.c_char_p), ("diff_id", ctypes.c_char_p), ("created_by", ctypes.c_char_p)]
 

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <memory>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -16,6 +18,7 @@
 #include "prefilter.h"
 #include "report.h"
 #include "scanner.h"
+#include "walkfs.h"
 #include "wire.h"
 
 using namespace tsg;
@@ -757,34 +760,99 @@ void json_str_array(std::string* js, const std::vector<std::string>& v) {
 int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const uint8_t* tar, size_t len,
                           const char* const* skip_files, uint32_t nskip_files, const char* const* skip_dirs,
                           uint32_t nskip_dirs, int threads, int pinned, tsg_prepared** out) {
-  if (!rs || !out || (len && !tar) || (nskip_files && !skip_files) || (nskip_dirs && !skip_dirs))
-    return fail(TSG_ERR_INVALID, "NULL argument");
+  tsg_feed_opts o{};
+  o.config_path = config_path;
+  o.skip_files = skip_files;
+  o.n_skip_files = nskip_files;
+  o.skip_dirs = skip_dirs;
+  o.n_skip_dirs = nskip_dirs;
+  o.threads = threads;
+  o.pinned = pinned;
+  return tsg_prepare_layer_tar_opts(rs, tar, len, &o, out);
+}
+
+namespace {
+int default_threads(int threads) {
+  return threads > 0 ? threads : static_cast<int>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+}
+
+std::vector<std::string> str_list(const char* const* v, uint32_t n) {
+  std::vector<std::string> out;
+  for (uint32_t i = 0; i < n; ++i) out.emplace_back(v[i]);
+  return out;
+}
+
+// tsg_feed_opts -> FeedOpts (+ walker skip lists); NULL opts = defaults
+bool feed_opts(const tsg_feed_opts* o, FeedOpts* fo, std::vector<std::string>* sf, std::vector<std::string>* sd,
+               int* threads, bool* pinned, std::string* err) {
+  *threads = default_threads(o ? o->threads : 0);
+  *pinned = o && o->pinned;
+  if (!o) return true;
+  if ((o->n_file_patterns && !o->file_patterns) || (o->n_skip_files && !o->skip_files) ||
+      (o->n_skip_dirs && !o->skip_dirs)) {
+    *err = "NULL argument";
+    return false;
+  }
+  fo->config_path = o->config_path ? o->config_path : "";
+  *sf = str_list(o->skip_files, o->n_skip_files);
+  *sd = str_list(o->skip_dirs, o->n_skip_dirs);
+  return parse_file_patterns(str_list(o->file_patterns, o->n_file_patterns), fo, err);
+}
+
+void set_scan_paths(tsg_prepared* p, const std::vector<std::string>& paths, const char* prefix) {
+  for (uint32_t i : p->b.index) p->scan_paths.push_back(prefix + paths[i]);
+  for (const auto& sp : p->scan_paths) {
+    p->path_ptrs.push_back(sp.c_str());
+    p->path_lens.push_back(static_cast<uint32_t>(sp.size()));
+  }
+}
+}  // namespace
+
+int tsg_prepare_batch_opts(const tsg_ruleset* rs, const uint8_t* raw, const uint64_t* raw_offsets, uint32_t nfiles,
+                           const char* const* paths, const uint32_t* path_lens, const tsg_feed_opts* opts,
+                           tsg_prepared** out) {
+  if (!rs || !out || !raw_offsets || (nfiles && (!raw || !paths))) return fail(TSG_ERR_INVALID, "NULL argument");
+  FeedOpts fo;
   std::vector<std::string> sf, sd;
-  for (uint32_t i = 0; i < nskip_files; ++i) sf.emplace_back(skip_files[i]);
-  for (uint32_t i = 0; i < nskip_dirs; ++i) sd.emplace_back(skip_dirs[i]);
-  LayerWalk walk;
+  int nt;
+  bool pinned;
   std::string err;
+  if (!feed_opts(opts, &fo, &sf, &sd, &nt, &pinned, &err)) return fail(TSG_ERR_INVALID, err);
+  auto* p = new tsg_prepared();
+  if (!prepare_batch(*rs->rs, fo, raw, raw_offsets, nfiles, paths, path_lens, nt, &p->b, &err,
+                     pinned ? pinned_alloc : nullptr)) {
+    delete p;
+    return fail(TSG_ERR_INVALID, err);
+  }
+  *out = p;
+  return TSG_OK;
+}
+
+int tsg_prepare_layer_tar_opts(const tsg_ruleset* rs, const uint8_t* tar, size_t len, const tsg_feed_opts* opts,
+                               tsg_prepared** out) {
+  if (!rs || !out || (len && !tar)) return fail(TSG_ERR_INVALID, "NULL argument");
+  FeedOpts fo;
+  std::vector<std::string> sf, sd;
+  int nt;
+  bool pinned;
+  std::string err;
+  if (!feed_opts(opts, &fo, &sf, &sd, &nt, &pinned, &err)) return fail(TSG_ERR_INVALID, err);
+  LayerWalk walk;
   if (!walk_layer_tar(tar, len, sf, sd, &walk, &err)) return fail(TSG_ERR_INVALID, err);
   std::vector<uint64_t> starts, sizes;
-  std::vector<std::string> paths;   // Required's path: the walker's (no leading '/') (analyzer.go:407-408)
+  std::vector<std::string> paths;
   for (const TarFile& f : walk.files) {
     starts.push_back(f.offset);
     sizes.push_back(f.size);
     paths.push_back(f.path);
   }
   auto* p = new tsg_prepared();
-  const int nt = threads > 0 ? threads : static_cast<int>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-  if (!prepare_files(*rs->rs, config_path ? config_path : "", tar, starts.data(), sizes.data(), paths, nt, &p->b, &err,
+  if (!prepare_files(*rs->rs, fo, tar, starts.data(), sizes.data(), paths, nt, &p->b, &err,
                      pinned ? pinned_alloc : nullptr)) {
     delete p;
     return fail(TSG_ERR_INVALID, err);
   }
-  // files extracted from an image get a leading '/' for Scan (secret.go:131-135)
-  for (uint32_t i : p->b.index) p->scan_paths.push_back("/" + paths[i]);
-  for (const auto& sp : p->scan_paths) {
-    p->path_ptrs.push_back(sp.c_str());
-    p->path_lens.push_back(static_cast<uint32_t>(sp.size()));
-  }
+  set_scan_paths(p, paths, "/");
   std::string& js = p->walk_json;
   js = "{\"files\": ";
   json_str_array(&js, paths);
@@ -799,9 +867,71 @@ int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const 
   return TSG_OK;
 }
 
+int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_opts* opts, tsg_prepared** out) {
+  if (!rs || !out || !root) return fail(TSG_ERR_INVALID, "NULL argument");
+  FeedOpts fo;
+  std::vector<std::string> sf, sd;
+  int nt;
+  bool pinned;
+  std::string err;
+  if (!feed_opts(opts, &fo, &sf, &sd, &nt, &pinned, &err)) return fail(TSG_ERR_INVALID, err);
+  const auto t0 = std::chrono::steady_clock::now();
+  FsWalk walk;
+  if (!walk_fs_tree(root, sf, sd, &walk, &err)) return fail(TSG_ERR_INVALID, err);
+  const auto t1 = std::chrono::steady_clock::now();
+  // AnalyzeFile's gate before the file is opened (analyzer.go:417-419)
+  const uint32_t n = static_cast<uint32_t>(walk.files.size());
+  std::vector<uint8_t> want(n, 0);
+  std::vector<uint64_t> starts(n, 0);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!secret_analyzer_wants(*rs->rs, fo, walk.files[i].rel, walk.files[i].size)) continue;
+    want[i] = 1;
+    starts[i] = total;
+    total += walk.files[i].size;
+  }
+  std::unique_ptr<uint8_t[]> raw(new uint8_t[std::max<uint64_t>(total, 1)]);
+  std::vector<uint64_t> got;
+  if (!read_fs_files(walk, want, starts, raw.get(), nt, &got, &err)) return fail(TSG_ERR_INVALID, err);
+  const auto t2 = std::chrono::steady_clock::now();
+  std::vector<uint64_t> rstarts, rsizes;
+  std::vector<std::string> paths;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!want[i] || got[i] == UINT64_MAX) continue;
+    rstarts.push_back(starts[i]);
+    rsizes.push_back(got[i]);
+    paths.push_back(walk.files[i].rel);
+  }
+  fo.assume_required = true;
+  auto* p = new tsg_prepared();
+  if (!prepare_files(*rs->rs, fo, raw.get(), rstarts.data(), rsizes.data(), paths, nt, &p->b, &err,
+                     pinned ? pinned_alloc : nullptr)) {
+    delete p;
+    return fail(TSG_ERR_INVALID, err);
+  }
+  const auto t3 = std::chrono::steady_clock::now();
+  set_scan_paths(p, paths, "");                 // fs scans: input.Dir is the root, no "/" prefix (secret.go:131-135)
+  std::vector<std::string> all;
+  for (const FsFile& f : walk.files) all.push_back(f.rel);
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  std::string& js = p->walk_json;
+  js = "{\"files\": ";
+  json_str_array(&js, all);
+  js += ", \"read_bytes\": " + std::to_string(total);
+  js += ", \"walk_ms\": " + std::to_string(ms(t0, t1)) + ", \"read_ms\": " + std::to_string(ms(t1, t2)) +
+        ", \"prep_ms\": " + std::to_string(ms(t2, t3));
+  js += ", \"pinned\": ";
+  js += p->b.pinned ? "true" : "false";
+  js += "}";
+  *out = p;
+  return TSG_OK;
+}
+
 int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens) {
   if (!p || !paths || !lens) return fail(TSG_ERR_INVALID, "NULL argument");
-  if (p->path_ptrs.size() != p->b.index.size()) return fail(TSG_ERR_INVALID, "not a layer-tar batch");
+  if (p->path_ptrs.size() != p->b.index.size()) return fail(TSG_ERR_INVALID, "not a layer-tar or fs-tree batch");
   *paths = p->path_ptrs.data();
   *lens = p->path_lens.data();
   return TSG_OK;

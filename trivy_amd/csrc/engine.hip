@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <thread>
 
@@ -924,6 +925,619 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
 }
 
+// K1 v5: v3's pass over a compact table, so two workgroups share a CU.
+//  * table: the scan DFA's byte classes with identical transition columns
+//    merged (exact: the automaton cannot tell them apart), rows of exactly
+//    Cr = C rounded to an odd dword count, no spare slot and no inline
+//    metadata; entries are the next state's row offset in DWORDS, so the
+//    transition address is one v_lshl_add ((s << 2) + class * 2) and offsets
+//    reach 256 KiB.  The builtin rules: 758 states x 50 classes = 75.8 KB.
+//  * output states (rows >= first_out) are looked up in global memory
+//    (L2-resident: oidx[row - first_out] -> OutMeta, output list), only at
+//    the rare drain of a lane's parked outputs;
+//  * LDS = class map + table + per-wave hit buffers of kH entries; with the
+//    builtin rules and kH = 64 that is 80.2 KB, two 1024-thread workgroups
+//    per CU (32 waves; kWpe = 8 waves per SIMD caps K1 at 64 VGPRs);
+//  * a 16-byte word is walked in two halves of 8 bytes: the 8 class reads
+//    first, then the 8 dependent transitions with a running max; a half whose
+//    max reaches the output rows (rare) is walked once more to park its
+//    outputs, so no per-byte state array is kept live.
+// Everything else (guided schedule, file-boundary words, '\n' counts,
+// fold-special flags, keyword register masks, deferred outputs) is v3's.
+struct K1Out5 {
+  const uint16_t* oidx;   // global: row - first_out -> output-state index
+};
+
+template <uint32_t kH>
+__device__ __forceinline__ void k1_emit_id5(const K1Ctx& x, K1Stream& t, uint32_t id, unsigned long long q) {
+  if (id < x.nkw) {
+    atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
+    return;
+  }
+  const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
+  if (li < kH) {
+    x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
+  } else {                                               // buffer full: straight to the region
+    const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
+    if (gi < x.region_cap) {
+      x.hits[gi] = (q << 24) | (id - x.nkw);
+    } else {                                             // region full: the shared overflow pool
+      const uint32_t oi = atomicAdd(x.over_cnt, 1u);
+      if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
+    }
+  }
+}
+
+template <uint32_t kH>
+__device__ __forceinline__ void k1_out5(const K1Ctx& x, const K1Out5& o, K1Stream& t, uint32_t st,
+                                        unsigned long long q) {
+  const OutMeta m = x.meta[o.oidx[st - x.first_out]];
+  t.kw0 |= m.kw0;
+  t.kw1 |= m.kw1;
+  for (uint32_t j = 0; j < m.list_count; ++j) k1_emit_id5<kH>(x, t, x.list[m.list_begin + j], q);
+}
+
+template <uint32_t kH>
+__device__ __forceinline__ void k1_drain5(const K1Ctx& x, const K1Out5& o, K1Stream& t, OutBuf& ob) {
+  for (uint32_t i = 0; i < ob.n; ++i) {
+    const uint32_t e = ob.p[i * ob.stride];
+    k1_out5<kH>(x, o, t, e & 0xffffu, t.emit + (e >> 16));
+  }
+  ob.n = 0;
+}
+
+// LDS layout of v5: [0, 256) class map (merged class * 2), [256, ...) table
+constexpr uint32_t kTabOff5 = 256;
+__device__ __forceinline__ uint32_t k1_step5(uint32_t s, uint32_t c2) { return k1_lds16((s << 2) + c2 + kTabOff5); }
+
+// One 16-byte word with file-boundary and range-end checks (rare lines).
+template <uint32_t kH>
+__device__ __forceinline__ void k1_word_slow5(const K1Ctx& x, const K1Out5& o, K1Stream& t, const uint32_t w[4]) {
+  const unsigned long long end = t.end;
+  unsigned long long fend = x.offsets[t.f + 1];
+  if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
+  for (int k = 0; k < 16; ++k) {
+    const unsigned long long q = t.p + k;
+    if (q >= end) break;
+    if (q >= fend) {
+      flush_kw(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
+      do { ++t.f; fend = x.offsets[t.f + 1]; } while (q >= fend);
+      t.s = 0;
+      t.p12 = 0;
+    }
+    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    t.s = k1_step5(t.s, k1_lds8(b));
+    if (q >= t.emit) {
+      t.nl += (b == 0x0au);
+      if (t.s >= x.first_out) k1_out5<kH>(x, o, t, t.s, q);
+    }
+    t.p12 = ((t.p12 << 8) & 0xff00u) | b;
+  }
+  t.p += 16;
+  t.lim = min(end, fend);
+}
+
+__device__ __forceinline__ void k1_park5(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t st, uint32_t k,
+                                         bool* full) {
+  if (ob.n < kOutSlots) {
+    ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k - t.emit) << 16) | st;
+    ++ob.n;
+  } else {
+    *full = true;
+  }
+}
+
+template <uint32_t kH>
+__device__ __forceinline__ void k1_word5(const K1Ctx& x, const K1Out5& o, K1Stream& t, OutBuf& ob, uint32_t w0,
+                                         uint32_t w1, uint32_t w2, uint32_t w3) {
+  const bool emit = t.p >= t.emit;
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t s = t.s;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t c2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c2[k] = k1_lds8((w[2 * h + (k >> 2)] >> ((k & 3) * 8)) & 0xffu);
+    const uint32_t s0 = s;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s = k1_step5(s, c2[k]);
+      mx = max(mx, s);
+    }
+    if (emit && mx >= x.first_out) {
+      // rare: walk the half again from its start state and park (or, with the
+      // slots full, handle) every output position
+      uint32_t r = s0;
+      for (int k = 0; k < 8; ++k) {
+        r = k1_step5(r, c2[k]);
+        if (r >= x.first_out) {
+          bool full = false;
+          k1_park5(x, t, ob, r, 8 * h + k, &full);
+          if (full) k1_out5<kH>(x, o, t, r, t.p + 8 * h + k);
+        }
+      }
+    }
+  }
+  t.s = s;
+  if (emit) {
+    uint32_t u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t xx = w[j] ^ 0x0a0a0a0au;
+      u[j] = ((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu;   // bit 7 of a byte: not '\n'
+    }
+    t.nl += 128u - (__popc(u[0]) + __popc(u[1]) + __popc(u[2]) + __popc(u[3]));
+  }
+  t.p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
+  t.p += 16;
+}
+
+// kWpe: waves per SIMD the register budget is sized for (8: two 1024-thread
+// workgroups per CU, <= 64 VGPRs; 4: one); kW: 16-byte words per register
+// line; kH: per-wave LDS hit buffer entries.
+template <int kWpe, int kW, uint32_t kH>
+__global__ __attribute__((amdgpu_flat_work_group_size(1024, 1024), amdgpu_waves_per_eu(kWpe, kWpe)))
+void tsg_k1_scan_v5(
+    const uint8_t* __restrict__ data, unsigned long long total,
+    const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls, uint32_t table_bytes, uint32_t first_out,
+    const OutMeta* __restrict__ g_meta, const uint16_t* __restrict__ g_oidx, const uint32_t* __restrict__ g_list,
+    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
+    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
+    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
+    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
+    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
+    uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr uint32_t kThreads = 1024, kWaves = kThreads / 64;
+  constexpr uint32_t kL = kW * 16;
+  if (!k1_lds_base_ok(smem)) {                   // the integer LDS addresses assume a zero base
+    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
+    return;
+  }
+  const uint32_t padded = (table_bytes + 15) & ~15u;
+  const uint32_t hits_off = kTabOff5 + padded;
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
+  uint32_t* s_hitcnt = s_hits + kWaves * kH;
+  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_block[0] = 0;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(g_next);
+    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff5);
+    for (uint32_t i = threadIdx.x; i < padded / 16; i += kThreads) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += kThreads) smem[i] = g_cls[i];
+  }
+  K1Ctx x;
+  x.data = data; x.total = total; x.chunk = chunk;
+  x.offsets = offsets; x.nfiles = nfiles;
+  x.next = nullptr; x.cls = smem;
+  x.first_out = first_out; x.nclasses = 0;
+  x.meta = g_meta;
+  x.list = g_list;
+  x.nkw = nkw;
+  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
+  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
+  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
+  x.w_hits = s_hits + wid * kH; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
+  const K1Out5 o{g_oidx};
+  __syncthreads();
+  // v3's guided schedule (4-, then 2-, then 1-chunk ranges per lane)
+  const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
+  const unsigned long long n1 = min(nchunks, W * 64 * tail_rounds);
+  const unsigned long long n2 = min(nchunks - n1, W * 128 * tail_rounds);
+  const unsigned long long n4 = nchunks - n1 - n2;
+  const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
+  const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
+  for (;;) {
+    unsigned long long item = 0;
+    if (lane == 0) {
+      item = atomicAdd(item_ctr, 1u);
+      *x.w_hitcnt = 0;
+    }
+    item = __shfl(item, 0);
+    if (item >= nitems) break;                                 // wave-uniform exit
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long c0, rend;
+    uint32_t kU;
+    if (item < i4) { kU = 4; c0 = item * 256; rend = n4; }
+    else if (item < i4 + i2) { kU = 2; c0 = n4 + (item - i4) * 128; rend = n4 + n2; }
+    else { kU = 1; c0 = n4 + n2 + (item - i4 - i2) * 64; rend = nchunks; }
+    x.item_base = c0 * static_cast<unsigned long long>(chunk);
+    const unsigned long long c = c0 + lane * kU;
+    if (c < rend) {
+      K1Stream t;
+      k1_init(x, t, min(c * chunk, total), warm_lines * kL);
+      t.end = min(min(c + kU, rend) * chunk, total);
+      t.cend = min(t.emit + chunk, t.end);
+      t.ci = c;
+      if (t.p < t.end) t.lim = min(t.end, x.offsets[t.f + 1]);
+      OutBuf ob{obuf + blockIdx.x * kThreads + threadIdx.x, gridDim.x * kThreads, 0};
+      v4u cur[kW], nxt[kW];
+      bool have = false;
+      for (;;) {
+        if (!(t.p < t.lim || t.p < t.end)) break;
+        if (t.p >= t.cend && t.cend < t.end) {                // a chunk of the range is done
+          if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+          t.nl = 0;
+          ++t.ci;
+          t.cend = min(t.cend + chunk, t.end);
+        }
+        if (t.p + kL <= t.lim) {
+          if (!have) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) cur[i] = *reinterpret_cast<const v4u*>(data + t.p + 16 * i);
+          }
+          have = t.p + 2 * kL <= t.lim;
+          if (have) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) nxt[i] = *reinterpret_cast<const v4u*>(data + t.p + kL + 16 * i);
+          }
+          if (x.primary) {
+            uint32_t hb = 0;
+#pragma unroll
+            for (int i = 0; i < kW; ++i) hb |= cur[i].x | cur[i].y | cur[i].z | cur[i].w;
+            if ((hb & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
+          }
+#pragma unroll 1
+          for (int i = 0; i < kW; ++i) k1_word5<kH>(x, o, t, ob, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+          if (have) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) cur[i] = nxt[i];
+          }
+        } else {
+          // a line with a file boundary or the range end (rare): word by word
+          have = false;
+          k1_drain5<kH>(x, o, t, ob);                        // parked outputs belong to file t.f
+          for (int i = 0; i < kW && t.p < t.end; ++i) {
+            if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
+              if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+              t.nl = 0;
+              ++t.ci;
+              t.cend = min(t.cend + chunk, t.end);
+            }
+            const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            k1_word_slow5<kH>(x, o, t, w);
+          }
+        }
+      }
+      k1_drain5<kH>(x, o, t, ob);
+      flush_kw(x.kwmask, kw_words, t.f, t.kw0, t.kw1);
+      if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);   // the range's last chunk
+    }
+    // flush this wave's hit buffer (the wave has reconverged here)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t n = min(*x.w_hitcnt, kH);
+    uint32_t b0 = 0, o0 = 0;
+    if (lane == 0 && n) {
+      b0 = atomicAdd(x.b_hitcnt, n);
+      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
+    }
+    b0 = __shfl(b0, 0);
+    o0 = __shfl(o0, 0);
+    const uint32_t spill_from = max(b0, region_cap);
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t h = x.w_hits[i];
+      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
+      if (b0 + i < region_cap) {
+        x.hits[b0 + i] = v;
+      } else {
+        const uint32_t oi = o0 + (b0 + i - spill_from);
+        if (oi < x.over_cap) x.over[oi] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
+}
+
+// K1 v6: v5's compact table at two 1024-thread workgroups per CU with the
+// per-lane state cut to fit 64 VGPRs without spilling: positions are 32-bit
+// offsets from the lane's first byte, one 64-byte register line (no double
+// buffer: with 8 waves per SIMD other waves cover a line's load), the
+// deferred-output slot count as the only per-lane output state, and the
+// uniform context in scalar registers.
+struct K1LeanCtx {
+  const uint8_t* __restrict__ data;
+  const uint64_t* __restrict__ offsets;
+  uint32_t nfiles, first_out, nkw, kw_words, region_cap, over_cap, ob_stride;
+  bool primary;
+  const OutMeta* __restrict__ meta;
+  const uint16_t* __restrict__ oidx;
+  const uint32_t* __restrict__ list;
+  uint32_t* __restrict__ kwbits;
+  uint32_t* __restrict__ kwmask;
+  unsigned long long* __restrict__ hits;
+  unsigned long long* __restrict__ over;
+  uint32_t* over_cnt;
+  uint32_t* b_hitcnt;
+  uint32_t* w_hits;
+  uint32_t* w_hitcnt;
+  uint32_t* __restrict__ fflags;
+  uint32_t* __restrict__ ob;      // this lane's first deferred-output slot
+  unsigned long long item_base;
+};
+
+struct K1Lean {
+  unsigned long long base;        // absolute position of offset 0 (the warm-up start)
+  uint32_t p, lim, end, emit, cend, ci;
+  uint32_t f, s, p12, nl, obn;
+  unsigned long long kw0, kw1;
+};
+
+template <uint32_t kH>
+__device__ __noinline__ void k1_lean_out(const K1LeanCtx& x, K1Lean& t, uint32_t st, unsigned long long q) {
+  const OutMeta m = x.meta[x.oidx[st - x.first_out]];
+  t.kw0 |= m.kw0;
+  t.kw1 |= m.kw1;
+  for (uint32_t j = 0; j < m.list_count; ++j) {
+    const uint32_t id = x.list[m.list_begin + j];
+    if (id < x.nkw) {
+      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
+      continue;
+    }
+    const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
+    if (li < kH) {
+      x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
+    } else {
+      const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
+      if (gi < x.region_cap) {
+        x.hits[gi] = (q << 24) | (id - x.nkw);
+      } else {
+        const uint32_t oi = atomicAdd(x.over_cnt, 1u);
+        if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
+      }
+    }
+  }
+}
+
+template <uint32_t kH>
+__device__ __forceinline__ void k1_lean_drain(const K1LeanCtx& x, K1Lean& t) {
+  for (uint32_t i = 0; i < t.obn; ++i) {
+    const uint32_t e = x.ob[i * x.ob_stride];
+    k1_lean_out<kH>(x, t, e & 0xffffu, t.base + t.emit + (e >> 16));
+  }
+  t.obn = 0;
+}
+
+__device__ __forceinline__ void k1_lean_flush(const K1LeanCtx& x, K1Lean& t) {
+  uint32_t* w = x.kwmask + static_cast<size_t>(t.f) * x.kw_words;
+  if (t.kw0) {
+    or_bits(w + 0, static_cast<uint32_t>(t.kw0));
+    or_bits(w + 1, static_cast<uint32_t>(t.kw0 >> 32));
+  }
+  if (t.kw1) {
+    or_bits(w + 2, static_cast<uint32_t>(t.kw1));
+    or_bits(w + 3, static_cast<uint32_t>(t.kw1 >> 32));
+  }
+  t.kw0 = t.kw1 = 0;
+}
+
+// a word with file-boundary and range-end checks (rare)
+template <uint32_t kH>
+__device__ __noinline__ void k1_lean_slow(const K1LeanCtx& x, K1Lean& t, v4u v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t fend = static_cast<uint32_t>(min(x.offsets[t.f + 1] - t.base, 0xffffffffull));
+  const bool special = x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit;
+  uint32_t a = t.p12 & 0xffu, bb = t.p12 >> 8;
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t q = t.p + k;
+    if (q >= t.end) break;
+    if (q >= fend) {
+      k1_lean_flush(x, t);
+      do { ++t.f; fend = static_cast<uint32_t>(min(x.offsets[t.f + 1] - t.base, 0xffffffffull)); } while (q >= fend);
+      t.s = 0;
+      t.p12 = 0;
+      a = bb = 0;
+    }
+    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    if (special && ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)))
+      atomicOr(&x.fflags[t.f], 1u);
+    bb = a;
+    a = b;
+    t.s = k1_step5(t.s, k1_lds8(b));
+    if (q >= t.emit) {
+      t.nl += (b == 0x0au);
+      if (t.s >= x.first_out) k1_lean_out<kH>(x, t, t.s, t.base + q);
+    }
+    t.p12 = ((t.p12 << 8) & 0xff00u) | b;
+  }
+  t.p += 16;
+  t.lim = min(t.end, fend);
+}
+
+template <uint32_t kH>
+__device__ __forceinline__ void k1_lean_word(const K1LeanCtx& x, K1Lean& t, v4u v) {
+  const bool emit = t.p >= t.emit;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t s = t.s;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t c2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c2[k] = k1_lds8((w[2 * h + (k >> 2)] >> ((k & 3) * 8)) & 0xffu);
+    const uint32_t s0 = s;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s = k1_step5(s, c2[k]);
+      mx = max(mx, s);
+    }
+    if (emit && mx >= x.first_out) {
+      uint32_t r = s0;
+      for (int k = 0; k < 8; ++k) {
+        r = k1_step5(r, c2[k]);
+        if (r >= x.first_out) {
+          if (t.obn < kOutSlots) {
+            x.ob[t.obn * x.ob_stride] = ((t.p + 8 * h + k - t.emit) << 16) | r;
+            ++t.obn;
+          } else {
+            k1_lean_out<kH>(x, t, r, t.base + t.p + 8 * h + k);
+          }
+        }
+      }
+    }
+  }
+  t.s = s;
+  if (emit) {
+    uint32_t u = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t xx = w[j] ^ 0x0a0a0a0au;
+      u += __popc(((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu);   // bit 7 set: not '\n'
+    }
+    t.nl += 128u - u;
+  }
+  t.p12 = (w[3] >> 24) | ((w[3] >> 8) & 0xff00u);
+  t.p += 16;
+}
+
+template <uint32_t kH>
+__global__ __attribute__((amdgpu_flat_work_group_size(1024, 1024), amdgpu_waves_per_eu(8, 8)))
+void tsg_k1_scan_v6(
+    const uint8_t* __restrict__ data, unsigned long long total,
+    const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls, uint32_t table_bytes, uint32_t first_out,
+    const OutMeta* __restrict__ g_meta, const uint16_t* __restrict__ g_oidx, const uint32_t* __restrict__ g_list,
+    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
+    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
+    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
+    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
+    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
+    uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr uint32_t kThreads = 1024, kWaves = kThreads / 64, kL = 64;
+  if (!k1_lds_base_ok(smem)) {
+    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
+    return;
+  }
+  const uint32_t padded = (table_bytes + 15) & ~15u;
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + kTabOff5 + padded);
+  uint32_t* s_hitcnt = s_hits + kWaves * kH;
+  uint32_t* s_block = s_hitcnt + kMaxWaves;
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_block[0] = 0;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(g_next);
+    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff5);
+    for (uint32_t i = threadIdx.x; i < padded / 16; i += kThreads) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += kThreads) smem[i] = g_cls[i];
+  }
+  K1LeanCtx x;
+  x.data = data; x.offsets = offsets; x.nfiles = nfiles; x.first_out = first_out; x.nkw = nkw;
+  x.kw_words = kw_words; x.region_cap = region_cap; x.over_cap = over_cap; x.ob_stride = gridDim.x * kThreads;
+  x.primary = primary != 0;
+  x.meta = g_meta; x.oidx = g_oidx; x.list = g_list;
+  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32;
+  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.over = over; x.over_cnt = over_cnt;
+  x.b_hitcnt = s_block; x.w_hits = s_hits + wid * kH; x.w_hitcnt = s_hitcnt + wid;
+  x.fflags = fflags; x.ob = obuf + blockIdx.x * kThreads + threadIdx.x;
+  __syncthreads();
+  const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
+  const unsigned long long n1 = min(nchunks, W * 64 * tail_rounds);
+  const unsigned long long n2 = min(nchunks - n1, W * 128 * tail_rounds);
+  const unsigned long long n4 = nchunks - n1 - n2;
+  const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
+  const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
+  const uint32_t warm = warm_lines * kL;
+  for (;;) {
+    unsigned long long item = 0;
+    if (lane == 0) {
+      item = atomicAdd(item_ctr, 1u);
+      *x.w_hitcnt = 0;
+    }
+    item = __shfl(item, 0);
+    if (item >= nitems) break;
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long c0, rend;
+    uint32_t kU;
+    if (item < i4) { kU = 4; c0 = item * 256; rend = n4; }
+    else if (item < i4 + i2) { kU = 2; c0 = n4 + (item - i4) * 128; rend = n4 + n2; }
+    else { kU = 1; c0 = n4 + n2 + (item - i4 - i2) * 64; rend = nchunks; }
+    x.item_base = c0 * static_cast<unsigned long long>(chunk);
+    const unsigned long long c = c0 + lane * kU;
+    if (c < rend) {
+      K1Lean t;
+      const unsigned long long start = min(c * chunk, total);
+      t.base = start > warm ? start - warm : 0;
+      t.p = 0;
+      t.emit = static_cast<uint32_t>(start - t.base);
+      t.end = static_cast<uint32_t>(min(min(c + kU, rend) * chunk, total) - t.base);
+      t.cend = min(t.emit + chunk, t.end);
+      t.ci = static_cast<uint32_t>(c);
+      t.s = 0; t.p12 = 0; t.nl = 0; t.obn = 0; t.kw0 = t.kw1 = 0;
+      t.f = file_of(offsets, nfiles, t.base);
+      t.lim = static_cast<uint32_t>(min(static_cast<unsigned long long>(t.end), offsets[t.f + 1] - t.base));
+      while (t.p < t.end) {
+        if (t.p >= t.cend && t.cend < t.end) {                // a chunk of the range is done
+          if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+          t.nl = 0;
+          ++t.ci;
+          t.cend = min(t.cend + chunk, t.end);
+        }
+        const uint8_t* lp = data + t.base + t.p;
+        if (t.p + kL <= t.lim) {
+          v4u line[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) line[i] = *reinterpret_cast<const v4u*>(lp + 16 * i);
+          if (x.primary) {
+            uint32_t hb = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) hb |= line[i].x | line[i].y | line[i].z | line[i].w;
+            if ((hb & 0x80808080u) && k1_line_special(lp, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) k1_lean_word<kH>(x, t, line[i]);
+        } else {
+          k1_lean_drain<kH>(x, t);                           // parked outputs belong to file t.f
+          for (int i = 0; i < 4 && t.p < t.end; ++i) {
+            if (t.p >= t.cend && t.cend < t.end) {
+              if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+              t.nl = 0;
+              ++t.ci;
+              t.cend = min(t.cend + chunk, t.end);
+            }
+            k1_lean_slow<kH>(x, t, *reinterpret_cast<const v4u*>(data + t.base + t.p));
+          }
+        }
+      }
+      k1_lean_drain<kH>(x, t);
+      k1_lean_flush(x, t);
+      if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t n = min(*x.w_hitcnt, kH);
+    uint32_t b0 = 0, o0 = 0;
+    if (lane == 0 && n) {
+      b0 = atomicAdd(x.b_hitcnt, n);
+      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
+    }
+    b0 = __shfl(b0, 0);
+    o0 = __shfl(o0, 0);
+    const uint32_t spill_from = max(b0, region_cap);
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t h = x.w_hits[i];
+      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
+      if (b0 + i < region_cap) {
+        x.hits[b0 + i] = v;
+      } else {
+        const uint32_t oi = o0 + (b0 + i - spill_from);
+        if (oi < x.over_cap) x.over[oi] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
+}
+
 // K1 v4: v3's per-byte work on TWO streams per lane.  v3's transition chain
 // is one dependent LDS round trip per byte per lane (measured: the no-HBM
 // build runs at 3.3 TB/s against 3.0 with HBM, so K1 is bound by that chain,
@@ -1282,6 +1896,23 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
   return true;
 }
 
+// v5 LDS bytes: class map + table + per-wave hit buffers + counters
+constexpr uint32_t kK1HitsDual = 64, kK1HitsSingle = 512;
+constexpr uint32_t k1_lds5(uint32_t table_bytes, uint32_t hits) {
+  return kTabOff5 + ((table_bytes + 15) & ~15u) + 16 * hits * 4 + kMaxWaves * 4 + 16;
+}
+
+// v5 instantiations: dual (two workgroups per CU, 8 waves per SIMD) with
+// 64- or 32-byte register lines, or single (one workgroup per CU)
+const void* k1_kernel5(bool dual, int line_words) {
+  if (dual) {
+    if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v5<8, 2, kK1HitsDual>);
+    return reinterpret_cast<const void*>(&tsg_k1_scan_v6<kK1HitsDual>);
+  }
+  if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v5<4, 2, kK1HitsSingle>);
+  return reinterpret_cast<const void*>(&tsg_k1_scan_v5<4, 4, kK1HitsSingle>);
+}
+
 // Default K1 chunk for a launch of `bytes`: about a million lane chunks per
 // launch, 1-4 KiB.  Measured on MI355X (r2g, v3 K1): a 1 GB launch 0.52 ms
 // at 1 KiB vs 0.56 at 4 KiB (shorter wave items, shorter tail); 2 GB best at
@@ -1290,7 +1921,7 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // the '\n'-count granularity and the last round's range: 2 KiB for launches
 // of 2 GiB and more (measured r2r: 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB.
 uint32_t k1_chunk_for(uint64_t bytes, int variant) {
-  if (variant == 3) return bytes >= (2ull << 30) ? 2048 : 1024;
+  if (variant == 3 || variant == 5) return bytes >= (2ull << 30) ? 2048 : 1024;
   uint32_t c = 1024;
   while (c < 4096 && static_cast<uint64_t>(c) * (1u << 20) < bytes) c <<= 1;
   return c;
@@ -1312,6 +1943,12 @@ struct K1Group {
   uint32_t kw_base = 0, warm_lines = 0, warm_lines64 = 0;
   size_t meta_bytes = 0;
   bool in_lds = false;
+  // v5 compact layout: merged classes, rows of row5 dwords, dword offsets
+  uint16_t* next5 = nullptr;
+  uint8_t* cls5 = nullptr;
+  uint16_t* oidx5 = nullptr;   // row - first_out5 -> output-state index
+  uint32_t table5_bytes = 0, first_out5 = 0, nclasses5 = 0, row5 = 0, max_pattern = 0;
+  bool dual5 = false;          // class map + table + kK1HitsDual hit buffers fit half a CU's LDS
 };
 
 // The compiled rule tables on one device plus that device's pool of lanes.
@@ -1389,7 +2026,7 @@ DeviceTables::~DeviceTables() {
   void* ps[] = {anchors, rules, rule_kw, vdfa, v_next, v_acc, v_cls};
   for (void* p : ps) if (p) hipFree(p);
   for (K1Group& g : k1g) {
-    void* gs[] = {g.next, g.cls, g.meta, g.list};
+    void* gs[] = {g.next, g.cls, g.meta, g.list, g.next5, g.cls5, g.oidx5};
     for (void* p : gs) if (p) hipFree(p);
   }
 }
@@ -1494,6 +2131,39 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     if (!dev_upload(sn, &g.next, err) || !dev_upload(cls, &g.cls, err) || !dev_upload(meta, &g.meta, err) ||
         !dev_upload(olist, &g.list, err)) {
       return false;
+    }
+    {
+      // v5: classes whose transition columns are identical merged (exact),
+      // rows of an odd dword count, entries = the next row's DWORD offset
+      std::map<std::vector<uint16_t>, uint32_t> colid;
+      std::vector<uint32_t> newc(C);
+      for (uint32_t c = 0; c < C; ++c) {
+        std::vector<uint16_t> col(sd.t.nstates);
+        for (uint32_t st = 0; st < sd.t.nstates; ++st) col[st] = sd.t.next[static_cast<size_t>(st) * C + c];
+        newc[c] = colid.emplace(std::move(col), static_cast<uint32_t>(colid.size())).first->second;
+      }
+      const uint32_t C5 = static_cast<uint32_t>(colid.size());
+      uint32_t cr = (C5 + 1) & ~1u;
+      if (((cr / 2) & 1u) == 0) cr += 2;
+      const uint32_t rw = cr / 2;
+      if (static_cast<uint64_t>(sd.t.nstates) * rw > 65535) { *err = "scan DFA group too large for K1 v5"; return false; }
+      std::vector<uint16_t> t5(static_cast<size_t>(sd.t.nstates) * cr, 0);
+      for (uint32_t st = 0; st < sd.t.nstates; ++st)
+        for (uint32_t c = 0; c < C; ++c)
+          t5[static_cast<size_t>(st) * cr + newc[c]] = static_cast<uint16_t>(sd.t.next[static_cast<size_t>(st) * C + c] * rw);
+      std::vector<uint16_t> oidx(std::max<size_t>(1, static_cast<size_t>(sd.t.nstates - fo) * rw), 0);
+      for (uint32_t o = 0; o < sd.t.nstates - fo; ++o) oidx[static_cast<size_t>(o) * rw] = static_cast<uint16_t>(o);
+      std::vector<uint8_t> c5(256);
+      for (int b = 0; b < 256; ++b) c5[b] = static_cast<uint8_t>(newc[sd.t.byte_class[b]] * 2);
+      g.nclasses5 = C5;
+      g.row5 = rw;
+      g.first_out5 = fo * rw;
+      g.table5_bytes = static_cast<uint32_t>(t5.size() * 2);
+      g.max_pattern = sd.max_pattern_bytes;
+      g.dual5 = k1_lds5(g.table5_bytes, kK1HitsDual) * 2 <= kLdsBytes;
+      t5.resize(((t5.size() * 2 + 15) / 16) * 8, 0);
+      if (!dev_upload(t5, &g.next5, err) || !dev_upload(c5, &g.cls5, err) || !dev_upload(oidx, &g.oidx5, err))
+        return false;
     }
     dt->kw_words = std::max<uint32_t>(dt->kw_words, g.kw_base / 32 + 4);   // a group's masks span 4 words from kw_base
     dt->k1g.push_back(g);
@@ -1622,9 +2292,14 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const long long v = std::atoll(c);
     if (v >= 0) e->segment_tail_ = static_cast<uint64_t>(v);
   }
+  if (const char* c = std::getenv("TSG_K1_LINE5")) {
+    const int v = std::atoi(c);
+    if (v == 2 || v == 4) e->k1_line5_ = v;
+  }
+  if (const char* c = std::getenv("TSG_K1_SINGLE5")) e->k1_single5_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_K1_VARIANT")) {
     const int v = std::atoi(c);
-    if (v == 1 || v == 3 || v == 4) e->k1_variant_ = v;
+    if (v == 1 || v == 3 || v == 4 || v == 5) e->k1_variant_ = v;
   }
   if (const char* cfg = std::getenv("TSG_K1_CFG")) {
     unsigned t = 0, k = 0;
@@ -1789,9 +2464,13 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     const uint64_t want_blocks = (nchunks + static_cast<uint64_t>(nthr) * ks - 1) / (static_cast<uint64_t>(nthr) * ks);
     // one resident workgroup per CU (the LDS table takes most of the CU's
     // 160 KiB): a grid of exactly one workgroup per CU, grid-stride
-    bool all_lds = true;
-    for (const K1Group& g : dt.k1g) all_lds &= g.in_lds;
-    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, all_lds ? sms : sms * 2ull)));
+    bool all_lds = true, all_dual = true;
+    for (const K1Group& g : dt.k1g) { all_lds &= g.in_lds; all_dual &= g.dual5; }
+    // v5 with compact tables: two workgroups per CU
+    const bool v5 = k1_variant_ == 5 && nthr == 1024 && ks == 1;
+    const bool dual = v5 && all_dual && !k1_single5_;
+    const uint32_t per_cu = (!all_lds || dual) ? 2 : 1;
+    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * static_cast<uint64_t>(per_cu))));
     st->k1_blocks = blocks;
     st->k1_threads = nthr;
     st->table_in_lds = all_lds;
@@ -1802,6 +2481,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     // v3 runs the groups whose table is in LDS (1024 threads, one stream per
     // lane); the others keep v1
     auto k1_var = [&](const K1Group& g) {
+      if (v5) return 5;
       if (k1_variant_ == 4 && g.in_lds && ks == 1 && (nthr == 1024 || nthr == 512)) return 4;
       return k1_variant_ == 3 && g.in_lds && nthr == 1024 && ks == 1 ? 3 : 1;
     };
@@ -1809,18 +2489,25 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
              (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
     };
+    auto lds_of = [&](const K1Group& g) -> size_t {
+      return v5 ? k1_lds5(g.table5_bytes, dual ? kK1HitsDual : kK1HitsSingle) : k1_lds(g);
+    };
+    auto kernel_of = [&](const K1Group& g) -> const void* {
+      return v5 ? k1_kernel5(dual, k1_line5_) : k1_kernel(g.in_lds, nthr, ks, k1_var(g), k1_abl_);
+    };
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
       const K1Group& g = dt.k1g[gi];
-      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_var(g), k1_abl_);
+      const void* kfn = kernel_of(g);
       if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG / TSG_K1_ABL)"; return false; }
-      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(k1_lds(g))));
+      if (lds_of(g) > kLdsBytes) { *err = "K1 LDS budget exceeded"; return false; }
+      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_of(g))));
     }
     HIP_OK(hipEventRecord(ln.ev[0], s));
     uint32_t launches = 0;
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = dt.k1g[gi];
-      const size_t lds = k1_lds(g);
-      const void* kfn = k1_kernel(g.in_lds, nthr, ks, k1_var(g), k1_abl_);
+      const size_t lds = lds_of(g);
+      const void* kfn = kernel_of(g);
       uint32_t* a_items = ln.d_cnt + 4 + gi;         // v3's work-item counter (zeroed with d_cnt)
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
@@ -1841,6 +2528,21 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
       uint32_t a_rcap = region_cap;
       uint32_t a_tail = k1_tail_rounds_;
+      if (v5) {
+        uint16_t* a_next5 = g.next5;
+        uint8_t* a_cls5 = g.cls5;
+        uint16_t* a_oidx5 = g.oidx5;
+        uint32_t a_tb5 = g.table5_bytes, a_first5 = g.first_out5;
+        const uint32_t lb = 16u * static_cast<uint32_t>(k1_line5_);
+        uint32_t a_warm5 = g.max_pattern > 1 ? (g.max_pattern - 1 + lb - 1) / lb : 0;
+        void* args5[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next5, &a_cls5, &a_tb5, &a_first5,
+                         &a_meta, &a_oidx5, &a_list, &a_nkw, &a_warm5, &a_chunk, &a_nchunks,
+                         &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
+                         &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
+        HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args5, lds, s));
+        ++launches;
+        continue;
+      }
       void* args[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,

@@ -6,6 +6,8 @@
 // prepared at memory speed instead of one Go goroutine per file.
 #include "feed.h"
 
+#include "goregexp.h"
+
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -81,11 +83,26 @@ void parallel_for(uint32_t n, int threads, F&& fn) {
   for (auto& th : ts) th.join();
 }
 
+std::string trim_left_slash(const std::string& p) {
+  size_t i = 0;
+  while (i < p.size() && p[i] == '/') ++i;
+  return p.substr(i);
+}
+
+bool wants(const Ruleset& rs, const FeedOpts& opts, const std::string& path, uint64_t size,
+           const std::string& cfg_base) {
+  // filepath extracted from a tar file has no "/" prefix (analyzer.go:407-408)
+  const std::string clean = trim_left_slash(path);
+  for (const auto& rx : opts.patterns)                              // filePatternMatch (analyzer.go:522-530)
+    if (rx->match_string(reinterpret_cast<const uint8_t*>(clean.data()), clean.size())) return true;
+  return required(rs, clean, size, cfg_base);
+}
+
 // The two passes over nfiles files; file(i) gives (content, size, path).
 template <typename File>
-bool prepare_core(const Ruleset& rs, const std::string& config_path, uint32_t nfiles, File&& file, int threads,
+bool prepare_core(const Ruleset& rs, const FeedOpts& opts, uint32_t nfiles, File&& file, int threads,
                   PreparedBatch* out, FeedAlloc alloc) {
-  const std::string cfg_base = go_base(config_path);
+  const std::string cfg_base = go_base(opts.config_path);
   // pass 1: keep decision, binary flag and prepared size per file
   std::vector<uint8_t> keep(nfiles), bin(nfiles);
   std::vector<uint64_t> size(nfiles);
@@ -95,7 +112,7 @@ bool prepare_core(const Ruleset& rs, const std::string& config_path, uint32_t nf
     std::string path;
     file(i, &c, &n, &path);
     keep[i] = 0;
-    if (!required(rs, path, n, cfg_base)) return;
+    if (!opts.assume_required && !wants(rs, opts, path, n, cfg_base)) return;
     const bool binary = go_is_binary(c, n);                        // secret.go:104-108
     if (binary && go_ext(path) != ".pyc") return;                  // allowedBinary
     bin[i] = binary;
@@ -144,24 +161,60 @@ bool prepare_core(const Ruleset& rs, const std::string& config_path, uint32_t nf
 
 }  // namespace
 
+bool parse_file_patterns(const std::vector<std::string>& entries, FeedOpts* out, std::string* err) {
+  for (const std::string& p : entries) {
+    const size_t colon = p.find(':');                              // strings.SplitN(p, ":", 2)
+    if (colon == std::string::npos) {
+      *err = "invalid file pattern (" + p + ") expected format: \"fileType:regexPattern\" e.g. "
+             "\"dockerfile:my_dockerfile_*\"";
+      return false;
+    }
+    std::string rerr;
+    std::unique_ptr<re::Regexp> rx = re::Regexp::compile(p.substr(colon + 1), &rerr);   // regexp.Compile
+    if (!rx) { *err = "invalid file regexp (" + p + "): " + rerr; return false; }
+    if (p.compare(0, colon, "secret") == 0 && colon == 6) out->patterns.emplace_back(std::move(rx));
+  }
+  return true;
+}
+
+bool secret_analyzer_wants(const Ruleset& rs, const FeedOpts& opts, const std::string& path, uint64_t size) {
+  return wants(rs, opts, path, size, go_base(opts.config_path));
+}
+
 bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,
+                   uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
+                   PreparedBatch* out, std::string* err, FeedAlloc alloc) {
+  FeedOpts o;
+  o.config_path = config_path;
+  return prepare_batch(rs, o, raw, raw_off, nfiles, paths, path_lens, threads, out, err, alloc);
+}
+
+bool prepare_files(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* starts,
+                   const uint64_t* sizes, const std::vector<std::string>& paths, int threads, PreparedBatch* out,
+                   std::string* err, FeedAlloc alloc) {
+  FeedOpts o;
+  o.config_path = config_path;
+  return prepare_files(rs, o, raw, starts, sizes, paths, threads, out, err, alloc);
+}
+
+bool prepare_batch(const Ruleset& rs, const FeedOpts& opts, const uint8_t* raw, const uint64_t* raw_off,
                    uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
                    PreparedBatch* out, std::string* err, FeedAlloc alloc) {
   for (uint32_t i = 0; i < nfiles; ++i) {
     if (raw_off[i + 1] < raw_off[i]) { *err = "offsets must be non-decreasing"; return false; }
   }
-  return prepare_core(rs, config_path, nfiles, [&](uint32_t i, const uint8_t** c, uint64_t* n, std::string* path) {
+  return prepare_core(rs, opts, nfiles, [&](uint32_t i, const uint8_t** c, uint64_t* n, std::string* path) {
     *c = raw + raw_off[i];
     *n = raw_off[i + 1] - raw_off[i];
     *path = path_lens ? std::string(paths[i], path_lens[i]) : std::string(paths[i]);
   }, threads, out, alloc);
 }
 
-bool prepare_files(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* starts,
+bool prepare_files(const Ruleset& rs, const FeedOpts& opts, const uint8_t* raw, const uint64_t* starts,
                    const uint64_t* sizes, const std::vector<std::string>& paths, int threads, PreparedBatch* out,
                    std::string* err, FeedAlloc alloc) {
   (void)err;
-  return prepare_core(rs, config_path, static_cast<uint32_t>(paths.size()),
+  return prepare_core(rs, opts, static_cast<uint32_t>(paths.size()),
                       [&](uint32_t i, const uint8_t** c, uint64_t* n, std::string* path) {
                         *c = raw + starts[i];
                         *n = sizes[i];

@@ -17,11 +17,35 @@ struct PreparedBatch {
   std::vector<uint8_t> binary;     // ScanArgs.Binary (a .pyc scanned as printable runs)
 };
 
+namespace re { class Regexp; }
+
+// AnalyzerGroup options the secret analyzer's feed depends on.
+struct FeedOpts {
+  std::string config_path;                         // SecretAnalyzer.configPath (Required skips its base name)
+  std::vector<std::shared_ptr<re::Regexp>> patterns;   // --file-patterns "secret:<re>" (analyzer.go:332-350)
+  bool assume_required = false;                    // Required/patterns already decided by the caller
+};
+
+// --file-patterns entries ("fileType:regexPattern"; only "secret" ones kept),
+// with analyzer.go:332-350's errors for a malformed entry or regexp.
+bool parse_file_patterns(const std::vector<std::string>& entries, FeedOpts* out, std::string* err);
+
+// AnalyzeFile's gate for the secret analyzer (analyzer.go:403-419):
+// filePatternMatch(TrimLeft(path, "/")) || Required(TrimLeft(path, "/"), size)
+bool secret_analyzer_wants(const Ruleset& rs, const FeedOpts& opts, const std::string& path, uint64_t size);
+
 // Output buffer for the packed contents: returns memory of `bytes` bytes and
 // sets the deleter, or nullptr (the batch then uses the heap).
 using FeedAlloc = uint8_t* (*)(size_t bytes, void (**free_fn)(uint8_t*));
 
-// keep(i) = Required(path_i, size_i) && (!IsBinary || ext == ".pyc")
+// keep(i) = (filePatternMatch || Required)(path_i, size_i) && (!IsBinary || ext == ".pyc")
+bool prepare_batch(const Ruleset& rs, const FeedOpts& opts, const uint8_t* raw, const uint64_t* raw_off,
+                   uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
+                   PreparedBatch* out, std::string* err, FeedAlloc alloc = nullptr);
+bool prepare_files(const Ruleset& rs, const FeedOpts& opts, const uint8_t* raw, const uint64_t* starts,
+                   const uint64_t* sizes, const std::vector<std::string>& paths, int threads, PreparedBatch* out,
+                   std::string* err, FeedAlloc alloc = nullptr);
+
 bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,
                    uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
                    PreparedBatch* out, std::string* err, FeedAlloc alloc = nullptr);

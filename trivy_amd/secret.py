@@ -220,17 +220,26 @@ def pack(args_list):
     return data, offsets
 
 
-def PrepareBatch(scanner, files, config_path="", image=False, threads=0):
+def PrepareBatch(scanner, files, config_path="", image=False, threads=0, file_patterns=()):
     """Batched SecretAnalyzer.Required + Analyze content prep (tsg_prepare_batch;
     pkg/fanal/analyzer/secret/secret.go:103-190).  files: [(input.FilePath, raw
     bytes)].  Returns (ScanArgs list, source index list) for the kept files;
-    image=True adds the "/" prefix image files get (secret.go:133-135)."""
+    image=True adds the "/" prefix image files get (secret.go:133-135).
+    file_patterns: --file-patterns entries (tsg_prepare_batch_opts): a
+    "secret:<re>" match bypasses Required (analyzer.go:417-419)."""
     L = _lib.lib()
     raw, offsets = pack([ScanArgs(p, c) for p, c in files])
     paths, lens, _keep = _lib.pack_paths([p for p, _ in files])
     h = ctypes.c_void_p()
-    _lib.check(L.tsg_prepare_batch(scanner._rs, (config_path or "").encode(), raw.ctypes.data, offsets.ctypes.data,
-                                   len(files), paths, lens, threads, ctypes.byref(h)))
+    if file_patterns:
+        o, keep = _lib.feed_opts(config_path, file_patterns, threads=threads)
+        rc = L.tsg_prepare_batch_opts(scanner._rs, raw.ctypes.data, offsets.ctypes.data, len(files), paths, lens,
+                                      ctypes.byref(o), ctypes.byref(h))
+        if rc != 0:
+            raise ConfigError(L.tsg_last_error().decode("utf-8", "replace"))
+    else:
+        _lib.check(L.tsg_prepare_batch(scanner._rs, (config_path or "").encode(), raw.ctypes.data,
+                                       offsets.ctypes.data, len(files), paths, lens, threads, ctypes.byref(h)))
     try:
         d, o, ix, b = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
         nk = ctypes.c_uint32()
@@ -303,6 +312,58 @@ def PrepareLayerTar(scanner, tar, skip_files=(), skip_dirs=(), config_path="", t
         finally:
             L.tsg_result_free(res)
         return out, walk, secrets
+    finally:
+        L.tsg_prepared_free(h)
+
+
+def _prepared_args(L, h, with_paths, paths_in=None):
+    """(ScanArgs list, walk dict or None) of a tsg_prepared handle."""
+    d, o, ix, b = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    nk = ctypes.c_uint32()
+    _lib.check(L.tsg_prepared_view(h, ctypes.byref(d), ctypes.byref(o), ctypes.byref(ix), ctypes.byref(b),
+                                   ctypes.byref(nk)))
+    n = nk.value
+    offs = np.ctypeslib.as_array(ctypes.cast(o, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy() \
+        if n else np.zeros(1, np.uint64)
+    binf = np.ctypeslib.as_array(ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)), shape=(n,)).tolist() if n else []
+    index = np.ctypeslib.as_array(ctypes.cast(ix, ctypes.POINTER(ctypes.c_uint32)), shape=(n,)).tolist() if n else []
+    data = ctypes.string_at(d, int(offs[-1])) if n else b""
+    if with_paths:
+        pp, pl = ctypes.POINTER(ctypes.c_char_p)(), ctypes.POINTER(ctypes.c_uint32)()
+        _lib.check(L.tsg_prepared_paths(h, ctypes.byref(pp), ctypes.byref(pl)))
+        names = [ctypes.string_at(pp[k], pl[k]).decode("utf-8", "surrogateescape") for k in range(n)]
+    else:
+        names = [paths_in[i] for i in index]
+    return [ScanArgs(names[k], data[int(offs[k]):int(offs[k + 1])], bool(binf[k])) for k in range(n)], (d, o, b, n)
+
+
+def PrepareFsTree(scanner, root, skip_files=(), skip_dirs=(), file_patterns=(), config_path="", threads=0,
+                  pinned=False, scan=False):
+    """`trivy fs ROOT` feed: walker.FS.Walk + AnalyzeFile's gate + reads + content
+    prep (tsg_prepare_fs_tree).  Returns (ScanArgs list, walk dict); scan=True
+    also scans the prepared batch through tsg_scan_batch and returns
+    (ScanArgs list, walk dict, [types.Secret])."""
+    L = _lib.lib()
+    o, keep = _lib.feed_opts(config_path, file_patterns, skip_files, skip_dirs, threads, pinned)
+    h = ctypes.c_void_p()
+    rc = L.tsg_prepare_fs_tree(scanner._rs, os.fsencode(root), ctypes.byref(o), ctypes.byref(h))
+    if rc != 0:
+        raise WalkError(L.tsg_last_error().decode("utf-8", "replace"))
+    try:
+        walk = json.loads(L.tsg_prepared_walk_json(h).decode("utf-8", "surrogateescape"))
+        args, (d, off, b, n) = _prepared_args(L, h, True)
+        if not scan:
+            return args, walk
+        pp, pl = ctypes.POINTER(ctypes.c_char_p)(), ctypes.POINTER(ctypes.c_uint32)()
+        _lib.check(L.tsg_prepared_paths(h, ctypes.byref(pp), ctypes.byref(pl)))
+        res = ctypes.c_void_p()
+        _lib.check(L.tsg_scan_batch(scanner.engine(), d, off, n, pp, ctypes.cast(pl, ctypes.c_void_p), b,
+                                    ctypes.byref(res)))
+        try:
+            secrets = _lib.result_json(res)
+        finally:
+            L.tsg_result_free(res)
+        return args, walk, secrets
     finally:
         L.tsg_prepared_free(h)
 
