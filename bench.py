@@ -122,13 +122,23 @@ class PinnedAlloc:
 class PinnedBatch:
     """A packed batch in pinned host memory (tsg_alloc_pinned) + offsets, paths, binary flags."""
 
-    def __init__(self, L, data_u8, offsets, paths, binary=None, pinned=None):
+    def __init__(self, L, data_u8, offsets, paths, binary=None, pinned=None, prepared=None):
         """Copies data_u8 into new pinned memory, or adopts `pinned` (a
-        PinnedAlloc the data was generated into) without a copy."""
+        PinnedAlloc the data was generated into) or `prepared` (a tsg_prepared
+        handle whose data is pinned) without a copy."""
         from trivy_amd import _lib
         self.L = L
         self.nbytes = int(offsets[-1])
-        if pinned is not None:
+        self.prepared = prepared
+        if prepared is not None:
+            d_ = ctypes.c_void_p()
+            o_, i_, b_, nk = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint32()
+            _lib.check(L.tsg_prepared_view(prepared, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_),
+                                           ctypes.byref(b_), ctypes.byref(nk)))
+            self.ptr = d_
+            self.view = np.ctypeslib.as_array(ctypes.cast(d_, ctypes.POINTER(ctypes.c_uint8)),
+                                              shape=(self.nbytes + 64,))
+        elif pinned is not None:
             self.ptr, self.view = pinned.ptr, pinned.view
             pinned.ptr = None
         else:
@@ -148,7 +158,11 @@ class PinnedBatch:
         return bytes(self.view[int(self.offsets[i]):int(self.offsets[i + 1])])
 
     def free(self):
-        if self.ptr:
+        if self.prepared is not None:
+            self.L.tsg_prepared_free(self.prepared)
+            self.prepared = None
+            self.ptr = ctypes.c_void_p()
+        elif self.ptr:
             self.L.tsg_free_pinned(self.ptr)
             self.ptr = ctypes.c_void_p()
 
@@ -187,6 +201,114 @@ def layer_tar_rate(L, sc, batch, target_bytes, threads):
         L.tsg_prepared_free(h)
         best = dt if best is None else min(best, dt)
     return len(tar) / best / 1e9, nfiles, kept, best
+
+
+def _fs_type(path):
+    """Filesystem type of `path` from /proc/mounts (longest mount prefix)."""
+    best, typ = "", "?"
+    try:
+        for line in open("/proc/mounts"):
+            parts = line.split()
+            mnt = parts[1]
+            if (path == mnt or path.startswith(mnt.rstrip("/") + "/")) and len(mnt) > len(best):
+                best, typ = mnt, parts[2]
+    except OSError:
+        pass
+    return typ
+
+
+def tree_feed(L, sc, batch, threads, base_dir):
+    """`trivy fs` host feed over a real directory tree: the batch's files
+    written under base_dir, then tsg_prepare_fs_tree (walker.FS.Walk +
+    AnalyzeFile's gate + threaded reads + content prep into pinned memory)
+    with the page cache warm and cold (every file's pages dropped with
+    posix_fadvise(DONTNEED) after a sync), and the cold-read batch scanned by
+    tsg_scan_batch: disk -> findings.  Checks the tree's prepared files equal
+    tsg_prepare_batch over the same files in memory."""
+    import shutil
+    import tempfile
+    from trivy_amd import _lib
+    root = tempfile.mkdtemp(prefix="tsg_tree_", dir=base_dir)
+    try:
+        t0 = time.perf_counter()
+        for i in range(batch.nfiles):
+            fp = os.path.join(root, batch.paths[i])
+            os.makedirs(os.path.dirname(fp), exist_ok=True)
+            with open(fp, "wb") as f:
+                f.write(memoryview(batch.view[int(batch.offsets[i]):int(batch.offsets[i + 1])]))
+        os.sync()
+        t_write = time.perf_counter() - t0
+
+        def drop_cache():
+            for i in range(batch.nfiles):
+                fd = os.open(os.path.join(root, batch.paths[i]), os.O_RDONLY)
+                try:
+                    os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                finally:
+                    os.close(fd)
+
+        def run(scan):
+            o, _k = _lib.feed_opts(threads=threads, pinned=True)
+            h = ctypes.c_void_p()
+            t1 = time.perf_counter()
+            _lib.check(L.tsg_prepare_fs_tree(sc._rs, os.fsencode(root), ctypes.byref(o), ctypes.byref(h)))
+            dt = time.perf_counter() - t1
+            walk = json.loads(L.tsg_prepared_walk_json(h).decode("utf-8", "surrogateescape"))
+            d_, o_, i_, b_, nk = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(),
+                                  ctypes.c_uint32())
+            _lib.check(L.tsg_prepared_view(h, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_), ctypes.byref(b_),
+                                           ctypes.byref(nk)))
+            row = {"s": round(dt, 4), "walk_ms": round(walk["walk_ms"], 2), "read_ms": round(walk["read_ms"], 2),
+                   "prep_ms": round(walk["prep_ms"], 2), "read_bytes": walk["read_bytes"],
+                   "gbps": round(walk["read_bytes"] / dt / 1e9, 3), "kept_files": nk.value}
+            extra = None
+            if scan:
+                pp, pl = ctypes.POINTER(ctypes.c_char_p)(), ctypes.POINTER(ctypes.c_uint32)()
+                _lib.check(L.tsg_prepared_paths(h, ctypes.byref(pp), ctypes.byref(pl)))
+                res = ctypes.c_void_p()
+                t2 = time.perf_counter()
+                _lib.check(L.tsg_scan_batch(sc.engine(), d_, o_, nk.value, pp, ctypes.cast(pl, ctypes.c_void_p), b_,
+                                            ctypes.byref(res)))
+                ts = time.perf_counter() - t2
+                row["scan_s"] = round(ts, 4)
+                row["end_to_end_gbps"] = round(walk["read_bytes"] / (dt + ts) / 1e9, 3)
+                got = _lib.result_json(res)
+                L.tsg_result_free(res)
+                n = nk.value
+                offs = np.ctypeslib.as_array(ctypes.cast(o_, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,))
+                data = np.ctypeslib.as_array(ctypes.cast(d_, ctypes.POINTER(ctypes.c_uint8)), shape=(int(offs[-1]),))
+                names = [ctypes.string_at(pp[k], pl[k]).decode("utf-8", "surrogateescape") for k in range(n)]
+                extra = ({names[k]: bytes(data[int(offs[k]):int(offs[k + 1])]) for k in range(n)},
+                         {names[k]: got[k] for k in range(n)})
+            L.tsg_prepared_free(h)
+            return row, extra
+        warm, _ = run(False)
+        drop_cache()
+        cold, (tree_files, tree_res) = run(True)
+        # parity: the tree's prepared files == tsg_prepare_batch over the same files in memory
+        o, _k = _lib.feed_opts(threads=threads)
+        h = ctypes.c_void_p()
+        _lib.check(L.tsg_prepare_batch_opts(sc._rs, batch.ptr, batch.offsets.ctypes.data, batch.nfiles, batch.cpaths,
+                                            batch.clens, ctypes.byref(o), ctypes.byref(h)))
+        d_, o_, i_, b_, nk = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(),
+                              ctypes.c_uint32())
+        _lib.check(L.tsg_prepared_view(h, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_), ctypes.byref(b_),
+                                       ctypes.byref(nk)))
+        n = nk.value
+        offs = np.ctypeslib.as_array(ctypes.cast(o_, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,))
+        idx = np.ctypeslib.as_array(ctypes.cast(i_, ctypes.POINTER(ctypes.c_uint32)), shape=(n,))
+        data = np.ctypeslib.as_array(ctypes.cast(d_, ctypes.POINTER(ctypes.c_uint8)), shape=(int(offs[-1]) + 1,))
+        mem = {batch.paths[int(idx[k])]: bytes(data[int(offs[k]):int(offs[k + 1])]) for k in range(n)}
+        L.tsg_prepared_free(h)
+        same = mem == tree_files
+        return {"files": batch.nfiles, "bytes": batch.nbytes, "dir_fs": _fs_type(os.path.realpath(root)),
+                "write_s": round(t_write, 2), "warm": warm, "cold": cold, "prepared_equal_in_memory": same,
+                "findings": sum(len(r["Findings"]) for r in tree_res.values()),
+                "note": "tsg_prepare_fs_tree: walk + gate + %d reader threads + prep into pinned memory; cold = page "
+                        "cache dropped per file (posix_fadvise DONTNEED after sync; no effect on tmpfs); the cold "
+                        "batch then scanned by tsg_scan_batch (end_to_end = disk -> findings)" % threads}
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
 
 
 def numa_bind(device):
@@ -308,6 +430,10 @@ def main():
     ap.add_argument("--cpu-sample-mb", type=float, default=1200.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident comparison leg")
+    ap.add_argument("--tree", type=int, default=-1,
+                    help="1: also measure the `trivy fs` feed over the batch written as a directory tree "
+                         "(default: config 1 only)")
+    ap.add_argument("--tree-dir", default=os.environ.get("TSG_TREE_DIR", "/tmp"))
     ap.add_argument("--json-out", default="")
     ap.add_argument("--dry-launch", action="store_true",
                     help="ranks only report their wiring (rank, device, device_mask) and exit: the launcher's "
@@ -390,9 +516,11 @@ def main():
     hpb = ctypes.c_void_p()
     if args.config == 3 or rank == 0:
         paths, lens, _keep = _lib.pack_paths(corpus.paths)
+        # config 3 prepares straight into pinned memory: its output is the batch
+        fo, _fkeep = _lib.feed_opts(threads=args.threads, pinned=args.config == 3)
         t0 = time.perf_counter()
-        _lib.check(L.tsg_prepare_batch(sc._rs, None, corpus.data.ctypes.data, corpus.offsets.ctypes.data,
-                                       raw_files, paths, lens, args.threads, ctypes.byref(hpb)))
+        _lib.check(L.tsg_prepare_batch_opts(sc._rs, corpus.data.ctypes.data, corpus.offsets.ctypes.data, raw_files,
+                                            paths, lens, ctypes.byref(fo), ctypes.byref(hpb)))
         tprep = time.perf_counter() - t0
         d_, o_, i_, b_ = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
         _lib.check(L.tsg_prepared_view(hpb, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_),
@@ -406,14 +534,13 @@ def main():
         offs = np.ctypeslib.as_array(ctypes.cast(o_, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy()
         index = np.ctypeslib.as_array(ctypes.cast(i_, ctypes.POINTER(ctypes.c_uint32)), shape=(n,)).copy()
         binf = np.ctypeslib.as_array(ctypes.cast(b_, ctypes.POINTER(ctypes.c_uint8)), shape=(n,)).copy()
-        data = np.ctypeslib.as_array(ctypes.cast(d_, ctypes.POINTER(ctypes.c_uint8)), shape=(int(offs[-1]) + 64,))
         # image scans prefix "/" to layer paths (analyzer secret.go:133-135)
         scan_paths = ["/" + corpus.paths[i] for i in index]
-        batch = PinnedBatch(L, data, offs, scan_paths, binf)
+        batch = PinnedBatch(L, None, offs, scan_paths, binf, prepared=hpb)   # owns hpb now
     else:
         batch = PinnedBatch(L, None, corpus.offsets, corpus.paths, pinned=palloc)
-    if hpb:
-        L.tsg_prepared_free(hpb)
+        if hpb:
+            L.tsg_prepared_free(hpb)
     del corpus
     nfiles, nbytes = batch.nfiles, batch.nbytes
     bin_ptr = batch.binary.ctypes.data if batch.binary is not None else None
@@ -603,6 +730,17 @@ def main():
         out["host_feed"]["layer_tar_sample"] = "%d files / %.0f MB of this batch written as one PAX layer tar, %d " \
                                                "kept, best of 3: %.1f ms" % (tfiles, tgb * tdt * 1e3, tkept, tdt * 1e3)
         log("layer-tar feed (walk + Required + prep into pinned memory, %d threads): %.1f GB/s" % (args.threads, tgb))
+
+    if rank == 0 and (args.tree == 1 or (args.tree == -1 and args.config == 1)):
+        tr = tree_feed(L, sc, batch, args.threads, args.tree_dir)
+        out["host_feed"]["tree"] = tr
+        out["host_feed"]["tree_read_gbps"] = {"warm": tr["warm"]["gbps"], "cold": tr["cold"]["gbps"]}
+        log("fs-tree feed (%d files on %s): warm %.2f GB/s, cold %.2f GB/s, disk -> findings %.2f GB/s; "
+            "prepared == in-memory: %s" % (tr["files"], tr["dir_fs"], tr["warm"]["gbps"], tr["cold"]["gbps"],
+                                           tr["cold"]["end_to_end_gbps"], tr["prepared_equal_in_memory"]))
+        if not tr["prepared_equal_in_memory"]:
+            print("[bench] fs-tree feed differs from the in-memory preparation", file=sys.stderr, flush=True)
+            sys.exit(1)
 
     if not args.no_resident:
         # the same batch already resident in HBM (reported, never `value`)
