@@ -259,7 +259,8 @@ def tree_feed(L, sc, batch, threads, base_dir):
             _lib.check(L.tsg_prepared_view(h, ctypes.byref(d_), ctypes.byref(o_), ctypes.byref(i_), ctypes.byref(b_),
                                            ctypes.byref(nk)))
             row = {"s": round(dt, 4), "walk_ms": round(walk["walk_ms"], 2), "read_ms": round(walk["read_ms"], 2),
-                   "prep_ms": round(walk["prep_ms"], 2), "read_bytes": walk["read_bytes"],
+                   "prep_ms": round(walk["prep_ms"], 2), "pinned_alloc_ms": round(walk["alloc_ms"], 2),
+                   "read_bytes": walk["read_bytes"],
                    "gbps": round(walk["read_bytes"] / dt / 1e9, 3), "kept_files": nk.value}
             extra = None
             if scan:

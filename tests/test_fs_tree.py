@@ -162,3 +162,31 @@ def test_fs_tree_scan_gpu(tmp_path):
     ref = so.Scanner(None)
     assert secrets == [ref.scan(p, cc, b) for p, cc, b in want_args]
     assert sum(len(s["Findings"]) for s in secrets) > 20
+
+
+def test_parallel_walk_keeps_walkdir_order(tmp_path):
+    # directories read by several threads; the files come back in
+    # filepath.WalkDir's order (names that sort around '/': "a", "a-b", "a.b",
+    # "a0", upper case, UTF-8), equal to the oracle's sequential walk
+    import random
+    rng = random.Random(3)
+    names = ["a", "a-b", "a.b", "a0", "A", "b", "é", "z", "a_b", "ab"]
+    root = tmp_path / "t"
+    for _ in range(300):
+        depth = rng.randint(1, 4)
+        parts = [rng.choice(names) for _ in range(depth)]
+        d = root.joinpath(*parts[:-1])
+        if d.exists() and not d.is_dir():
+            continue
+        try:
+            d.mkdir(parents=True, exist_ok=True)
+            f = d / (parts[-1] + ".txt")
+            if not f.exists():
+                f.write_bytes(b"x = 1\n" * 3)
+        except (FileExistsError, NotADirectoryError):
+            continue
+    got, walk = S.PrepareFsTree(S.Scanner(None), str(root), threads=8)
+    want = [rel for rel, _ in wo.walk_fs(str(root))]
+    assert len(want) > 100
+    assert walk["files"] == want
+    assert [a.FilePath for a in got] == [r for r, _, _ in wo.fs_feed(so.SecretAnalyzer(""), str(root))]

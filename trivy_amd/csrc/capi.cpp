@@ -740,9 +740,14 @@ int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_
 void tsg_prepared_free(tsg_prepared* p) { delete p; }
 
 namespace {
+thread_local double g_pinned_alloc_ms = 0;   // time spent in pinned_alloc on this thread (feed reports)
+
 uint8_t* pinned_alloc(size_t bytes, void (**free_fn)(uint8_t*)) {
   void* p = nullptr;
-  if (tsg_alloc_pinned(bytes, &p) != 0 || !p) return nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = tsg_alloc_pinned(bytes, &p);
+  g_pinned_alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (rc != 0 || !p) return nullptr;
   *free_fn = [](uint8_t* q) { tsg_free_pinned(q); };
   return static_cast<uint8_t*>(p);
 }
@@ -877,18 +882,36 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
   if (!feed_opts(opts, &fo, &sf, &sd, &nt, &pinned, &err)) return fail(TSG_ERR_INVALID, err);
   const auto t0 = std::chrono::steady_clock::now();
   FsWalk walk;
-  if (!walk_fs_tree(root, sf, sd, &walk, &err)) return fail(TSG_ERR_INVALID, err);
+  if (!walk_fs_tree(root, sf, sd, nt, &walk, &err)) return fail(TSG_ERR_INVALID, err);
   const auto t1 = std::chrono::steady_clock::now();
-  // AnalyzeFile's gate before the file is opened (analyzer.go:417-419)
+  // AnalyzeFile's gate before the file is opened (analyzer.go:417-419): the
+  // path part first (in parallel), then Required's size check on info.Size()
   const uint32_t n = static_cast<uint32_t>(walk.files.size());
   std::vector<uint8_t> want(n, 0);
+  {
+    std::atomic<uint32_t> next{0};
+    auto run = [&]() {
+      for (;;) {
+        const uint32_t b = next.fetch_add(256);
+        if (b >= n) break;
+        for (uint32_t i = b; i < std::min(n, b + 256); ++i)
+          want[i] = static_cast<uint8_t>(secret_analyzer_wants_path(*rs->rs, fo, walk.files[i].rel));
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int t = 1; t < std::min<int>(nt, static_cast<int>(n / 256) + 1); ++t) ts.emplace_back(run);
+    run();
+    for (auto& th : ts) th.join();
+  }
+  stat_fs_files(&walk, want, nt);
   std::vector<uint64_t> starts(n, 0);
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    if (!secret_analyzer_wants(*rs->rs, fo, walk.files[i].rel, walk.files[i].size)) continue;
-    want[i] = 1;
+    if (!want[i]) continue;
+    const uint64_t sz = walk.files[i].size;
+    if (sz == UINT64_MAX || (want[i] == 2 && sz < 10)) { want[i] = 0; continue; }   // vanished / secret.go:154-156
     starts[i] = total;
-    total += walk.files[i].size;
+    total += sz;
   }
   std::unique_ptr<uint8_t[]> raw(new uint8_t[std::max<uint64_t>(total, 1)]);
   std::vector<uint64_t> got;
@@ -903,6 +926,7 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
     paths.push_back(walk.files[i].rel);
   }
   fo.assume_required = true;
+  g_pinned_alloc_ms = 0;
   auto* p = new tsg_prepared();
   if (!prepare_files(*rs->rs, fo, raw.get(), rstarts.data(), rsizes.data(), paths, nt, &p->b, &err,
                      pinned ? pinned_alloc : nullptr)) {
@@ -921,7 +945,7 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
   json_str_array(&js, all);
   js += ", \"read_bytes\": " + std::to_string(total);
   js += ", \"walk_ms\": " + std::to_string(ms(t0, t1)) + ", \"read_ms\": " + std::to_string(ms(t1, t2)) +
-        ", \"prep_ms\": " + std::to_string(ms(t2, t3));
+        ", \"prep_ms\": " + std::to_string(ms(t2, t3)) + ", \"alloc_ms\": " + std::to_string(g_pinned_alloc_ms);
   js += ", \"pinned\": ";
   js += p->b.pinned ? "true" : "false";
   js += "}";

@@ -638,6 +638,10 @@ constexpr int kAblNoLoad = 512;
 // measurement only: transitions addressed by pointer arithmetic on the
 // dynamic-LDS pointer (two VALU per byte) instead of the integer LDS address
 constexpr int kAblPtrAddr = 1024;
+// layout bit (results valid): no register double buffer -- a line's loads are
+// issued together when the line starts (a 128-byte line is then fetched in one
+// burst instead of two halves microseconds apart)
+constexpr int kAblSingle = 2048;
 // Deferred outputs (kAblDefer): a lane parks each output position of its
 // fast lines as (offset from the chunk start << 16 | state) in its own slots
 // of a global buffer (L2-resident) and handles them when its file or chunk
@@ -847,7 +851,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
 #pragma unroll
             for (int i = 0; i < kW; ++i) cur[i] = k1_load<kAbl>(data, t.p + 16 * i);
           }
-          have = t.p + 2 * kL <= t.lim;
+          have = !(kAbl & kAblSingle) && t.p + 2 * kL <= t.lim;
           if (have) {
 #pragma unroll
             for (int i = 0; i < kW; ++i) nxt[i] = k1_load<kAbl>(data, t.p + kL + 16 * i);
@@ -1267,14 +1271,17 @@ struct K1Lean {
   unsigned long long base;        // absolute position of offset 0 (the warm-up start)
   uint32_t p, lim, end, emit, cend, ci;
   uint32_t f, s, p12, nl, obn;
-  unsigned long long kw0, kw1;
 };
 
 template <uint32_t kH>
-__device__ __noinline__ void k1_lean_out(const K1LeanCtx& x, K1Lean& t, uint32_t st, unsigned long long q) {
+__device__ __forceinline__ void k1_lean_out(const K1LeanCtx& x, K1Lean& t, uint32_t st, unsigned long long q) {
   const OutMeta m = x.meta[x.oidx[st - x.first_out]];
-  t.kw0 |= m.kw0;
-  t.kw1 |= m.kw1;
+  // keyword masks straight to the file's bits (outputs are rare; no register masks)
+  uint32_t* w = x.kwmask + static_cast<size_t>(t.f) * x.kw_words;
+  or_bits(w + 0, static_cast<uint32_t>(m.kw0));
+  or_bits(w + 1, static_cast<uint32_t>(m.kw0 >> 32));
+  or_bits(w + 2, static_cast<uint32_t>(m.kw1));
+  or_bits(w + 3, static_cast<uint32_t>(m.kw1 >> 32));
   for (uint32_t j = 0; j < m.list_count; ++j) {
     const uint32_t id = x.list[m.list_begin + j];
     if (id < x.nkw) {
@@ -1305,22 +1312,9 @@ __device__ __forceinline__ void k1_lean_drain(const K1LeanCtx& x, K1Lean& t) {
   t.obn = 0;
 }
 
-__device__ __forceinline__ void k1_lean_flush(const K1LeanCtx& x, K1Lean& t) {
-  uint32_t* w = x.kwmask + static_cast<size_t>(t.f) * x.kw_words;
-  if (t.kw0) {
-    or_bits(w + 0, static_cast<uint32_t>(t.kw0));
-    or_bits(w + 1, static_cast<uint32_t>(t.kw0 >> 32));
-  }
-  if (t.kw1) {
-    or_bits(w + 2, static_cast<uint32_t>(t.kw1));
-    or_bits(w + 3, static_cast<uint32_t>(t.kw1 >> 32));
-  }
-  t.kw0 = t.kw1 = 0;
-}
-
 // a word with file-boundary and range-end checks (rare)
 template <uint32_t kH>
-__device__ __noinline__ void k1_lean_slow(const K1LeanCtx& x, K1Lean& t, v4u v) {
+__device__ __forceinline__ void k1_lean_slow(const K1LeanCtx& x, K1Lean& t, v4u v) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   uint32_t fend = static_cast<uint32_t>(min(x.offsets[t.f + 1] - t.base, 0xffffffffull));
   const bool special = x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit;
@@ -1329,7 +1323,6 @@ __device__ __noinline__ void k1_lean_slow(const K1LeanCtx& x, K1Lean& t, v4u v) 
     const uint32_t q = t.p + k;
     if (q >= t.end) break;
     if (q >= fend) {
-      k1_lean_flush(x, t);
       do { ++t.f; fend = static_cast<uint32_t>(min(x.offsets[t.f + 1] - t.base, 0xffffffffull)); } while (q >= fend);
       t.s = 0;
       t.p12 = 0;
@@ -1351,33 +1344,37 @@ __device__ __noinline__ void k1_lean_slow(const K1LeanCtx& x, K1Lean& t, v4u v) 
   t.lim = min(t.end, fend);
 }
 
-template <uint32_t kH>
+template <uint32_t kH, int kG>
 __device__ __forceinline__ void k1_lean_word(const K1LeanCtx& x, K1Lean& t, v4u v) {
   const bool emit = t.p >= t.emit;
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   uint32_t s = t.s;
+  // groups of kG bytes: kG class reads in flight, then kG dependent transitions
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    uint32_t c2[8];
+  for (int h = 0; h < 16 / kG; ++h) {
+    uint32_t c2[kG];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c2[k] = k1_lds8((w[2 * h + (k >> 2)] >> ((k & 3) * 8)) & 0xffu);
+    for (int k = 0; k < kG; ++k) {
+      const int j = kG * h + k;
+      c2[k] = k1_lds8((w[j >> 2] >> ((j & 3) * 8)) & 0xffu);
+    }
     const uint32_t s0 = s;
     uint32_t mx = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kG; ++k) {
       s = k1_step5(s, c2[k]);
       mx = max(mx, s);
     }
     if (emit && mx >= x.first_out) {
       uint32_t r = s0;
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < kG; ++k) {
         r = k1_step5(r, c2[k]);
         if (r >= x.first_out) {
           if (t.obn < kOutSlots) {
-            x.ob[t.obn * x.ob_stride] = ((t.p + 8 * h + k - t.emit) << 16) | r;
+            x.ob[t.obn * x.ob_stride] = ((t.p + kG * h + k - t.emit) << 16) | r;
             ++t.obn;
           } else {
-            k1_lean_out<kH>(x, t, r, t.base + t.p + 8 * h + k);
+            k1_lean_out<kH>(x, t, r, t.base + t.p + kG * h + k);
           }
         }
       }
@@ -1397,7 +1394,7 @@ __device__ __forceinline__ void k1_lean_word(const K1LeanCtx& x, K1Lean& t, v4u 
   t.p += 16;
 }
 
-template <uint32_t kH>
+template <uint32_t kH, int kG>
 __global__ __attribute__((amdgpu_flat_work_group_size(1024, 1024), amdgpu_waves_per_eu(8, 8)))
 void tsg_k1_scan_v6(
     const uint8_t* __restrict__ data, unsigned long long total,
@@ -1470,7 +1467,7 @@ void tsg_k1_scan_v6(
       t.end = static_cast<uint32_t>(min(min(c + kU, rend) * chunk, total) - t.base);
       t.cend = min(t.emit + chunk, t.end);
       t.ci = static_cast<uint32_t>(c);
-      t.s = 0; t.p12 = 0; t.nl = 0; t.obn = 0; t.kw0 = t.kw1 = 0;
+      t.s = 0; t.p12 = 0; t.nl = 0; t.obn = 0;
       t.f = file_of(offsets, nfiles, t.base);
       t.lim = static_cast<uint32_t>(min(static_cast<unsigned long long>(t.end), offsets[t.f + 1] - t.base));
       while (t.p < t.end) {
@@ -1492,7 +1489,7 @@ void tsg_k1_scan_v6(
             if ((hb & 0x80808080u) && k1_line_special(lp, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) k1_lean_word<kH>(x, t, line[i]);
+          for (int i = 0; i < 4; ++i) k1_lean_word<kH, kG>(x, t, line[i]);
         } else {
           k1_lean_drain<kH>(x, t);                           // parked outputs belong to file t.f
           for (int i = 0; i < 4 && t.p < t.end; ++i) {
@@ -1507,7 +1504,6 @@ void tsg_k1_scan_v6(
         }
       }
       k1_lean_drain<kH>(x, t);
-      k1_lean_flush(x, t);
       if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1868,7 +1864,7 @@ const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int a
       TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(82) TSG_K1_V3(146) TSG_K1_V3(210) TSG_K1_V3(112) TSG_K1_V3(240)
       TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466)
       TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(912) TSG_K1_V3(784)
-      TSG_K1_V3(1488)
+      TSG_K1_V3(1488) TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(2192)
 #undef TSG_K1_V3
       default: return nullptr;
     }
@@ -1906,8 +1902,8 @@ constexpr uint32_t k1_lds5(uint32_t table_bytes, uint32_t hits) {
 // 64- or 32-byte register lines, or single (one workgroup per CU)
 const void* k1_kernel5(bool dual, int line_words) {
   if (dual) {
-    if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v5<8, 2, kK1HitsDual>);
-    return reinterpret_cast<const void*>(&tsg_k1_scan_v6<kK1HitsDual>);
+    if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v6<kK1HitsDual, 4>);
+    return reinterpret_cast<const void*>(&tsg_k1_scan_v6<kK1HitsDual, 8>);
   }
   if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v5<4, 2, kK1HitsSingle>);
   return reinterpret_cast<const void*>(&tsg_k1_scan_v5<4, 4, kK1HitsSingle>);

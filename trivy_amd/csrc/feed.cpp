@@ -42,8 +42,15 @@ std::string go_ext(const std::string& name) {
   return "";
 }
 
+bool required_path(const Ruleset& rs, const std::string& path, const std::string& cfg_base);
+
 bool required(const Ruleset& rs, const std::string& path, uint64_t size, const std::string& cfg_base) {
   if (size < 10) return false;                                     // secret.go:154-156
+  return required_path(rs, path, cfg_base);
+}
+
+// Required's checks other than the size (secret.go:158-188)
+bool required_path(const Ruleset& rs, const std::string& path, const std::string& cfg_base) {
   const size_t slash = path.rfind('/');                            // filepath.Split
   const std::string dir = slash == std::string::npos ? "" : path.substr(0, slash + 1);
   const std::string name = slash == std::string::npos ? path : path.substr(slash + 1);
@@ -179,6 +186,13 @@ bool parse_file_patterns(const std::vector<std::string>& entries, FeedOpts* out,
 
 bool secret_analyzer_wants(const Ruleset& rs, const FeedOpts& opts, const std::string& path, uint64_t size) {
   return wants(rs, opts, path, size, go_base(opts.config_path));
+}
+
+int secret_analyzer_wants_path(const Ruleset& rs, const FeedOpts& opts, const std::string& path) {
+  const std::string clean = trim_left_slash(path);
+  for (const auto& rx : opts.patterns)
+    if (rx->match_string(reinterpret_cast<const uint8_t*>(clean.data()), clean.size())) return 1;
+  return required_path(rs, clean, go_base(opts.config_path)) ? 2 : 0;
 }
 
 bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,

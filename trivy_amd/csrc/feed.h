@@ -33,6 +33,9 @@ bool parse_file_patterns(const std::vector<std::string>& entries, FeedOpts* out,
 // AnalyzeFile's gate for the secret analyzer (analyzer.go:403-419):
 // filePatternMatch(TrimLeft(path, "/")) || Required(TrimLeft(path, "/"), size)
 bool secret_analyzer_wants(const Ruleset& rs, const FeedOpts& opts, const std::string& path, uint64_t size);
+// The same split for a walk that learns sizes later: 0 = not wanted, 1 =
+// wanted by a file pattern (any size), 2 = wanted if size >= 10 (Required).
+int secret_analyzer_wants_path(const Ruleset& rs, const FeedOpts& opts, const std::string& path);
 
 // Output buffer for the packed contents: returns memory of `bytes` bytes and
 // sets the deleter, or nullptr (the batch then uses the heap).

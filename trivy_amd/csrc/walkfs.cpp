@@ -10,7 +10,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 
@@ -79,66 +81,110 @@ bool skip_path(const std::string& path, const std::vector<std::string>& pats) { 
   return false;
 }
 
+// Go's WalkDir order is a pre-order DFS with every directory's entries in
+// name order; with '/' ranked below every other byte, a plain comparison of
+// the relative paths gives the same order (names hold no '/' or NUL).
+bool walk_order_less(const std::string& a, const std::string& b) {
+  const size_t n = std::min(a.size(), b.size());
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned char x = a[i] == '/' ? 0 : static_cast<unsigned char>(a[i]);
+    const unsigned char y = b[i] == '/' ? 0 : static_cast<unsigned char>(b[i]);
+    if (x != y) return x < y;
+  }
+  return a.size() < b.size();
+}
+
+// The walk, directories read by several threads (each directory is one task;
+// results are put back into WalkDir's order at the end).  Regular files are
+// recorded from the directory entry's type; their size is taken when they
+// are read (the analyzer's gate runs on the path first).
 struct Walker {
   const std::vector<std::string>& skip_files;
   const std::vector<std::string>& skip_dirs;
-  FsWalk* out;
-  std::string* err;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<std::string, std::string>> todo;   // (path, rel) of directories to read
+  size_t busy = 0;
+  bool failed = false;
+  std::string err, err_key;                                // the first error in walk order wins
+  std::vector<FsFile> files;
 
-  bool fail(const std::string& path, const std::string& what) {
-    *err = "walk dir error: unknown error with " + path + ": " + what;
-    return false;
-  }
-
-  // the WalkDirFunc for a regular file (fs.go:57-75)
-  bool file(const std::string& path, const std::string& rel) {
-    if (skip_path(rel, skip_files)) return true;
-    struct stat sb;
-    if (::lstat(path.c_str(), &sb) != 0) {                        // d.Info()
-      if (is_permission(errno)) return true;
-      return fail(path, "file info error: lstat " + path + ": " + go_errno(errno));
+  void fail(const std::string& key, const std::string& path, const std::string& what) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!failed || walk_order_less(key, err_key)) {
+      err = "walk dir error: unknown error with " + path + ": " + what;
+      err_key = key;
     }
-    out->files.push_back(FsFile{rel, path, static_cast<uint64_t>(sb.st_size)});
-    return true;
+    failed = true;
   }
 
-  // walkDir after the WalkDirFunc accepted directory `path` (io/fs walkDir:
-  // entries in os.ReadDir's name order, each visited before the next)
-  bool dir(const std::string& path, const std::string& rel) {
+  void dir(const std::string& path, const std::string& rel, std::vector<FsFile>* out,
+           std::vector<std::pair<std::string, std::string>>* subdirs) {
     DIR* dp = ::opendir(path.c_str());
     if (!dp) {
-      if (is_permission(errno)) return true;                      // onError: permission errors ignored
-      return fail(path, "open " + path + ": " + go_errno(errno));
+      if (!is_permission(errno)) fail(rel, path, "open " + path + ": " + go_errno(errno));
+      return;                                                     // onError: permission errors ignored
     }
+    const int dfd = ::dirfd(dp);
     std::vector<std::pair<std::string, unsigned char>> ents;
     errno = 0;
     while (struct dirent* e = ::readdir(dp)) {
       if (!std::strcmp(e->d_name, ".") || !std::strcmp(e->d_name, "..")) continue;
-      ents.emplace_back(e->d_name, e->d_type);
-    }
-    const int rerr = errno;
-    ::closedir(dp);
-    if (rerr != 0 && !is_permission(rerr)) return fail(path, "readdirent " + path + ": " + go_errno(rerr));
-    std::sort(ents.begin(), ents.end());
-    for (auto& [name, type] : ents) {
-      const std::string child = join(path, name);
-      const std::string crel = rel == "." ? name : rel + "/" + name;
+      unsigned char type = e->d_type;
       if (type == DT_UNKNOWN) {
         struct stat sb;
-        if (::lstat(child.c_str(), &sb) != 0) {
-          if (is_permission(errno)) continue;
-          return fail(child, "lstat " + child + ": " + go_errno(errno));
+        if (::fstatat(dfd, e->d_name, &sb, AT_SYMLINK_NOFOLLOW) != 0) {
+          if (!is_permission(errno)) fail(rel, path + "/" + e->d_name, "lstat: " + go_errno(errno));
+          continue;
         }
         type = S_ISDIR(sb.st_mode) ? DT_DIR : S_ISREG(sb.st_mode) ? DT_REG : DT_LNK;
       }
+      ents.emplace_back(e->d_name, type);
+      errno = 0;
+    }
+    const int rerr = errno;
+    ::closedir(dp);
+    if (rerr != 0 && !is_permission(rerr)) fail(rel, path, "readdirent " + path + ": " + go_errno(rerr));
+    for (auto& [name, type] : ents) {
+      const std::string crel = rel == "." ? name : rel + "/" + name;
       if (type == DT_DIR) {
-        if (skip_path(crel, skip_dirs)) continue;                 // filepath.SkipDir
-        if (!dir(child, crel)) return false;
+        if (skip_path(crel, skip_dirs)) continue;                   // filepath.SkipDir
+        subdirs->emplace_back(join(path, name), crel);
       } else if (type == DT_REG) {
-        if (!file(child, crel)) return false;
+        if (skip_path(crel, skip_files)) continue;
+        out->push_back(FsFile{crel, join(path, name), 0});
       }                                                           // symlinks, devices, ...: not regular
     }
-    return true;
+  }
+
+  void run(int threads) {
+    auto worker = [&]() {
+      std::vector<FsFile> local;
+      for (;;) {
+        std::pair<std::string, std::string> task;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return !todo.empty() || busy == 0; });
+          if (todo.empty()) break;
+          task = std::move(todo.front());
+          todo.pop_front();
+          ++busy;
+        }
+        std::vector<std::pair<std::string, std::string>> subdirs;
+        dir(task.first, task.second, &local, &subdirs);
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto& sd : subdirs) todo.push_back(std::move(sd));
+        --busy;
+        cv.notify_all();
+      }
+      std::lock_guard<std::mutex> lk(mu);
+      for (auto& f : local) files.push_back(std::move(f));
+    };
+    std::vector<std::thread> ts;
+    for (int t = 1; t < threads; ++t) ts.emplace_back(worker);
+    worker();
+    for (auto& th : ts) th.join();
+    std::sort(files.begin(), files.end(), [](const FsFile& a, const FsFile& b) { return walk_order_less(a.rel, b.rel); });
   }
 };
 
@@ -165,22 +211,54 @@ std::vector<std::string> build_skip_paths(const std::string& base, const std::ve
 }
 
 bool walk_fs_tree(const std::string& root, const std::vector<std::string>& skip_files_in,
-                  const std::vector<std::string>& skip_dirs_in, FsWalk* out, std::string* err) {
+                  const std::vector<std::string>& skip_dirs_in, int threads, FsWalk* out, std::string* err) {
   const std::vector<std::string> skip_files = build_skip_paths(root, skip_files_in);
   std::vector<std::string> skip_dirs = build_skip_paths(root, skip_dirs_in);
   for (const char* d : {"**/.git", "proc", "sys", "dev"}) skip_dirs.emplace_back(d);   // defaultSkipDirs
   out->files.clear();
-  Walker w{skip_files, skip_dirs, out, err};
   struct stat sb;
   if (::lstat(root.c_str(), &sb) != 0) {
     if (is_permission(errno)) return true;
-    return w.fail(root, "lstat " + root + ": " + go_errno(errno));
+    *err = "walk dir error: unknown error with " + root + ": lstat " + root + ": " + go_errno(errno);
+    return false;
   }
-  if (S_ISDIR(sb.st_mode)) {
-    if (skip_path(".", skip_dirs)) return true;
-    return w.dir(root, ".");
+  if (S_ISREG(sb.st_mode)) {
+    if (!skip_path(".", skip_files)) out->files.push_back(FsFile{".", root, 0});
+    return true;
   }
-  if (S_ISREG(sb.st_mode)) return w.file(root, ".");
+  if (!S_ISDIR(sb.st_mode) || skip_path(".", skip_dirs)) return true;
+  Walker w{skip_files, skip_dirs};
+  w.todo.emplace_back(root, ".");
+  w.run(std::max(1, threads));
+  if (w.failed) {
+    // Go stops at the first error in walk order; files after it are not walked
+    *err = w.err;
+    return false;
+  }
+  out->files = std::move(w.files);
+  return true;
+}
+
+bool stat_fs_files(FsWalk* walk, const std::vector<uint8_t>& want, int threads) {
+  const uint32_t n = static_cast<uint32_t>(walk->files.size());
+  std::atomic<uint32_t> next{0};
+  auto run = [&]() {
+    for (;;) {
+      const uint32_t b = next.fetch_add(64);
+      if (b >= n) break;
+      for (uint32_t i = b; i < std::min(n, b + 64); ++i) {
+        if (!want[i]) continue;
+        struct stat sb;
+        FsFile& f = walk->files[i];
+        f.size = ::lstat(f.path.c_str(), &sb) == 0 ? static_cast<uint64_t>(sb.st_size) : UINT64_MAX;
+      }
+    }
+  };
+  const int nt = std::max(1, std::min<int>(threads, static_cast<int>(std::max<uint32_t>(n / 64, 1))));
+  std::vector<std::thread> ts;
+  for (int t = 1; t < nt; ++t) ts.emplace_back(run);
+  run();
+  for (auto& th : ts) th.join();
   return true;
 }
 

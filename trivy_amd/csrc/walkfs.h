@@ -15,7 +15,7 @@ namespace tsg {
 struct FsFile {
   std::string rel;      // filepath.ToSlash(filepath.Rel(root, path)): the analyzer's FilePath
   std::string path;     // path as opened (root joined with the entries)
-  uint64_t size = 0;    // d.Info().Size() at walk time
+  uint64_t size = 0;    // info.Size() (stat_fs_files; UINT64_MAX: vanished)
 };
 
 struct FsWalk {
@@ -24,8 +24,13 @@ struct FsWalk {
 
 // skip_files / skip_dirs as given on the command line (--skip-files /
 // --skip-dirs); err mirrors Walk's "walk dir error: unknown error with ...".
+// Directories are read by `threads` threads; the files come back in
+// WalkDir's order.
 bool walk_fs_tree(const std::string& root, const std::vector<std::string>& skip_files,
-                  const std::vector<std::string>& skip_dirs, FsWalk* out, std::string* err);
+                  const std::vector<std::string>& skip_dirs, int threads, FsWalk* out, std::string* err);
+
+// info.Size() of the files with want[i] (lstat, `threads` threads)
+bool stat_fs_files(FsWalk* walk, const std::vector<uint8_t>& want, int threads);
 
 // walker.FS.BuildSkipPaths(base, paths) with the process's working directory
 std::string go_filepath_clean(const std::string& p);
