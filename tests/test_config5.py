@@ -62,10 +62,7 @@ def test_config5_parity_cpu(tmp_path, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["", "5"])
-def test_config5_parity_gpu(tmp_path, monkeypatch, variant):
-    if variant:
-        monkeypatch.setenv("TSG_K1_VARIANT", variant)
+def test_config5_parity_gpu(tmp_path):
     path, args, _ = _setup(tmp_path, 1_000_000, 7)
     want = _want(path, args)
     got = S.Scanner(S.ParseConfig(path)).ScanBatch(args)

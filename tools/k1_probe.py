@@ -31,9 +31,8 @@ def main():
     ap.add_argument("--prewarm-ms", type=float, default=0.0,
                     help="keep the GPU busy (torch elementwise kernels) this long right before each K1/K2 run")
     ap.add_argument("--variants", default="",
-                    help="comma list of VARIANT[:ABL[:CHUNK[:THREADS/STREAMS[:NAME=V+NAME=V]]]] (TSG_K1_VARIANT / "
-                         "TSG_K1_ABL / TSG_K1_CHUNK / TSG_K1_CFG / extra TSG_* settings), "
-                         "one engine each")
+                    help="comma list of ABL[:CHUNK[:NAME=V+NAME=V]] (TSG_K1_ABL build bits / TSG_K1_CHUNK / extra "
+                         "TSG_* settings), one engine each")
     args = ap.parse_args()
     import torch
 
@@ -53,20 +52,13 @@ def main():
     variants = [v for v in args.variants.split(",") if v] or [None]
     for v in variants:
         if v is not None:
-            parts = v.split(":") + ["", "", "", ""]
-            os.environ["TSG_K1_VARIANT"] = parts[0]
-            os.environ["TSG_K1_ABL"] = parts[1] or "0"
-            if parts[2]:
-                os.environ["TSG_K1_CHUNK"] = parts[2]
+            parts = v.split(":") + ["", ""]
+            os.environ["TSG_K1_ABL"] = parts[0] or "464"
+            if parts[1]:
+                os.environ["TSG_K1_CHUNK"] = parts[1]
             else:
                 os.environ.pop("TSG_K1_CHUNK", None)
-            if parts[3]:
-                os.environ["TSG_K1_CFG"] = parts[3].replace("/", ",")
-            else:
-                os.environ.pop("TSG_K1_CFG", None)
-            for k in ("TSG_K1_LINE5", "TSG_K1_SINGLE5"):
-                os.environ.pop(k, None)
-            for kv in (parts[4] if len(parts) > 4 else "").split("+"):   # extra NAME=VALUE settings
+            for kv in parts[2].split("+"):                # extra NAME=VALUE settings
                 if "=" in kv:
                     k, _, val = kv.partition("=")
                     os.environ[k] = val

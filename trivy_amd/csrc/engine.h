@@ -100,14 +100,7 @@ class Engine {
   std::vector<CallCtx*> free_calls_;
   // tuning (TSG_* environment knobs, read once at create)
   uint32_t chunk_ = 0;                  // K1 bytes per lane chunk (TSG_K1_CHUNK); 0 = by launch size (k1_chunk_for)
-  int k1_streams_ = 1;                  // TSG_K1_CFG="threads,streams"
-  uint32_t k1_threads_ = 1024;
-  int k1_variant_ = 3;                  // TSG_K1_VARIANT: 1 = tsg_k1_scan, 3 = tsg_k1_scan_v3, 4 = tsg_k1_scan_v4
-  // chunks per lane in one K1 wave item (the hit record's offset range)
-  int k1_item_chunks() const { return k1_variant_ == 4 ? 2 : (k1_variant_ == 3 || k1_variant_ == 5) ? 4 : k1_streams_; }
-  int k1_line5_ = 4;                    // v5: 16-byte words per register line (TSG_K1_LINE5: 2 or 4)
-  bool k1_single5_ = false;             // v5: force one workgroup per CU (TSG_K1_SINGLE5=1)
-  // TSG_K1_ABL: v3 build (kAbl* bits).  Default 464 = deferred outputs +
+  // TSG_K1_ABL: K1 build (kAbl* bits).  Default 464 = deferred outputs +
   // rolled word loop + 64-byte lines + temporal loads (layout bits, results
   // valid); the other bits are measurement builds whose results are invalid.
   int k1_abl_ = 464;

@@ -71,7 +71,8 @@ constexpr uint32_t kWaveHits = kK1WaveHits;   // per-wave LDS hit buffer entries
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
 constexpr double kDenseFilesPerGB = 8000.0;   // upload segmentation: "many small files" (image layers: ~48k/GB)
-constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [2] overflow, [3] v4 LDS-base error, [4 + g] v3/v4 items of group g
+constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [1] K2 count, [2] overflow, [3] LDS-base error, [4 + g] K1 items of group g
+constexpr int kItemChunks = 4;         // a K1 wave item: 64 lanes x (up to) 4 chunks
 
 // Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
 // record's 32 - kAnchorBits offset bits.
@@ -120,7 +121,7 @@ __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
 // state depends only on the last max_pattern_bytes - 1 bytes of the file.
 struct K1Stream {
   unsigned long long p, lim, emit;   // next byte; min(stream end, file end); first byte with outputs
-  unsigned long long end;            // stream end (v1 / v4: one chunk; v3: the lane's range of chunks)
+  unsigned long long end;            // stream end: the lane's range of chunks
   unsigned long long cend;           // v3: end of the current chunk (its '\n' count is stored there)
   unsigned long long ci;             // v3: index of the current chunk
   uint32_t f, s, p12, nl;            // file; DFA row offset; previous two bytes (p1 | p2 << 8); newlines
@@ -167,7 +168,7 @@ __device__ __forceinline__ uint32_t k1_step(const uint16_t* next, uint32_t s, ui
   return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(next) + ((s << 1) + c2));
 }
 
-// LDS reads by integer LDS address (v3 / v4): the kernel's dynamic LDS starts
+// LDS reads by integer LDS address: the kernel's dynamic LDS starts
 // at offset 0 (no static LDS; checked at run time by k1_lds_base_ok), so a
 // transition address is one v_lshl_add_u32 feeding a ds_read_u16 whose
 // immediate offset is the table's position.
@@ -180,32 +181,6 @@ __device__ __forceinline__ bool k1_lds_base_ok(const uint8_t* smem) {
 }
 
 __device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Stream& t) { return t.end; }
-
-__device__ __forceinline__ void k1_out(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
-  const uint32_t o = x.next[st + x.nclasses];          // output-state index (row's spare slot)
-  const OutMeta m = x.meta[o];
-  t.kw0 |= m.kw0;
-  t.kw1 |= m.kw1;
-  for (uint32_t j = 0; j < m.list_count; ++j) {
-    const uint32_t id = x.list[m.list_begin + j];
-    if (id < x.nkw) {
-      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
-    } else {
-      const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
-      if (li < kWaveHits) {
-        x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
-      } else {                                           // buffer full: straight to the region
-        const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
-        if (gi < x.region_cap) {
-          x.hits[gi] = (q << 24) | (id - x.nkw);
-        } else {                                         // region full: the shared overflow pool
-          const uint32_t oi = atomicAdd(x.over_cnt, 1u);
-          if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
-        }
-      }
-    }
-  }
-}
 
 // U+0130 / U+017F / U+212A fold onto ASCII letters: flag every file that
 // overlaps a 16-byte word ending such a sequence (host re-scans it exactly).
@@ -257,7 +232,6 @@ __device__ __forceinline__ void k1_out_v3(const K1Ctx& x, K1Stream& t, uint32_t 
 }
 
 // One 16-byte word of one stream with file-boundary and stream-end checks.
-template <bool kInlineMeta = false>
 __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4], uint32_t S = 0) {
   const unsigned long long end = k1_end(x, t);
   unsigned long long fend = x.offsets[t.f + 1];
@@ -276,8 +250,7 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
     if (q >= t.emit) {
       t.nl += (b == 0x0au);
       if (t.s >= x.first_out) {
-        if (kInlineMeta) k1_out_v3(x, t, t.s, q, S);
-        else k1_out(x, t, t.s, q);
+        k1_out_v3(x, t, t.s, q, S);
       }
     }
     t.p12 = ((t.p12 << 8) & 0xff00u) | b;
@@ -286,18 +259,7 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
   t.lim = min(end, fend);
 }
 
-// Outputs of a fast word (rare): walk it again from its start state and emit.
-__device__ __forceinline__ void k1_word_emit(const K1Ctx& x, K1Stream& t, uint32_t s0, uint32_t w0, uint32_t w1,
-                                             uint32_t w2, uint32_t w3) {
-  const uint32_t w[4] = {w0, w1, w2, w3};
-  uint32_t s = s0;
-  for (int k = 0; k < 16; ++k) {
-    s = k1_step(x.next, s, x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu]);
-    if (s >= x.first_out) k1_out(x, t, s, t.p + k);
-  }
-}
-
-// warm_bytes: a multiple of the kernel's line size (v1 / v4: 128 B, v3: 64 B)
+// warm_bytes: a multiple of the kernel's line size (64 B; 128 B for the kAblLine64-off builds)
 __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned long long c0, uint32_t warm_bytes) {
   t.emit = c0;
   t.p = c0 > warm_bytes ? c0 - warm_bytes : 0;   // c0 is a multiple of 128
@@ -314,201 +276,6 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
   t.lim = min(end, x.offsets[t.f + 1]);
 }
 
-// K1: one pass over the batch.  Workgroup b scans a contiguous range of wave
-// work items (an item = 64 lanes x kS consecutive chunks); its waves take
-// items from an LDS counter.  Each wave owns an LDS hit buffer, flushed once
-// per item into the workgroup's own region of the hit list (LDS atomics
-// only: no global atomic is shared between workgroups, which serialise at the
-// memory side).  block_hits[b] = hits written by workgroup b (> region_cap:
-// overflow, the host grows the list and runs K1 again).
-template <bool kLds, int kS, int kThreads>
-__global__ __launch_bounds__(kThreads) void tsg_k1_scan(
-    const uint8_t* __restrict__ data, unsigned long long total,
-    const uint64_t* __restrict__ offsets, uint32_t nfiles,
-    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
-    uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
-    const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
-    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
-    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
-    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
-    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ /*item_ctr: v3*/,
-    uint32_t* __restrict__ /*obuf: v3*/, uint32_t /*tail_rounds: v3*/) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // LDS layout: [per-wave hit buffers | per-wave counts | region count, item counter | (scan table | class map |
-  //              output meta | output list)]
-  constexpr uint32_t kWaves = kThreads / 64;
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
-  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count, [1] next item
-  uint8_t* s_tab = smem + kWaves * kWaveHits * 4 + kMaxWaves * 4 + 16;
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) { s_block[0] = 0; s_block[1] = 0; }
-  K1Ctx x;
-  x.data = data; x.total = total; x.chunk = chunk;
-  x.offsets = offsets; x.nfiles = nfiles;
-  x.next = g_next; x.cls = g_cls;
-  x.first_out = first_out; x.nclasses = nclasses;
-  x.meta = g_meta; x.list = g_list; x.nkw = nkw;
-  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
-  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
-  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
-  x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
-  if (kLds) {
-    uint16_t* s_next = reinterpret_cast<uint16_t*>(s_tab);
-    const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
-    uint8_t* s_cls = s_tab + padded;
-    const uint4* src = reinterpret_cast<const uint4*>(g_next);
-    uint4* dst = reinterpret_cast<uint4*>(s_next);
-    for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = g_cls[i];
-    OutMeta* s_meta = reinterpret_cast<OutMeta*>(s_cls + 256);
-    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_meta + nmeta);
-    for (uint32_t i = threadIdx.x; i < nmeta; i += blockDim.x) s_meta[i] = g_meta[i];
-    for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
-    x.next = s_next;
-    x.cls = s_cls;
-    x.meta = s_meta;
-    x.list = s_list;
-  }
-  __syncthreads();
-  const unsigned long long nwork = (nchunks + kS - 1) / kS;   // lane work units (kS chunks each)
-  const unsigned long long nitems = (nwork + 63) / 64;       // wave work items
-  const unsigned long long per_block = (nitems + gridDim.x - 1) / gridDim.x;
-  const unsigned long long first_item = per_block * blockIdx.x;
-  const unsigned long long last_item = min(first_item + per_block, nitems);
-  for (;;) {
-    unsigned long long item = 0;
-    if (lane == 0) {
-      item = first_item + atomicAdd(&s_block[1], 1u);
-      *x.w_hitcnt = 0;
-    }
-    item = __shfl(item, 0);
-    if (item >= last_item) break;                              // wave-uniform exit
-    __builtin_amdgcn_wave_barrier();
-    x.item_base = item * 64 * kS * static_cast<unsigned long long>(chunk);
-    const unsigned long long wi = item * 64 + lane;
-    if (wi < nwork) {
-      K1Stream S[kS];
-#pragma unroll
-      for (int j = 0; j < kS; ++j) k1_init(x, S[j], min((wi * kS + j) * chunk, total), warm_lines * 128u);
-      for (;;) {
-        bool any = false, all_fast = true;
-#pragma unroll
-        for (int j = 0; j < kS; ++j) {
-          any |= S[j].p < S[j].lim || S[j].p < k1_end(x, S[j]);
-          all_fast &= S[j].p + 128 <= S[j].lim;   // a whole line inside the stream and one file
-        }
-        if (!any) break;
-        if (all_fast) {
-          uint4 line[kS][8];
-#pragma unroll
-          for (int j = 0; j < kS; ++j) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              // the 8 loads of a line are issued back to back so the line is
-              // fetched from HBM once
-              const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(data + S[j].p + 16 * i));
-              line[j][i] = make_uint4(v.x, v.y, v.z, v.w);
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            // the class lookups do not depend on the state: issue them all,
-            // then walk the kS dependent transition chains interleaved
-            uint32_t cl[kS][16];
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-              const uint32_t w[4] = {line[j][i].x, line[j][i].y, line[j][i].z, line[j][i].w};
-              if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && S[j].p >= S[j].emit)
-                k1_special(x, S[j], w, ~0ull, ~0ull);
-#pragma unroll
-              for (int k = 0; k < 16; ++k) cl[j][k] = x.cls[(w[k >> 2] >> ((k & 3) * 8)) & 0xffu];
-            }
-            uint32_t st[kS][16], mx[kS];
-#pragma unroll
-            for (int j = 0; j < kS; ++j) mx[j] = 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-#pragma unroll
-              for (int j = 0; j < kS; ++j) {
-                st[j][k] = k1_step(x.next, k ? st[j][k - 1] : S[j].s, cl[j][k]);
-                mx[j] = max(mx[j], st[j][k]);
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-              const uint32_t w0 = line[j][i].x, w1 = line[j][i].y, w2 = line[j][i].z, w3 = line[j][i].w;
-              S[j].s = st[j][15];
-              if (S[j].p >= S[j].emit) {
-                S[j].nl += nl_in_word(w0) + nl_in_word(w1) + nl_in_word(w2) + nl_in_word(w3);
-                // outputs (a few % of lane-words): the states are in
-                // registers; each position is skipped by the whole wave
-                // unless one of its lanes has an output there
-                if (mx[j] >= first_out) {
-#pragma unroll
-                  for (int k = 0; k < 16; ++k)
-                    if (st[j][k] >= first_out) k1_out(x, S[j], st[j][k], S[j].p + k);
-                }
-              }
-              S[j].p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
-              S[j].p += 16;
-            }
-          }
-        } else {
-          // a line with a file boundary or a stream end (rare): word by word,
-          // one stream at a time, words re-read from memory (L2 hits)
-          for (int j = 0; j < kS; ++j) {
-            for (int i = 0; i < 8 && S[j].p < k1_end(x, S[j]); ++i) {
-              const v4u v = *reinterpret_cast<const v4u*>(data + S[j].p);
-              const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-              k1_word_slow(x, S[j], w);
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kS; ++j) {
-        const unsigned long long c = wi * kS + j;
-        if (c < nchunks) {
-          flush_kw(x.kwmask, kw_words, S[j].f, S[j].kw0, S[j].kw1);
-          if (x.primary) nl_count[c] = static_cast<uint16_t>(S[j].nl);
-        }
-      }
-    }
-    // flush this wave's hit buffer (the wave has reconverged here)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t n = min(*x.w_hitcnt, kWaveHits);
-    uint32_t b0 = 0, o0 = 0;
-    if (lane == 0 && n) {
-      b0 = atomicAdd(x.b_hitcnt, n);
-      // entries past the region's capacity go to the shared overflow pool
-      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
-    }
-    b0 = __shfl(b0, 0);
-    o0 = __shfl(o0, 0);
-    const uint32_t spill_from = max(b0, region_cap);
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t h = x.w_hits[i];
-      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
-      if (b0 + i < region_cap) {
-        x.hits[b0 + i] = v;
-      } else {
-        const uint32_t oi = o0 + (b0 + i - spill_from);
-        if (oi < x.over_cap) x.over[oi] = v;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
-}
-
-// kStats (TSG_K2_STATS, measurement): per rule, atomically count the hits,
-// the hits past the keyword gate, the verify starts walked and the bytes
-// walked (k2s[4 * rule + 0..3]).
 template <bool kStats>
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
@@ -888,7 +655,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            k1_word_slow<true>(x, t, w, S);
+            k1_word_slow(x, t, w, S);
           }
         }
       }
@@ -929,947 +696,18 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
 }
 
-// K1 v5: v3's pass over a compact table, so two workgroups share a CU.
-//  * table: the scan DFA's byte classes with identical transition columns
-//    merged (exact: the automaton cannot tell them apart), rows of exactly
-//    Cr = C rounded to an odd dword count, no spare slot and no inline
-//    metadata; entries are the next state's row offset in DWORDS, so the
-//    transition address is one v_lshl_add ((s << 2) + class * 2) and offsets
-//    reach 256 KiB.  The builtin rules: 758 states x 50 classes = 75.8 KB.
-//  * output states (rows >= first_out) are looked up in global memory
-//    (L2-resident: oidx[row - first_out] -> OutMeta, output list), only at
-//    the rare drain of a lane's parked outputs;
-//  * LDS = class map + table + per-wave hit buffers of kH entries; with the
-//    builtin rules and kH = 64 that is 80.2 KB, two 1024-thread workgroups
-//    per CU (32 waves; kWpe = 8 waves per SIMD caps K1 at 64 VGPRs);
-//  * a 16-byte word is walked in two halves of 8 bytes: the 8 class reads
-//    first, then the 8 dependent transitions with a running max; a half whose
-//    max reaches the output rows (rare) is walked once more to park its
-//    outputs, so no per-byte state array is kept live.
-// Everything else (guided schedule, file-boundary words, '\n' counts,
-// fold-special flags, keyword register masks, deferred outputs) is v3's.
-struct K1Out5 {
-  const uint16_t* oidx;   // global: row - first_out -> output-state index
-};
-
-template <uint32_t kH>
-__device__ __forceinline__ void k1_emit_id5(const K1Ctx& x, K1Stream& t, uint32_t id, unsigned long long q) {
-  if (id < x.nkw) {
-    atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
-    return;
-  }
-  const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
-  if (li < kH) {
-    x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
-  } else {                                               // buffer full: straight to the region
-    const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
-    if (gi < x.region_cap) {
-      x.hits[gi] = (q << 24) | (id - x.nkw);
-    } else {                                             // region full: the shared overflow pool
-      const uint32_t oi = atomicAdd(x.over_cnt, 1u);
-      if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
-    }
-  }
-}
-
-template <uint32_t kH>
-__device__ __forceinline__ void k1_out5(const K1Ctx& x, const K1Out5& o, K1Stream& t, uint32_t st,
-                                        unsigned long long q) {
-  const OutMeta m = x.meta[o.oidx[st - x.first_out]];
-  t.kw0 |= m.kw0;
-  t.kw1 |= m.kw1;
-  for (uint32_t j = 0; j < m.list_count; ++j) k1_emit_id5<kH>(x, t, x.list[m.list_begin + j], q);
-}
-
-template <uint32_t kH>
-__device__ __forceinline__ void k1_drain5(const K1Ctx& x, const K1Out5& o, K1Stream& t, OutBuf& ob) {
-  for (uint32_t i = 0; i < ob.n; ++i) {
-    const uint32_t e = ob.p[i * ob.stride];
-    k1_out5<kH>(x, o, t, e & 0xffffu, t.emit + (e >> 16));
-  }
-  ob.n = 0;
-}
-
-// LDS layout of v5: [0, 256) class map (merged class * 2), [256, ...) table
-constexpr uint32_t kTabOff5 = 256;
-__device__ __forceinline__ uint32_t k1_step5(uint32_t s, uint32_t c2) { return k1_lds16((s << 2) + c2 + kTabOff5); }
-
-// One 16-byte word with file-boundary and range-end checks (rare lines).
-template <uint32_t kH>
-__device__ __forceinline__ void k1_word_slow5(const K1Ctx& x, const K1Out5& o, K1Stream& t, const uint32_t w[4]) {
-  const unsigned long long end = t.end;
-  unsigned long long fend = x.offsets[t.f + 1];
-  if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
-  for (int k = 0; k < 16; ++k) {
-    const unsigned long long q = t.p + k;
-    if (q >= end) break;
-    if (q >= fend) {
-      flush_kw(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
-      do { ++t.f; fend = x.offsets[t.f + 1]; } while (q >= fend);
-      t.s = 0;
-      t.p12 = 0;
-    }
-    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-    t.s = k1_step5(t.s, k1_lds8(b));
-    if (q >= t.emit) {
-      t.nl += (b == 0x0au);
-      if (t.s >= x.first_out) k1_out5<kH>(x, o, t, t.s, q);
-    }
-    t.p12 = ((t.p12 << 8) & 0xff00u) | b;
-  }
-  t.p += 16;
-  t.lim = min(end, fend);
-}
-
-__device__ __forceinline__ void k1_park5(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t st, uint32_t k,
-                                         bool* full) {
-  if (ob.n < kOutSlots) {
-    ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k - t.emit) << 16) | st;
-    ++ob.n;
-  } else {
-    *full = true;
-  }
-}
-
-template <uint32_t kH>
-__device__ __forceinline__ void k1_word5(const K1Ctx& x, const K1Out5& o, K1Stream& t, OutBuf& ob, uint32_t w0,
-                                         uint32_t w1, uint32_t w2, uint32_t w3) {
-  const bool emit = t.p >= t.emit;
-  const uint32_t w[4] = {w0, w1, w2, w3};
-  uint32_t s = t.s;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    uint32_t c2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c2[k] = k1_lds8((w[2 * h + (k >> 2)] >> ((k & 3) * 8)) & 0xffu);
-    const uint32_t s0 = s;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s = k1_step5(s, c2[k]);
-      mx = max(mx, s);
-    }
-    if (emit && mx >= x.first_out) {
-      // rare: walk the half again from its start state and park (or, with the
-      // slots full, handle) every output position
-      uint32_t r = s0;
-      for (int k = 0; k < 8; ++k) {
-        r = k1_step5(r, c2[k]);
-        if (r >= x.first_out) {
-          bool full = false;
-          k1_park5(x, t, ob, r, 8 * h + k, &full);
-          if (full) k1_out5<kH>(x, o, t, r, t.p + 8 * h + k);
-        }
-      }
-    }
-  }
-  t.s = s;
-  if (emit) {
-    uint32_t u[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t xx = w[j] ^ 0x0a0a0a0au;
-      u[j] = ((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu;   // bit 7 of a byte: not '\n'
-    }
-    t.nl += 128u - (__popc(u[0]) + __popc(u[1]) + __popc(u[2]) + __popc(u[3]));
-  }
-  t.p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
-  t.p += 16;
-}
-
-// kWpe: waves per SIMD the register budget is sized for (8: two 1024-thread
-// workgroups per CU, <= 64 VGPRs; 4: one); kW: 16-byte words per register
-// line; kH: per-wave LDS hit buffer entries.
-template <int kWpe, int kW, uint32_t kH>
-__global__ __attribute__((amdgpu_flat_work_group_size(1024, 1024), amdgpu_waves_per_eu(kWpe, kWpe)))
-void tsg_k1_scan_v5(
-    const uint8_t* __restrict__ data, unsigned long long total,
-    const uint64_t* __restrict__ offsets, uint32_t nfiles,
-    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls, uint32_t table_bytes, uint32_t first_out,
-    const OutMeta* __restrict__ g_meta, const uint16_t* __restrict__ g_oidx, const uint32_t* __restrict__ g_list,
-    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
-    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
-    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
-    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
-    uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr uint32_t kThreads = 1024, kWaves = kThreads / 64;
-  constexpr uint32_t kL = kW * 16;
-  if (!k1_lds_base_ok(smem)) {                   // the integer LDS addresses assume a zero base
-    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
-    return;
-  }
-  const uint32_t padded = (table_bytes + 15) & ~15u;
-  const uint32_t hits_off = kTabOff5 + padded;
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
-  uint32_t* s_hitcnt = s_hits + kWaves * kH;
-  uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_block[0] = 0;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(g_next);
-    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff5);
-    for (uint32_t i = threadIdx.x; i < padded / 16; i += kThreads) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += kThreads) smem[i] = g_cls[i];
-  }
-  K1Ctx x;
-  x.data = data; x.total = total; x.chunk = chunk;
-  x.offsets = offsets; x.nfiles = nfiles;
-  x.next = nullptr; x.cls = smem;
-  x.first_out = first_out; x.nclasses = 0;
-  x.meta = g_meta;
-  x.list = g_list;
-  x.nkw = nkw;
-  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
-  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
-  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
-  x.w_hits = s_hits + wid * kH; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
-  const K1Out5 o{g_oidx};
-  __syncthreads();
-  // v3's guided schedule (4-, then 2-, then 1-chunk ranges per lane)
-  const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
-  const unsigned long long n1 = min(nchunks, W * 64 * tail_rounds);
-  const unsigned long long n2 = min(nchunks - n1, W * 128 * tail_rounds);
-  const unsigned long long n4 = nchunks - n1 - n2;
-  const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
-  const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
-  for (;;) {
-    unsigned long long item = 0;
-    if (lane == 0) {
-      item = atomicAdd(item_ctr, 1u);
-      *x.w_hitcnt = 0;
-    }
-    item = __shfl(item, 0);
-    if (item >= nitems) break;                                 // wave-uniform exit
-    __builtin_amdgcn_wave_barrier();
-    unsigned long long c0, rend;
-    uint32_t kU;
-    if (item < i4) { kU = 4; c0 = item * 256; rend = n4; }
-    else if (item < i4 + i2) { kU = 2; c0 = n4 + (item - i4) * 128; rend = n4 + n2; }
-    else { kU = 1; c0 = n4 + n2 + (item - i4 - i2) * 64; rend = nchunks; }
-    x.item_base = c0 * static_cast<unsigned long long>(chunk);
-    const unsigned long long c = c0 + lane * kU;
-    if (c < rend) {
-      K1Stream t;
-      k1_init(x, t, min(c * chunk, total), warm_lines * kL);
-      t.end = min(min(c + kU, rend) * chunk, total);
-      t.cend = min(t.emit + chunk, t.end);
-      t.ci = c;
-      if (t.p < t.end) t.lim = min(t.end, x.offsets[t.f + 1]);
-      OutBuf ob{obuf + blockIdx.x * kThreads + threadIdx.x, gridDim.x * kThreads, 0};
-      v4u cur[kW], nxt[kW];
-      bool have = false;
-      for (;;) {
-        if (!(t.p < t.lim || t.p < t.end)) break;
-        if (t.p >= t.cend && t.cend < t.end) {                // a chunk of the range is done
-          if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
-          t.nl = 0;
-          ++t.ci;
-          t.cend = min(t.cend + chunk, t.end);
-        }
-        if (t.p + kL <= t.lim) {
-          if (!have) {
-#pragma unroll
-            for (int i = 0; i < kW; ++i) cur[i] = *reinterpret_cast<const v4u*>(data + t.p + 16 * i);
-          }
-          have = t.p + 2 * kL <= t.lim;
-          if (have) {
-#pragma unroll
-            for (int i = 0; i < kW; ++i) nxt[i] = *reinterpret_cast<const v4u*>(data + t.p + kL + 16 * i);
-          }
-          if (x.primary) {
-            uint32_t hb = 0;
-#pragma unroll
-            for (int i = 0; i < kW; ++i) hb |= cur[i].x | cur[i].y | cur[i].z | cur[i].w;
-            if ((hb & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
-          }
-#pragma unroll 1
-          for (int i = 0; i < kW; ++i) k1_word5<kH>(x, o, t, ob, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
-          if (have) {
-#pragma unroll
-            for (int i = 0; i < kW; ++i) cur[i] = nxt[i];
-          }
-        } else {
-          // a line with a file boundary or the range end (rare): word by word
-          have = false;
-          k1_drain5<kH>(x, o, t, ob);                        // parked outputs belong to file t.f
-          for (int i = 0; i < kW && t.p < t.end; ++i) {
-            if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
-              if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
-              t.nl = 0;
-              ++t.ci;
-              t.cend = min(t.cend + chunk, t.end);
-            }
-            const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            k1_word_slow5<kH>(x, o, t, w);
-          }
-        }
-      }
-      k1_drain5<kH>(x, o, t, ob);
-      flush_kw(x.kwmask, kw_words, t.f, t.kw0, t.kw1);
-      if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);   // the range's last chunk
-    }
-    // flush this wave's hit buffer (the wave has reconverged here)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t n = min(*x.w_hitcnt, kH);
-    uint32_t b0 = 0, o0 = 0;
-    if (lane == 0 && n) {
-      b0 = atomicAdd(x.b_hitcnt, n);
-      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
-    }
-    b0 = __shfl(b0, 0);
-    o0 = __shfl(o0, 0);
-    const uint32_t spill_from = max(b0, region_cap);
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t h = x.w_hits[i];
-      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
-      if (b0 + i < region_cap) {
-        x.hits[b0 + i] = v;
-      } else {
-        const uint32_t oi = o0 + (b0 + i - spill_from);
-        if (oi < x.over_cap) x.over[oi] = v;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
-}
-
-// K1 v6: v5's compact table at two 1024-thread workgroups per CU with the
-// per-lane state cut to fit 64 VGPRs without spilling: positions are 32-bit
-// offsets from the lane's first byte, one 64-byte register line (no double
-// buffer: with 8 waves per SIMD other waves cover a line's load), the
-// deferred-output slot count as the only per-lane output state, and the
-// uniform context in scalar registers.
-struct K1LeanCtx {
-  const uint8_t* __restrict__ data;
-  const uint64_t* __restrict__ offsets;
-  uint32_t nfiles, first_out, nkw, kw_words, region_cap, over_cap, ob_stride;
-  bool primary;
-  const OutMeta* __restrict__ meta;
-  const uint16_t* __restrict__ oidx;
-  const uint32_t* __restrict__ list;
-  uint32_t* __restrict__ kwbits;
-  uint32_t* __restrict__ kwmask;
-  unsigned long long* __restrict__ hits;
-  unsigned long long* __restrict__ over;
-  uint32_t* over_cnt;
-  uint32_t* b_hitcnt;
-  uint32_t* w_hits;
-  uint32_t* w_hitcnt;
-  uint32_t* __restrict__ fflags;
-  uint32_t* __restrict__ ob;      // this lane's first deferred-output slot
-  unsigned long long item_base;
-};
-
-struct K1Lean {
-  unsigned long long base;        // absolute position of offset 0 (the warm-up start)
-  uint32_t p, lim, end, emit, cend, ci;
-  uint32_t f, s, p12, nl, obn;
-};
-
-template <uint32_t kH>
-__device__ __forceinline__ void k1_lean_out(const K1LeanCtx& x, K1Lean& t, uint32_t st, unsigned long long q) {
-  const OutMeta m = x.meta[x.oidx[st - x.first_out]];
-  // keyword masks straight to the file's bits (outputs are rare; no register masks)
-  uint32_t* w = x.kwmask + static_cast<size_t>(t.f) * x.kw_words;
-  or_bits(w + 0, static_cast<uint32_t>(m.kw0));
-  or_bits(w + 1, static_cast<uint32_t>(m.kw0 >> 32));
-  or_bits(w + 2, static_cast<uint32_t>(m.kw1));
-  or_bits(w + 3, static_cast<uint32_t>(m.kw1 >> 32));
-  for (uint32_t j = 0; j < m.list_count; ++j) {
-    const uint32_t id = x.list[m.list_begin + j];
-    if (id < x.nkw) {
-      atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
-      continue;
-    }
-    const uint32_t li = atomicAdd(x.w_hitcnt, 1u);
-    if (li < kH) {
-      x.w_hits[li] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
-    } else {
-      const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
-      if (gi < x.region_cap) {
-        x.hits[gi] = (q << 24) | (id - x.nkw);
-      } else {
-        const uint32_t oi = atomicAdd(x.over_cnt, 1u);
-        if (oi < x.over_cap) x.over[oi] = (q << 24) | (id - x.nkw);
-      }
-    }
-  }
-}
-
-template <uint32_t kH>
-__device__ __forceinline__ void k1_lean_drain(const K1LeanCtx& x, K1Lean& t) {
-  for (uint32_t i = 0; i < t.obn; ++i) {
-    const uint32_t e = x.ob[i * x.ob_stride];
-    k1_lean_out<kH>(x, t, e & 0xffffu, t.base + t.emit + (e >> 16));
-  }
-  t.obn = 0;
-}
-
-// a word with file-boundary and range-end checks (rare)
-template <uint32_t kH>
-__device__ __forceinline__ void k1_lean_slow(const K1LeanCtx& x, K1Lean& t, v4u v) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t fend = static_cast<uint32_t>(min(x.offsets[t.f + 1] - t.base, 0xffffffffull));
-  const bool special = x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit;
-  uint32_t a = t.p12 & 0xffu, bb = t.p12 >> 8;
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t q = t.p + k;
-    if (q >= t.end) break;
-    if (q >= fend) {
-      do { ++t.f; fend = static_cast<uint32_t>(min(x.offsets[t.f + 1] - t.base, 0xffffffffull)); } while (q >= fend);
-      t.s = 0;
-      t.p12 = 0;
-      a = bb = 0;
-    }
-    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-    if (special && ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)))
-      atomicOr(&x.fflags[t.f], 1u);
-    bb = a;
-    a = b;
-    t.s = k1_step5(t.s, k1_lds8(b));
-    if (q >= t.emit) {
-      t.nl += (b == 0x0au);
-      if (t.s >= x.first_out) k1_lean_out<kH>(x, t, t.s, t.base + q);
-    }
-    t.p12 = ((t.p12 << 8) & 0xff00u) | b;
-  }
-  t.p += 16;
-  t.lim = min(t.end, fend);
-}
-
-template <uint32_t kH, int kG>
-__device__ __forceinline__ void k1_lean_word(const K1LeanCtx& x, K1Lean& t, v4u v) {
-  const bool emit = t.p >= t.emit;
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t s = t.s;
-  // groups of kG bytes: kG class reads in flight, then kG dependent transitions
-#pragma unroll
-  for (int h = 0; h < 16 / kG; ++h) {
-    uint32_t c2[kG];
-#pragma unroll
-    for (int k = 0; k < kG; ++k) {
-      const int j = kG * h + k;
-      c2[k] = k1_lds8((w[j >> 2] >> ((j & 3) * 8)) & 0xffu);
-    }
-    const uint32_t s0 = s;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < kG; ++k) {
-      s = k1_step5(s, c2[k]);
-      mx = max(mx, s);
-    }
-    if (emit && mx >= x.first_out) {
-      uint32_t r = s0;
-      for (int k = 0; k < kG; ++k) {
-        r = k1_step5(r, c2[k]);
-        if (r >= x.first_out) {
-          if (t.obn < kOutSlots) {
-            x.ob[t.obn * x.ob_stride] = ((t.p + kG * h + k - t.emit) << 16) | r;
-            ++t.obn;
-          } else {
-            k1_lean_out<kH>(x, t, r, t.base + t.p + kG * h + k);
-          }
-        }
-      }
-    }
-  }
-  t.s = s;
-  if (emit) {
-    uint32_t u = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t xx = w[j] ^ 0x0a0a0a0au;
-      u += __popc(((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu);   // bit 7 set: not '\n'
-    }
-    t.nl += 128u - u;
-  }
-  t.p12 = (w[3] >> 24) | ((w[3] >> 8) & 0xff00u);
-  t.p += 16;
-}
-
-template <uint32_t kH, int kG>
-__global__ __attribute__((amdgpu_flat_work_group_size(1024, 1024), amdgpu_waves_per_eu(8, 8)))
-void tsg_k1_scan_v6(
-    const uint8_t* __restrict__ data, unsigned long long total,
-    const uint64_t* __restrict__ offsets, uint32_t nfiles,
-    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls, uint32_t table_bytes, uint32_t first_out,
-    const OutMeta* __restrict__ g_meta, const uint16_t* __restrict__ g_oidx, const uint32_t* __restrict__ g_list,
-    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
-    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
-    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
-    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
-    uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr uint32_t kThreads = 1024, kWaves = kThreads / 64, kL = 64;
-  if (!k1_lds_base_ok(smem)) {
-    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
-    return;
-  }
-  const uint32_t padded = (table_bytes + 15) & ~15u;
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + kTabOff5 + padded);
-  uint32_t* s_hitcnt = s_hits + kWaves * kH;
-  uint32_t* s_block = s_hitcnt + kMaxWaves;
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_block[0] = 0;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(g_next);
-    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff5);
-    for (uint32_t i = threadIdx.x; i < padded / 16; i += kThreads) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += kThreads) smem[i] = g_cls[i];
-  }
-  K1LeanCtx x;
-  x.data = data; x.offsets = offsets; x.nfiles = nfiles; x.first_out = first_out; x.nkw = nkw;
-  x.kw_words = kw_words; x.region_cap = region_cap; x.over_cap = over_cap; x.ob_stride = gridDim.x * kThreads;
-  x.primary = primary != 0;
-  x.meta = g_meta; x.oidx = g_oidx; x.list = g_list;
-  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32;
-  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.over = over; x.over_cnt = over_cnt;
-  x.b_hitcnt = s_block; x.w_hits = s_hits + wid * kH; x.w_hitcnt = s_hitcnt + wid;
-  x.fflags = fflags; x.ob = obuf + blockIdx.x * kThreads + threadIdx.x;
-  __syncthreads();
-  const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
-  const unsigned long long n1 = min(nchunks, W * 64 * tail_rounds);
-  const unsigned long long n2 = min(nchunks - n1, W * 128 * tail_rounds);
-  const unsigned long long n4 = nchunks - n1 - n2;
-  const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
-  const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
-  const uint32_t warm = warm_lines * kL;
-  for (;;) {
-    unsigned long long item = 0;
-    if (lane == 0) {
-      item = atomicAdd(item_ctr, 1u);
-      *x.w_hitcnt = 0;
-    }
-    item = __shfl(item, 0);
-    if (item >= nitems) break;
-    __builtin_amdgcn_wave_barrier();
-    unsigned long long c0, rend;
-    uint32_t kU;
-    if (item < i4) { kU = 4; c0 = item * 256; rend = n4; }
-    else if (item < i4 + i2) { kU = 2; c0 = n4 + (item - i4) * 128; rend = n4 + n2; }
-    else { kU = 1; c0 = n4 + n2 + (item - i4 - i2) * 64; rend = nchunks; }
-    x.item_base = c0 * static_cast<unsigned long long>(chunk);
-    const unsigned long long c = c0 + lane * kU;
-    if (c < rend) {
-      K1Lean t;
-      const unsigned long long start = min(c * chunk, total);
-      t.base = start > warm ? start - warm : 0;
-      t.p = 0;
-      t.emit = static_cast<uint32_t>(start - t.base);
-      t.end = static_cast<uint32_t>(min(min(c + kU, rend) * chunk, total) - t.base);
-      t.cend = min(t.emit + chunk, t.end);
-      t.ci = static_cast<uint32_t>(c);
-      t.s = 0; t.p12 = 0; t.nl = 0; t.obn = 0;
-      t.f = file_of(offsets, nfiles, t.base);
-      t.lim = static_cast<uint32_t>(min(static_cast<unsigned long long>(t.end), offsets[t.f + 1] - t.base));
-      while (t.p < t.end) {
-        if (t.p >= t.cend && t.cend < t.end) {                // a chunk of the range is done
-          if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
-          t.nl = 0;
-          ++t.ci;
-          t.cend = min(t.cend + chunk, t.end);
-        }
-        const uint8_t* lp = data + t.base + t.p;
-        if (t.p + kL <= t.lim) {
-          v4u line[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) line[i] = *reinterpret_cast<const v4u*>(lp + 16 * i);
-          if (x.primary) {
-            uint32_t hb = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) hb |= line[i].x | line[i].y | line[i].z | line[i].w;
-            if ((hb & 0x80808080u) && k1_line_special(lp, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) k1_lean_word<kH, kG>(x, t, line[i]);
-        } else {
-          k1_lean_drain<kH>(x, t);                           // parked outputs belong to file t.f
-          for (int i = 0; i < 4 && t.p < t.end; ++i) {
-            if (t.p >= t.cend && t.cend < t.end) {
-              if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
-              t.nl = 0;
-              ++t.ci;
-              t.cend = min(t.cend + chunk, t.end);
-            }
-            k1_lean_slow<kH>(x, t, *reinterpret_cast<const v4u*>(data + t.base + t.p));
-          }
-        }
-      }
-      k1_lean_drain<kH>(x, t);
-      if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t n = min(*x.w_hitcnt, kH);
-    uint32_t b0 = 0, o0 = 0;
-    if (lane == 0 && n) {
-      b0 = atomicAdd(x.b_hitcnt, n);
-      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
-    }
-    b0 = __shfl(b0, 0);
-    o0 = __shfl(o0, 0);
-    const uint32_t spill_from = max(b0, region_cap);
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t h = x.w_hits[i];
-      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
-      if (b0 + i < region_cap) {
-        x.hits[b0 + i] = v;
-      } else {
-        const uint32_t oi = o0 + (b0 + i - spill_from);
-        if (oi < x.over_cap) x.over[oi] = v;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
-}
-
-// K1 v4: v3's per-byte work on TWO streams per lane.  v3's transition chain
-// is one dependent LDS round trip per byte per lane (measured: the no-HBM
-// build runs at 3.3 TB/s against 3.0 with HBM, so K1 is bound by that chain,
-// not by memory); v4 walks the lane's two adjacent chunks (2c, 2c + 1) with
-// their chains interleaved, so two transitions are in flight per lane.
-//  * a wave item is 64 lanes x 2 chunks; the hit record's item offset spans
-//    128 x chunk bytes (k1_max_chunk(2));
-//  * the transition address is one v_lshl_add_u32 ((s << 1) + c2) feeding a
-//    ds_read_u16 with the table's offset as its immediate: the table is read
-//    through an LDS-address-space pointer built from that integer, which
-//    requires the kernel's dynamic LDS to start at address 0 (no static LDS;
-//    checked at run time, the kernel reports a mismatch instead of reading);
-//  * output states are checked per 8 bytes (max of 8 states) and parked in
-//    the stream's deferred-output slots as in v3;
-//  * lines of one stream with a file boundary or chunk end, and the tail of
-//    a stream once the other has finished, take v3's single-stream code.
-constexpr uint32_t kOutDrainV4 = 8, kOutSlotsV4 = kOutDrainV4 + 64;   // per stream
-
-// park the outputs among 4 consecutive states of a stream in its slots (a
-// line adds at most 64; the slots are drained after any line that leaves
-// more than kOutDrainV4 parked, so kOutSlotsV4 never overflows); t.p is the
-// word's first byte, k0 the first state's byte in it.  No output is handled
-// inside the word loop: the handling code (k1_out_v3) exists only at the
-// few drain sites, which keeps the hot loop small in the instruction cache.
-__device__ __forceinline__ void k1_v4_outs(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t S, const uint32_t st[4],
-                                           int k0) {
-  if (max(max(st[0], st[1]), max(st[2], st[3])) >= x.first_out) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (st[k] >= x.first_out) {
-        ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k0 + k - t.emit) << 16) | st[k];
-        ++ob.n;
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t k1_nl_word(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-  const uint32_t w[4] = {w0, w1, w2, w3};
-  uint32_t n = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t xx = w[j] ^ 0x0a0a0a0au;
-    n += __popc(((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu);   // bit 7 of a byte: not '\n'
-  }
-  return 128u - n;
-}
-
-// one 16-byte word of each of two streams, chains interleaved
-__device__ __forceinline__ void k1_v4_pair(const K1Ctx& x, K1Stream& a, K1Stream& b, OutBuf& oa, OutBuf& ob, uint32_t S,
-                                           v4u wa, v4u wb) {
-  constexpr uint32_t kTabOff = 256;
-  const uint32_t A[4] = {wa.x, wa.y, wa.z, wa.w}, B[4] = {wb.x, wb.y, wb.z, wb.w};
-  const bool ea = a.p >= a.emit, eb = b.p >= b.emit;
-  uint32_t sa = a.s, sb = b.s;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {              // dword h of each word: bounded live ranges
-    uint32_t ca[4], cb[4], ta[4], tb[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      ca[k] = k1_lds8((A[h] >> (k * 8)) & 0xffu);
-      cb[k] = k1_lds8((B[h] >> (k * 8)) & 0xffu);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      sa = k1_lds16((sa << 1) + ca[k] + kTabOff);
-      sb = k1_lds16((sb << 1) + cb[k] + kTabOff);
-      ta[k] = sa;
-      tb[k] = sb;
-    }
-    if (ea) k1_v4_outs(x, a, oa, S, ta, 4 * h);
-    if (eb) k1_v4_outs(x, b, ob, S, tb, 4 * h);
-  }
-  a.s = sa;
-  b.s = sb;
-  if (ea) a.nl += k1_nl_word(A[0], A[1], A[2], A[3]);
-  if (eb) b.nl += k1_nl_word(B[0], B[1], B[2], B[3]);
-  a.p12 = (A[3] >> 24) | ((A[3] >> 8) & 0xff00u);
-  b.p12 = (B[3] >> 24) | ((B[3] >> 8) & 0xff00u);
-  a.p += 16;
-  b.p += 16;
-}
-
-// one 16-byte word of one stream (v4's layout, 4-byte output groups)
-__device__ __forceinline__ void k1_v4_single(const K1Ctx& x, K1Stream& a, OutBuf& oa, uint32_t S, v4u wa) {
-  constexpr uint32_t kTabOff = 256;
-  const uint32_t A[4] = {wa.x, wa.y, wa.z, wa.w};
-  const bool ea = a.p >= a.emit;
-  uint32_t sa = a.s;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    uint32_t ca[4], ta[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ca[k] = k1_lds8((A[h] >> (k * 8)) & 0xffu);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      sa = k1_lds16((sa << 1) + ca[k] + kTabOff);
-      ta[k] = sa;
-    }
-    if (ea) k1_v4_outs(x, a, oa, S, ta, 4 * h);
-  }
-  a.s = sa;
-  if (ea) a.nl += k1_nl_word(A[0], A[1], A[2], A[3]);
-  a.p12 = (A[3] >> 24) | ((A[3] >> 8) & 0xff00u);
-  a.p += 16;
-}
-
-template <int kThreads>
-__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v4(
-    const uint8_t* __restrict__ data, unsigned long long total,
-    const uint64_t* __restrict__ offsets, uint32_t nfiles,
-    const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
-    uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
-    const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
-    uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
-    uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
-    unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
-    unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
-    uint32_t* __restrict__ obuf, uint32_t /*tail_rounds: v3*/) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int kAbl = kAblTemporal | kAblLine64 | kAblDefer;   // v3's single-stream code for the odd lines
-  constexpr uint32_t kWaves = kThreads / 64;
-  constexpr uint32_t kTabOff = 256;
-  constexpr int kW = 4;                          // 16-byte words per 64-byte line
-  constexpr uint32_t kL = kW * 16;
-  if (!k1_lds_base_ok(smem)) {                   // the integer LDS addresses assume a zero base
-    if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
-    return;
-  }
-  const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
-  const uint32_t list_off = kTabOff + padded;
-  const uint32_t hits_off = (list_off + nlist * 4 + 15) & ~15u;
-  uint32_t S = (nclasses + 2) & ~1u;             // k1_row_stride(nclasses): the silent-row stride
-  if (((S / 2) & 1u) == 0) S += 2;
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
-  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
-  uint32_t* s_block = s_hitcnt + kMaxWaves;
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_block[0] = 0;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(g_next);
-    uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff);
-    for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[i] = g_cls[i];
-    uint32_t* s_list = reinterpret_cast<uint32_t*>(smem + list_off);
-    for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
-  }
-  K1Ctx x;
-  x.data = data; x.total = total; x.chunk = chunk;
-  x.offsets = offsets; x.nfiles = nfiles;
-  x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
-  x.cls = smem;
-  x.first_out = first_out; x.nclasses = nclasses;
-  x.meta = nullptr;
-  x.list = reinterpret_cast<const uint32_t*>(smem + list_off);
-  x.nkw = nkw;
-  x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
-  x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
-  x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
-  x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
-  __syncthreads();
-  const unsigned long long nitems = (nchunks + 127) / 128;      // wave work items (64 lanes x 2 chunks)
-  const uint32_t nthreads = gridDim.x * kThreads;
-  for (;;) {
-    unsigned long long item = 0;
-    if (lane == 0) {
-      item = atomicAdd(item_ctr, 1u);
-      *x.w_hitcnt = 0;
-    }
-    item = __shfl(item, 0);
-    if (item >= nitems) break;                                 // wave-uniform exit
-    __builtin_amdgcn_wave_barrier();
-    x.item_base = item * 128 * static_cast<unsigned long long>(chunk);
-    const unsigned long long ca = item * 128 + 2 * lane;       // stream a's chunk; b's is ca + 1
-    if (ca < nchunks) {
-      K1Stream ta, tb;
-      k1_init(x, ta, min(ca * chunk, total), warm_lines * 128u);
-      k1_init(x, tb, min((ca + 1) * chunk, total), warm_lines * 128u);
-      OutBuf oa{obuf + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
-      OutBuf ob{obuf + static_cast<size_t>(nthreads) * kOutSlotsV4 + blockIdx.x * kThreads + threadIdx.x, nthreads, 0};
-      v4u la[kW], lb[kW];
-      bool ha = false, hb = false;                               // la / lb hold the line at t.p
-      // one stream's line holds a file boundary or its chunk end: word by
-      // word (its parked outputs belong to its current file: handle them
-      // first)
-      auto slow_line = [&](K1Stream& t, OutBuf& o) {
-        k1_drain(x, t, o, S);
-        for (int i = 0; i < kW && t.p < k1_end(x, t); ++i) {
-          const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
-          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-          k1_word_slow<true>(x, t, w, S);
-        }
-      };
-      // the other stream has finished: one stream's fast line
-      auto single_line = [&](K1Stream& t, OutBuf& o, v4u (&l)[kW], bool& h) {
-        if (!h) {
-#pragma unroll
-          for (int i = 0; i < kW; ++i) l[i] = k1_load<kAbl>(data, t.p + 16 * i);
-        }
-        if (x.primary) {
-          uint32_t m = 0;
-#pragma unroll
-          for (int i = 0; i < kW; ++i) m |= l[i].x | l[i].y | l[i].z | l[i].w;
-          if ((m & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
-        }
-        h = t.p + 2 * kL <= t.lim;
-        const unsigned long long q = t.p + kL;
-#pragma unroll
-        for (int i = 0; i < kW; ++i) {
-          const v4u w = l[i];
-          if (h) l[i] = k1_load<kAbl>(data, q + 16 * i);
-          k1_v4_single(x, t, o, S, w);
-        }
-        if (o.n > kOutDrainV4) k1_drain(x, t, o, S);
-      };
-      for (;;) {
-        const bool ra = ta.p < ta.lim || ta.p < k1_end(x, ta);
-        const bool rb = tb.p < tb.lim || tb.p < k1_end(x, tb);
-        if (!ra && !rb) break;
-        const bool fa = ta.p + kL <= ta.lim, fb = tb.p + kL <= tb.lim;
-        if (fa && fb) {
-          if (!ha) {
-#pragma unroll
-            for (int i = 0; i < kW; ++i) la[i] = k1_load<kAbl>(data, ta.p + 16 * i);
-          }
-          if (!hb) {
-#pragma unroll
-            for (int i = 0; i < kW; ++i) lb[i] = k1_load<kAbl>(data, tb.p + 16 * i);
-          }
-          if (x.primary) {
-            uint32_t ma = 0, mb = 0;
-#pragma unroll
-            for (int i = 0; i < kW; ++i) {
-              ma |= la[i].x | la[i].y | la[i].z | la[i].w;
-              mb |= lb[i].x | lb[i].y | lb[i].z | lb[i].w;
-            }
-            if ((ma & 0x80808080u) && k1_line_special(data + ta.p, ta.p12, kL)) atomicOr(&x.fflags[ta.f], 1u);
-            if ((mb & 0x80808080u) && k1_line_special(data + tb.p, tb.p12, kL)) atomicOr(&x.fflags[tb.f], 1u);
-          }
-          // rolling prefetch: once word i is taken, word i of the next line
-          // (when that line lies inside the stream) is loaded into its slot
-          ha = ta.p + 2 * kL <= ta.lim;
-          hb = tb.p + 2 * kL <= tb.lim;
-          const unsigned long long qa = ta.p + kL, qb = tb.p + kL;
-#pragma unroll
-          for (int i = 0; i < kW; ++i) {
-            const v4u wa = la[i], wb = lb[i];
-            if (ha) la[i] = k1_load<kAbl>(data, qa + 16 * i);
-            if (hb) lb[i] = k1_load<kAbl>(data, qb + 16 * i);
-            k1_v4_pair(x, ta, tb, oa, ob, S, wa, wb);
-          }
-          if (oa.n > kOutDrainV4) k1_drain(x, ta, oa, S);
-          if (ob.n > kOutDrainV4) k1_drain(x, tb, ob, S);
-        } else if (ra && !fa) {
-          ha = false;
-          slow_line(ta, oa);
-        } else if (rb && !fb) {
-          hb = false;
-          slow_line(tb, ob);
-        } else if (fa) {
-          single_line(ta, oa, la, ha);
-        } else {
-          single_line(tb, ob, lb, hb);
-        }
-      }
-      k1_drain(x, ta, oa, S);
-      k1_drain(x, tb, ob, S);
-      flush_kw(x.kwmask, kw_words, ta.f, ta.kw0, ta.kw1);
-      flush_kw(x.kwmask, kw_words, tb.f, tb.kw0, tb.kw1);
-      if (x.primary) {
-        nl_count[ca] = static_cast<uint16_t>(ta.nl);
-        if (ca + 1 < nchunks) nl_count[ca + 1] = static_cast<uint16_t>(tb.nl);
-      }
-    }
-    // flush this wave's hit buffer (the wave has reconverged here)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t n = min(*x.w_hitcnt, kWaveHits);
-    uint32_t b0 = 0, o0 = 0;
-    if (lane == 0 && n) {
-      b0 = atomicAdd(x.b_hitcnt, n);
-      if (b0 + n > region_cap) o0 = atomicAdd(x.over_cnt, b0 + n - max(b0, region_cap));
-    }
-    b0 = __shfl(b0, 0);
-    o0 = __shfl(o0, 0);
-    const uint32_t spill_from = max(b0, region_cap);
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t h = x.w_hits[i];
-      const unsigned long long v = ((x.item_base + (h >> kAnchorBits)) << 24) | (h & ((1u << kAnchorBits) - 1));
-      if (b0 + i < region_cap) {
-        x.hits[b0 + i] = v;
-      } else {
-        const uint32_t oi = o0 + (b0 + i - spill_from);
-        if (oi < x.over_cap) x.over[oi] = v;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
-}
-
-// K1 instantiations: (workgroup size, interleaved streams per lane)
-template <bool kLds>
-const void* k1_kernel_t(uint32_t threads, int ks) {
-  if (threads == 1024 && ks == 1) return reinterpret_cast<const void*>(&tsg_k1_scan<kLds, 1, 1024>);
-  if (threads == 512 && ks == 2) return reinterpret_cast<const void*>(&tsg_k1_scan<kLds, 2, 512>);
-  return nullptr;
-}
-
-// variant 3 (tsg_k1_scan_v3) needs the table in LDS, 1024 threads, one stream
-// per lane; `abl` selects a measurement build (kAbl*)
-const void* k1_kernel(bool lds, uint32_t threads, int ks, int variant = 1, int abl = 0) {
-  if (variant == 4) {
-    if (!lds || ks != 1) return nullptr;
-    if (threads == 1024) return reinterpret_cast<const void*>(&tsg_k1_scan_v4<1024>);
-    if (threads == 512) return reinterpret_cast<const void*>(&tsg_k1_scan_v4<512>);
-    return nullptr;
-  }
-  if (variant == 3) {
-    if (!lds || threads != 1024 || ks != 1) return nullptr;
-    switch (abl) {
+// K1 builds: the default (464) and the measurement builds kept for the
+// DESIGN.md 4.1 ablations (kAbl bits; tools/k1_probe.py --variants 3:ABL)
+const void* k1_kernel(int abl) {
+  switch (abl) {
 #define TSG_K1_V3(A) case (A): return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, (A)>);
-      TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(17) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(26) TSG_K1_V3(27)
-      TSG_K1_V3(31) TSG_K1_V3(32) TSG_K1_V3(48)
-      TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(82) TSG_K1_V3(146) TSG_K1_V3(210) TSG_K1_V3(112) TSG_K1_V3(240)
-      TSG_K1_V3(272) TSG_K1_V3(336) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466)
-      TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(912) TSG_K1_V3(784)
-      TSG_K1_V3(1488) TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(2192)
+    TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(32) TSG_K1_V3(48)
+    TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464)
+    TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
+    TSG_K1_V3(2448) TSG_K1_V3(2512)
 #undef TSG_K1_V3
-      default: return nullptr;
-    }
+    default: return nullptr;
   }
-  return lds ? k1_kernel_t<true>(threads, ks) : k1_kernel_t<false>(threads, ks);
 }
 
 template <typename T>
@@ -1892,36 +730,11 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
   return true;
 }
 
-// v5 LDS bytes: class map + table + per-wave hit buffers + counters
-constexpr uint32_t kK1HitsDual = 64, kK1HitsSingle = 512;
-constexpr uint32_t k1_lds5(uint32_t table_bytes, uint32_t hits) {
-  return kTabOff5 + ((table_bytes + 15) & ~15u) + 16 * hits * 4 + kMaxWaves * 4 + 16;
-}
-
-// v5 instantiations: dual (two workgroups per CU, 8 waves per SIMD) with
-// 64- or 32-byte register lines, or single (one workgroup per CU)
-const void* k1_kernel5(bool dual, int line_words) {
-  if (dual) {
-    if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v6<kK1HitsDual, 4>);
-    return reinterpret_cast<const void*>(&tsg_k1_scan_v6<kK1HitsDual, 8>);
-  }
-  if (line_words == 2) return reinterpret_cast<const void*>(&tsg_k1_scan_v5<4, 2, kK1HitsSingle>);
-  return reinterpret_cast<const void*>(&tsg_k1_scan_v5<4, 4, kK1HitsSingle>);
-}
-
-// Default K1 chunk for a launch of `bytes`: about a million lane chunks per
-// launch, 1-4 KiB.  Measured on MI355X (r2g, v3 K1): a 1 GB launch 0.52 ms
-// at 1 KiB vs 0.56 at 4 KiB (shorter wave items, shorter tail); 2 GB best at
-// 2 KiB; 4 GB and more best at 4 KiB (less warm-up per byte).
-// v3 walks ranges of 1-4 chunks per lane (guided schedule): its chunk is
-// the '\n'-count granularity and the last round's range: 2 KiB for launches
-// of 2 GiB and more (measured r2r: 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB.
-uint32_t k1_chunk_for(uint64_t bytes, int variant) {
-  if (variant == 3 || variant == 5) return bytes >= (2ull << 30) ? 2048 : 1024;
-  uint32_t c = 1024;
-  while (c < 4096 && static_cast<uint64_t>(c) * (1u << 20) < bytes) c <<= 1;
-  return c;
-}
+// Default K1 chunk for a launch of `bytes`.  K1 walks ranges of 1-4 chunks
+// per lane (guided schedule): its chunk is the '\n'-count granularity and the
+// last round's range: 2 KiB for launches of 2 GiB and more (measured r2r:
+// 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB.
+uint32_t k1_chunk_for(uint64_t bytes) { return bytes >= (2ull << 30) ? 2048 : 1024; }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1939,12 +752,6 @@ struct K1Group {
   uint32_t kw_base = 0, warm_lines = 0, warm_lines64 = 0;
   size_t meta_bytes = 0;
   bool in_lds = false;
-  // v5 compact layout: merged classes, rows of row5 dwords, dword offsets
-  uint16_t* next5 = nullptr;
-  uint8_t* cls5 = nullptr;
-  uint16_t* oidx5 = nullptr;   // row - first_out5 -> output-state index
-  uint32_t table5_bytes = 0, first_out5 = 0, nclasses5 = 0, row5 = 0, max_pattern = 0;
-  bool dual5 = false;          // class map + table + kK1HitsDual hit buffers fit half a CU's LDS
 };
 
 // The compiled rule tables on one device plus that device's pool of lanes.
@@ -2022,7 +829,7 @@ DeviceTables::~DeviceTables() {
   void* ps[] = {anchors, rules, rule_kw, vdfa, v_next, v_acc, v_cls};
   for (void* p : ps) if (p) hipFree(p);
   for (K1Group& g : k1g) {
-    void* gs[] = {g.next, g.cls, g.meta, g.list, g.next5, g.cls5, g.oidx5};
+    void* gs[] = {g.next, g.cls, g.meta, g.list};
     for (void* p : gs) if (p) hipFree(p);
   }
 }
@@ -2063,7 +870,7 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     // the same class of different states over different LDS banks (a 64-class
     // row is 32 dwords, which would put every state's class c in one bank).
     // Silent rows first (stride S), then output rows (stride So): slot C of an
-    // output row holds the output-state index (K1 v1's meta lookup), slots
+    // output row holds the output-state index (kept for the layout), slots
     // S..S+9 its metadata inline (v3: keyword masks and list in the same LDS
     // round trip as the row address)
     const uint32_t C = sd.t.nclasses;
@@ -2075,7 +882,7 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     g.first_out = fo * stride;
     g.kw_base = sd.kw_base;
     const uint32_t warm = sd.max_pattern_bytes > 0 ? sd.max_pattern_bytes - 1 : 0;
-    g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk (v1, v4)
+    g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk (128-B line builds)
     g.warm_lines64 = (warm + 63) / 64;          // v3 (64-byte lines): whole 64-byte lines
     // entries hold the next state's row offset: the DFA chain is then one
     // add + one LDS read per byte (no multiply)
@@ -2127,39 +934,6 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     if (!dev_upload(sn, &g.next, err) || !dev_upload(cls, &g.cls, err) || !dev_upload(meta, &g.meta, err) ||
         !dev_upload(olist, &g.list, err)) {
       return false;
-    }
-    {
-      // v5: classes whose transition columns are identical merged (exact),
-      // rows of an odd dword count, entries = the next row's DWORD offset
-      std::map<std::vector<uint16_t>, uint32_t> colid;
-      std::vector<uint32_t> newc(C);
-      for (uint32_t c = 0; c < C; ++c) {
-        std::vector<uint16_t> col(sd.t.nstates);
-        for (uint32_t st = 0; st < sd.t.nstates; ++st) col[st] = sd.t.next[static_cast<size_t>(st) * C + c];
-        newc[c] = colid.emplace(std::move(col), static_cast<uint32_t>(colid.size())).first->second;
-      }
-      const uint32_t C5 = static_cast<uint32_t>(colid.size());
-      uint32_t cr = (C5 + 1) & ~1u;
-      if (((cr / 2) & 1u) == 0) cr += 2;
-      const uint32_t rw = cr / 2;
-      if (static_cast<uint64_t>(sd.t.nstates) * rw > 65535) { *err = "scan DFA group too large for K1 v5"; return false; }
-      std::vector<uint16_t> t5(static_cast<size_t>(sd.t.nstates) * cr, 0);
-      for (uint32_t st = 0; st < sd.t.nstates; ++st)
-        for (uint32_t c = 0; c < C; ++c)
-          t5[static_cast<size_t>(st) * cr + newc[c]] = static_cast<uint16_t>(sd.t.next[static_cast<size_t>(st) * C + c] * rw);
-      std::vector<uint16_t> oidx(std::max<size_t>(1, static_cast<size_t>(sd.t.nstates - fo) * rw), 0);
-      for (uint32_t o = 0; o < sd.t.nstates - fo; ++o) oidx[static_cast<size_t>(o) * rw] = static_cast<uint16_t>(o);
-      std::vector<uint8_t> c5(256);
-      for (int b = 0; b < 256; ++b) c5[b] = static_cast<uint8_t>(newc[sd.t.byte_class[b]] * 2);
-      g.nclasses5 = C5;
-      g.row5 = rw;
-      g.first_out5 = fo * rw;
-      g.table5_bytes = static_cast<uint32_t>(t5.size() * 2);
-      g.max_pattern = sd.max_pattern_bytes;
-      g.dual5 = k1_lds5(g.table5_bytes, kK1HitsDual) * 2 <= kLdsBytes;
-      t5.resize(((t5.size() * 2 + 15) / 16) * 8, 0);
-      if (!dev_upload(t5, &g.next5, err) || !dev_upload(c5, &g.cls5, err) || !dev_upload(oidx, &g.oidx5, err))
-        return false;
     }
     dt->kw_words = std::max<uint32_t>(dt->kw_words, g.kw_base / 32 + 4);   // a group's masks span 4 words from kw_base
     dt->k1g.push_back(g);
@@ -2288,23 +1062,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const long long v = std::atoll(c);
     if (v >= 0) e->segment_tail_ = static_cast<uint64_t>(v);
   }
-  if (const char* c = std::getenv("TSG_K1_LINE5")) {
-    const int v = std::atoi(c);
-    if (v == 2 || v == 4) e->k1_line5_ = v;
-  }
-  if (const char* c = std::getenv("TSG_K1_SINGLE5")) e->k1_single5_ = std::atoi(c) != 0;
-  if (const char* c = std::getenv("TSG_K1_VARIANT")) {
-    const int v = std::atoi(c);
-    if (v == 1 || v == 3 || v == 4 || v == 5) e->k1_variant_ = v;
-  }
-  if (const char* cfg = std::getenv("TSG_K1_CFG")) {
-    unsigned t = 0, k = 0;
-    if (std::sscanf(cfg, "%u,%u", &t, &k) == 2 && k1_kernel(true, t, static_cast<int>(k), e->k1_variant_, 0)) {
-      e->k1_threads_ = t;
-      e->k1_streams_ = static_cast<int>(k);
-    }
-  }
-  if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // measurement builds of v3 only
+  if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // K1 measurement builds (kAbl bits)
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
@@ -2317,10 +1075,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   }
   if (const char* c = std::getenv("TSG_K1_CHUNK")) {
     // K1's LDS hit record keeps (offset in the wave item) << kAnchorBits in
-    // 32 bits and a wave item spans 64 * k1_streams * chunk bytes: larger
-    // chunks are clamped so the offset cannot wrap
+    // 32 bits and a wave item spans 64 lanes x 4 chunks: larger chunks are
+    // clamped so the offset cannot wrap
     const long v = std::atol(c);
-    if (v >= 256 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(e->k1_item_chunks())));
+    if (v >= 256 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(kItemChunks)));
   }
   for (int d : devices) {
     std::unique_ptr<DeviceTables> dt(new DeviceTables());
@@ -2424,8 +1182,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
-  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, k1_variant_);
-  if (kChunk > k1_max_chunk(k1_item_chunks()) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total);
+  if (kChunk > k1_max_chunk(kItemChunks) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   if ((k1_abl_ & kAblNoLoad) && total < (1u << 20) + 64) { *err = "TSG_K1_ABL no-load build needs a batch of >= 1 MiB"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
@@ -2444,10 +1202,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   if (4 + ngroups > kCntBytes / 4) { *err = "too many scan-DFA groups"; return false; }
   if (!ensure(&ln.d_bh, &ln.d_bh_cap, 2ull * std::max(dt.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
   if (!ensure(&ln.d_ff, &ln.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
-  // deferred-output slots: v3 kOutSlots per thread (x2 grid slack), v4 two
-  // streams x kOutSlotsV4 per thread
-  if (!ensure(&ln.d_ob, &ln.d_ob_cap, static_cast<size_t>(std::max(dt.sms, 1)) * 1024 *
-                                          std::max<size_t>(2 * kOutSlots, 2 * kOutSlotsV4), err)) return false;
+  // deferred-output slots: kOutSlots per thread (x2 grid slack)
+  if (!ensure(&ln.d_ob, &ln.d_ob_cap, static_cast<size_t>(std::max(dt.sms, 1)) * 1024 * 2 * kOutSlots, err))
+    return false;
 
   const uint32_t sms = static_cast<uint32_t>(dt.sms);
   const Prefilter& pf = pf_;
@@ -2455,47 +1212,26 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     HIP_OK(hipMemsetAsync(ln.d_kw, 0, kw_n * sizeof(uint32_t), s));
     HIP_OK(hipMemsetAsync(ln.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), s));
     HIP_OK(hipMemsetAsync(ln.d_cnt, 0, kCntBytes, s));
-    const int ks = k1_streams_;
-    const uint32_t nthr = k1_threads_;
-    const uint64_t want_blocks = (nchunks + static_cast<uint64_t>(nthr) * ks - 1) / (static_cast<uint64_t>(nthr) * ks);
+    constexpr uint32_t nthr = 1024;
+    const uint64_t want_blocks = (nchunks + nthr - 1) / nthr;
     // one resident workgroup per CU (the LDS table takes most of the CU's
-    // 160 KiB): a grid of exactly one workgroup per CU, grid-stride
-    bool all_lds = true, all_dual = true;
-    for (const K1Group& g : dt.k1g) { all_lds &= g.in_lds; all_dual &= g.dual5; }
-    // v5 with compact tables: two workgroups per CU
-    const bool v5 = k1_variant_ == 5 && nthr == 1024 && ks == 1;
-    const bool dual = v5 && all_dual && !k1_single5_;
-    const uint32_t per_cu = (!all_lds || dual) ? 2 : 1;
-    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms * static_cast<uint64_t>(per_cu))));
+    // 160 KiB): a grid of exactly one workgroup per CU, waves take items
+    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms)));
     st->k1_blocks = blocks;
     st->k1_threads = nthr;
-    st->table_in_lds = all_lds;
+    st->table_in_lds = 1;
     // one hit region per (group, workgroup); K2 walks all of them
     const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
     const uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(ln.hit_cap / nregions, 0xffffffffu));
     HIP_OK(hipMemsetAsync(ln.d_bh, 0, nregions * sizeof(uint32_t), s));
-    // v3 runs the groups whose table is in LDS (1024 threads, one stream per
-    // lane); the others keep v1
-    auto k1_var = [&](const K1Group& g) {
-      if (v5) return 5;
-      if (k1_variant_ == 4 && g.in_lds && ks == 1 && (nthr == 1024 || nthr == 512)) return 4;
-      return k1_variant_ == 3 && g.in_lds && nthr == 1024 && ks == 1 ? 3 : 1;
-    };
-    auto k1_lds = [&](const K1Group& g) {
-      return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 +
-             (g.in_lds ? ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes : 0);
-    };
     auto lds_of = [&](const K1Group& g) -> size_t {
-      return v5 ? k1_lds5(g.table5_bytes, dual ? kK1HitsDual : kK1HitsSingle) : k1_lds(g);
+      return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 + ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes;
     };
-    auto kernel_of = [&](const K1Group& g) -> const void* {
-      return v5 ? k1_kernel5(dual, k1_line5_) : k1_kernel(g.in_lds, nthr, ks, k1_var(g), k1_abl_);
-    };
+    const void* kfn = k1_kernel(k1_abl_);
+    if (!kfn) { *err = "unsupported K1 build (TSG_K1_ABL)"; return false; }
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
       const K1Group& g = dt.k1g[gi];
-      const void* kfn = kernel_of(g);
-      if (!kfn) { *err = "unsupported K1 configuration (TSG_K1_CFG / TSG_K1_ABL)"; return false; }
-      if (lds_of(g) > kLdsBytes) { *err = "K1 LDS budget exceeded"; return false; }
+      if (!g.in_lds || lds_of(g) > kLdsBytes) { *err = "K1 LDS budget exceeded"; return false; }
       HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_of(g))));
     }
     HIP_OK(hipEventRecord(ln.ev[0], s));
@@ -2503,13 +1239,11 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = dt.k1g[gi];
       const size_t lds = lds_of(g);
-      const void* kfn = kernel_of(g);
       uint32_t* a_items = ln.d_cnt + 4 + gi;         // v3's work-item counter (zeroed with d_cnt)
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
       uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
-      const bool v3_line64 = k1_var(g) == 3 && (k1_abl_ & kAblLine64);
-      uint32_t a_warm = v3_line64 ? g.warm_lines64 : g.warm_lines;
+      uint32_t a_warm = (k1_abl_ & kAblLine64) ? g.warm_lines64 : g.warm_lines;
       unsigned long long a_nchunks = nchunks;
       uint32_t a_chunk = kChunk;
       uint32_t a_kww = dt.kw_words, a_kwbase = g.kw_base, a_primary = gi == 0;
@@ -2524,21 +1258,6 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
       uint32_t a_rcap = region_cap;
       uint32_t a_tail = k1_tail_rounds_;
-      if (v5) {
-        uint16_t* a_next5 = g.next5;
-        uint8_t* a_cls5 = g.cls5;
-        uint16_t* a_oidx5 = g.oidx5;
-        uint32_t a_tb5 = g.table5_bytes, a_first5 = g.first_out5;
-        const uint32_t lb = 16u * static_cast<uint32_t>(k1_line5_);
-        uint32_t a_warm5 = g.max_pattern > 1 ? (g.max_pattern - 1 + lb - 1) / lb : 0;
-        void* args5[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next5, &a_cls5, &a_tb5, &a_first5,
-                         &a_meta, &a_oidx5, &a_list, &a_nkw, &a_warm5, &a_chunk, &a_nchunks,
-                         &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
-                         &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
-        HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args5, lds, s));
-        ++launches;
-        continue;
-      }
       void* args[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
