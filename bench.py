@@ -495,7 +495,8 @@ def main():
     # into the pinned batch (config 3 scans tsg_prepare_batch's output)
     palloc = PinnedAlloc(L) if args.config != 3 else None
     corpus = synth.generate(int(gb * 1e9), seed=args.seed + rank, sizes=sizes,
-                            layout="image" if args.config == 3 else "src", alloc=palloc)
+                            layout="image" if args.config == 3 else "src", alloc=palloc,
+                            progress=lambda i, n: log("generating: %d of %d files" % (i, n)))
     if args.config == 5:      # 500 custom rules + allow rules + exclude blocks (+ builtins)
         cfg5, plants = synth.config5(500, seed=args.seed)
         cfg_path = "/tmp/tsg_bench_config5_%d.yaml" % rank

@@ -371,10 +371,11 @@ IMAGE_DIRS = ("usr/share/doc/pkg%d", "usr/lib/python3.%d/site-packages/mod", "us
 
 
 def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4, near_miss=0.1,
-             base_bytes=32 << 20, max_files=None, layout="src", alloc=None):
+             base_bytes=32 << 20, max_files=None, layout="src", alloc=None, progress=None):
     """A seeded Corpus of ~total_bytes.  `alloc(n)` (optional) returns the
     uint8 array of n bytes the corpus is written into -- e.g. a view of pinned
-    host memory, so a bench holds one copy of its batch instead of two."""
+    host memory, so a bench holds one copy of its batch instead of two.
+    `progress(i, nfiles)` (optional) is called every 200k files."""
     rng = random.Random(seed)
     samples = load_samples()
     rule_ids = sorted(k for k, v in samples.items() if v)
@@ -396,6 +397,8 @@ def generate(total_bytes, seed=DEFAULT_SEED, sizes="lognormal", plant_rate=1e-4,
     seg = 1 << 16
     B = len(base)
     for i, s in enumerate(sz):
+        if progress is not None and i and i % 200000 == 0:
+            progress(i, n)
         o = int(offsets[i])
         filled = 0
         while filled < s:
