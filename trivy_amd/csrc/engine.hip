@@ -67,7 +67,7 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
   return f;
 }
 
-constexpr uint32_t kWaveHits = kK1WaveHits;   // per-wave LDS hit buffer entries (4 bytes: offset in item << 11 | anchor)
+constexpr uint32_t kWaveHits = kK1WaveHits;   // largest per-wave LDS hit buffer (entries of 4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
 constexpr double kDenseFilesPerGB = 8000.0;   // upload segmentation: "many small files" (image layers: ~48k/GB)
@@ -140,7 +140,8 @@ struct K1Ctx {
   uint32_t nfiles;
   const uint16_t* next;   // pre-multiplied: next[s + c] is the next state's row offset
   const uint8_t* cls;     // byte -> class * 2
-  uint32_t first_out;     // row offset of the first state with outputs
+  uint32_t first_out;     // row offset (dwords) of the first state with outputs
+  uint32_t wave_hits;     // per-wave LDS hit buffer entries of this launch
   uint32_t nclasses;      // row slot `nclasses` holds the output-state index
   const OutMeta* meta;
   const uint32_t* list;
@@ -163,9 +164,10 @@ struct K1Ctx {
 
 // One transition: `s` is the current state's row offset (state * stride, in
 // uint16 elements) and `c2` the byte's class times 2 (the class map is stored
-// pre-doubled), so the LDS byte address is (s << 1) + c2.
+// pre-doubled) and rows start on dwords, so the LDS byte address is
+// (s << 2) + c2 with `s` the row offset in dwords (tables up to 256 KiB).
 __device__ __forceinline__ uint32_t k1_step(const uint16_t* next, uint32_t s, uint32_t c2) {
-  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(next) + ((s << 1) + c2));
+  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(next) + ((s << 2) + c2));
 }
 
 // LDS reads by integer LDS address: the kernel's dynamic LDS starts
@@ -205,7 +207,7 @@ __device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, co
 // masks and the list position inline after the spare slot (S = silent-row
 // stride), so one LDS round trip fetches them.
 __device__ __forceinline__ void k1_out_v3(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q, uint32_t S) {
-  const uint32_t* m = reinterpret_cast<const uint32_t*>(x.next + st + S);   // 4-byte aligned: st and S are even
+  const uint32_t* m = reinterpret_cast<const uint32_t*>(x.next + 2 * st + S);   // 4-byte aligned: S is even
   const uint32_t a0 = m[0], a1 = m[1], a2 = m[2], a3 = m[3], li = m[4];
   t.kw0 |= (static_cast<unsigned long long>(a1) << 32) | a0;
   t.kw1 |= (static_cast<unsigned long long>(a3) << 32) | a2;
@@ -216,7 +218,7 @@ __device__ __forceinline__ void k1_out_v3(const K1Ctx& x, K1Stream& t, uint32_t 
       atomicOr(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
     } else {
       const uint32_t li2 = atomicAdd(x.w_hitcnt, 1u);
-      if (li2 < kWaveHits) {
+      if (li2 < x.wave_hits) {
         x.w_hits[li2] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
       } else {                                           // buffer full: straight to the region
         const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
@@ -469,8 +471,8 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
   uint32_t s = t.s;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (kAbl & kAblPtrAddr) s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 1) + c2[k]);
-    else s = k1_lds16((s << 1) + c2[k] + kTabOff);
+    if (kAbl & kAblPtrAddr) s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 2) + c2[k]);
+    else s = k1_lds16((s << 2) + c2[k] + kTabOff);
     st[k] = s;
   }
   t.s = s;
@@ -515,7 +517,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
     uint32_t nclasses, uint32_t table_words16, uint32_t first_out,
-    const OutMeta* __restrict__ g_meta, uint32_t nmeta, const uint32_t* __restrict__ g_list, uint32_t nlist,
+    const OutMeta* __restrict__ g_meta, uint32_t wave_hits, const uint32_t* __restrict__ g_list, uint32_t nlist,
     uint32_t nkw, uint32_t warm_lines, uint32_t chunk, unsigned long long nchunks,
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
@@ -536,7 +538,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   uint32_t S = (nclasses + 2) & ~1u;             // k1_row_stride(nclasses): the silent-row stride
   if (((S / 2) & 1u) == 0) S += 2;
   uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
-  uint32_t* s_hitcnt = s_hits + kWaves * kWaveHits;
+  uint32_t* s_hitcnt = s_hits + kWaves * wave_hits;
   uint32_t* s_block = s_hitcnt + kMaxWaves;      // [0] region fill count
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_block[0] = 0;
@@ -553,14 +555,14 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   x.offsets = offsets; x.nfiles = nfiles;
   x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
   x.cls = smem;
-  x.first_out = first_out; x.nclasses = nclasses;
+  x.first_out = first_out; x.nclasses = nclasses; x.wave_hits = wave_hits;
   x.meta = nullptr;
   x.list = reinterpret_cast<const uint32_t*>(smem + list_off);
   x.nkw = nkw;
   x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
   x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
   x.over = over; x.over_cnt = over_cnt; x.over_cap = over_cap;
-  x.w_hits = s_hits + wid * kWaveHits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
+  x.w_hits = s_hits + wid * wave_hits; x.w_hitcnt = s_hitcnt + wid; x.fflags = fflags;
   __syncthreads();
   // Guided work schedule.  A wave item gives each of its 64 lanes a range of
   // kU consecutive chunks, walked as one stream (one warm-up) that stores the
@@ -670,7 +672,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     // flush this wave's hit buffer (the wave has reconverged here)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const uint32_t n = min(*x.w_hitcnt, kWaveHits);
+    const uint32_t n = min(*x.w_hitcnt, wave_hits);
     uint32_t b0 = 0, o0 = 0;
     if (lane == 0 && n) {
       b0 = atomicAdd(x.b_hitcnt, n);
@@ -879,15 +881,15 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     const uint32_t fo = sd.first_out_state;
     g.stride = stride;
     g.nclasses = C;
-    g.first_out = fo * stride;
+    g.first_out = fo * stride / 2;               // row offsets in dwords (stride is even)
     g.kw_base = sd.kw_base;
     const uint32_t warm = sd.max_pattern_bytes > 0 ? sd.max_pattern_bytes - 1 : 0;
     g.warm_lines = (warm + 127) / 128;          // warm-up = whole 128-byte lines before the chunk (128-B line builds)
     g.warm_lines64 = (warm + 63) / 64;          // v3 (64-byte lines): whole 64-byte lines
     // entries hold the next state's row offset: the DFA chain is then one
     // add + one LDS read per byte (no multiply)
-    if (k1_table_words16(sd) > 65535) {
-      *err = "scan DFA group too large for 16-bit pre-multiplied offsets";
+    if (k1_table_words16(sd) > 2 * 65535) {
+      *err = "scan DFA group too large for 16-bit pre-multiplied dword offsets";
       return false;
     }
     if (C > 127) { *err = "scan DFA has more than 127 byte classes"; return false; }
@@ -895,7 +897,7 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     std::vector<uint16_t> sn(k1_table_words16(sd), 0);
     for (uint32_t st = 0; st < sd.t.nstates; ++st) {
       for (uint32_t c = 0; c < C; ++c)
-        sn[row(st) + c] = static_cast<uint16_t>(row(sd.t.next[static_cast<size_t>(st) * C + c]));
+        sn[row(st) + c] = static_cast<uint16_t>(row(sd.t.next[static_cast<size_t>(st) * C + c]) / 2);
       if (st >= fo) sn[row(st) + C] = static_cast<uint16_t>(st - fo);
     }
     // per output state: keyword masks (ids kw_base .. kw_base+127) + list of other output ids
@@ -923,10 +925,10 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     g.ostride = ostride;
     g.nmeta = static_cast<uint32_t>(meta.size());
     g.nlist = static_cast<uint32_t>(olist.size());
-    g.meta_bytes = ((meta.size() * sizeof(OutMeta) + olist.size() * 4) + 15) & ~size_t(15);
+    g.meta_bytes = (olist.size() * 4 + 15) & ~size_t(15);   // in LDS: the output list (metadata is inline)
     g.table_words16 = static_cast<uint32_t>(sn.size());
     // LDS: per-wave hit buffers (16 waves) + counters + scan table + class map + output metadata
-    g.in_lds = kK1HitLdsBytes + ((static_cast<size_t>(g.table_words16) * 2 + 15) & ~size_t(15)) + 256 + g.meta_bytes <= kLdsBytes;
+    g.in_lds = kK1HitLdsMin + ((static_cast<size_t>(g.table_words16) * 2 + 15) & ~size_t(15)) + 256 + g.meta_bytes <= kLdsBytes;
     sn.resize(((sn.size() * 2 + 15) / 16) * 8, 0);
     // K1's class map holds class * 2 (see k1_step)
     std::vector<uint8_t> cls(256);
@@ -1224,9 +1226,18 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
     const uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(ln.hit_cap / nregions, 0xffffffffu));
     HIP_OK(hipMemsetAsync(ln.d_bh, 0, nregions * sizeof(uint32_t), s));
-    auto lds_of = [&](const K1Group& g) -> size_t {
-      return (nthr / 64) * kWaveHits * 4 + kMaxWaves * 4 + 16 + ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes;
+    // per-wave LDS hit buffers as large as the group's table leaves room for
+    // (512 entries for the builtin rules; large config-5 groups get fewer,
+    // further hits go straight to the workgroup's global region)
+    auto lds_for = [&](const K1Group& g, uint32_t h) -> size_t {
+      return (nthr / 64) * h * 4 + kMaxWaves * 4 + 16 + ((g.table_words16 * 2 + 15) & ~15u) + 256 + g.meta_bytes;
     };
+    auto hits_of = [&](const K1Group& g) -> uint32_t {
+      uint32_t h = kWaveHits;
+      while (h > kK1WaveHitsMin && lds_for(g, h) > kLdsBytes) h /= 2;
+      return h;
+    };
+    auto lds_of = [&](const K1Group& g) -> size_t { return lds_for(g, hits_of(g)); };
     const void* kfn = k1_kernel(k1_abl_);
     if (!kfn) { *err = "unsupported K1 build (TSG_K1_ABL)"; return false; }
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
@@ -1242,7 +1253,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t* a_items = ln.d_cnt + 4 + gi;         // v3's work-item counter (zeroed with d_cnt)
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
-      uint32_t a_first = g.first_out, a_nmeta = g.nmeta, a_nlist = g.nlist, a_nkw = pf.nkw;
+      uint32_t a_first = g.first_out, a_nmeta = hits_of(g), a_nlist = g.nlist, a_nkw = pf.nkw;
       uint32_t a_warm = (k1_abl_ & kAblLine64) ? g.warm_lines64 : g.warm_lines;
       unsigned long long a_nchunks = nchunks;
       uint32_t a_chunk = kChunk;

@@ -908,11 +908,13 @@ bool build_group(const std::vector<Pattern>& ps, ScanDfa* out, std::string* err)
   return true;
 }
 
-// One group when everything fits K1 (the builtin rules); otherwise sorted
-// patterns are packed into runs of ~kGroupTrieNodes estimated trie nodes, and
-// a run whose DFA still does not fit is halved until it does.
+// One group when everything fits K1 (the builtin rules).  Otherwise the
+// patterns, sorted so shared prefixes sit together, are cut into the fewest
+// balanced runs (by estimated trie nodes) whose DFAs all fit K1's LDS budget:
+// each group is one K1 pass over the data, so fewer groups is the lever on a
+// large ruleset's K1 time.  A run that still does not fit at many runs is
+// halved until it does.
 bool make_groups(Prefilter* pf, std::vector<Pattern> pats, std::string* err) {
-  constexpr uint32_t kGroupTrieNodes = 660;
   pf->groups.clear();
   std::string e;
   {
@@ -937,23 +939,42 @@ bool make_groups(Prefilter* pf, std::vector<Pattern> pats, std::string* err) {
     while (l < a.size() && l < b.size() && a[l] == b[l]) ++l;
     return l;
   };
-  // balanced runs: as many as the total estimate needs, equal shares
   uint64_t total = 0;
   for (size_t j = 0; j < order.size(); ++j)
     total += keys[order[j]].size() - (j ? lcp_of(keys[order[j]], keys[order[j - 1]]) : 0);
-  const uint64_t nruns = std::max<uint64_t>(1, (total + kGroupTrieNodes - 1) / kGroupTrieNodes);
-  const uint64_t share = (total + nruns - 1) / nruns;
-  std::vector<std::vector<Pattern>> runs(1);
-  uint64_t est = 0;
-  std::string prev;
-  for (size_t i : order) {
-    const std::string& k = keys[i];
-    size_t lcp = lcp_of(k, prev);
-    if (est + (k.size() - lcp) > share && !runs.back().empty() && runs.size() < nruns) { runs.emplace_back(); est = 0; lcp = 0; }
-    est += k.size() - lcp;
-    runs.back().push_back(pats[i]);
-    prev = k;
+  auto split = [&](uint64_t nruns) {
+    const uint64_t share = (total + nruns - 1) / nruns;
+    std::vector<std::vector<Pattern>> runs(1);
+    uint64_t est = 0;
+    std::string prev;
+    for (size_t i : order) {
+      const std::string& k = keys[i];
+      size_t lcp = lcp_of(k, prev);
+      if (est + (k.size() - lcp) > share && !runs.back().empty() && runs.size() < nruns) { runs.emplace_back(); est = 0; lcp = 0; }
+      est += k.size() - lcp;
+      runs.back().push_back(pats[i]);
+      prev = k;
+    }
+    return runs;
+  };
+  // ~130 bytes of LDS per trie node (a row of ~64 classes): the first guess
+  constexpr uint64_t kNodesPerGroup = (kK1LdsBytes - kK1HitLdsMin - 8192) / 130;
+  const uint64_t first = std::max<uint64_t>(2, (total + kNodesPerGroup - 1) / kNodesPerGroup);
+  for (uint64_t nruns = first; nruns <= 4 * first; ++nruns) {
+    std::vector<ScanDfa> gs;
+    bool ok = true;
+    for (auto& run : split(nruns)) {
+      ScanDfa d;
+      e.clear();
+      if (!build_group(run, &d, &e) || !k1_fits(d)) { ok = false; break; }
+      gs.push_back(std::move(d));
+    }
+    if (ok) {
+      pf->groups = std::move(gs);
+      return true;
+    }
   }
+  std::vector<std::vector<Pattern>> runs = split(4 * first);
   std::vector<std::vector<Pattern>> todo(runs.rbegin(), runs.rend());
   while (!todo.empty()) {
     std::vector<Pattern> ps = std::move(todo.back());
@@ -1017,13 +1038,14 @@ uint64_t k1_table_words16(const ScanDfa& d) {
 
 size_t k1_lds_table_bytes(const ScanDfa& d) {
   const size_t tab = (k1_table_words16(d) * 2 + 15) & ~size_t(15);
-  const size_t nout = d.t.nstates - d.first_out_state;
-  const size_t meta = (nout * 24 + d.out_ids.size() * 4 + 15) & ~size_t(15);   // OutMeta + (at most) every id listed
-  return tab + 256 + meta;
+  const size_t list = (d.out_ids.size() * 4 + 15) & ~size_t(15);   // (at most) every output id listed
+  return tab + 256 + list;
 }
 
+// K1 entries are dword row offsets in 16 bits (tables up to 256 KiB); the
+// per-wave hit buffers shrink to kK1WaveHitsMin entries for large groups
 bool k1_fits(const ScanDfa& d) {
-  return k1_table_words16(d) <= 65535 && kK1HitLdsBytes + k1_lds_table_bytes(d) <= kK1LdsBytes;
+  return k1_table_words16(d) <= 2 * 65535 && kK1HitLdsMin + k1_lds_table_bytes(d) <= kK1LdsBytes;
 }
 
 bool literal_gate(const re::Node& ast, re::LitGate* out, bool* bounded, uint32_t* dmin, uint32_t* dmax) {

@@ -49,8 +49,10 @@ struct ScanDfa {
 // transitions are uint16 row offsets (state * stride), so a GPU scan DFA
 // must satisfy nstates * stride <= 65535 and fit the LDS left over.
 constexpr uint32_t kK1LdsBytes = 160 * 1024;
-constexpr uint32_t kK1WaveHits = 512;    // per-wave LDS hit buffer entries (K1); further hits go straight to global
+constexpr uint32_t kK1WaveHits = 512;    // per-wave LDS hit buffer entries (K1) when the table leaves room
+constexpr uint32_t kK1WaveHitsMin = 64;  // ... and the least a group is planned with; further hits go to global
 constexpr uint32_t kK1HitLdsBytes = 16 * kK1WaveHits * 4 + 16 * 4 + 16;
+constexpr uint32_t kK1HitLdsMin = 16 * kK1WaveHitsMin * 4 + 16 * 4 + 16;
 uint32_t k1_row_stride(uint32_t nclasses);          // >= nclasses + 1, odd number of dwords
 // Output-state rows carry their output metadata inline after the spare slot:
 // keyword masks (8 x uint16) and the output list's begin / count (2 x uint16).
