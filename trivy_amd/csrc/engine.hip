@@ -207,7 +207,7 @@ __device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, co
 // masks and the list position inline after the spare slot (S = silent-row
 // stride), so one LDS round trip fetches them.
 __device__ __forceinline__ void k1_out_v3(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q, uint32_t S) {
-  const uint32_t* m = reinterpret_cast<const uint32_t*>(x.next + 2 * st + S);   // 4-byte aligned: S is even
+  const uint32_t* m = reinterpret_cast<const uint32_t*>(x.next + S) + st;   // st in dwords; 4-byte aligned: S is even
   const uint32_t a0 = m[0], a1 = m[1], a2 = m[2], a3 = m[3], li = m[4];
   t.kw0 |= (static_cast<unsigned long long>(a1) << 32) | a0;
   t.kw1 |= (static_cast<unsigned long long>(a3) << 32) | a2;
