@@ -778,6 +778,30 @@ bool build_reverse(const std::vector<const Node*>& items, size_t k, const SeqSet
   return true;
 }
 
+// Byte classes whose transition columns are identical are one class for the
+// automaton (exact: no state tells them apart).  The subset construction's
+// classes come from the NFA's edge sets, which can distinguish bytes the DFA
+// does not (the builtin scan DFA: 64 -> 50 classes), so merging shrinks every
+// K1 table row.
+void merge_classes(DfaTable* t) {
+  const uint32_t C = t->nclasses, N = t->nstates;
+  std::map<std::vector<uint16_t>, uint32_t> colid;
+  std::vector<uint32_t> newc(C);
+  for (uint32_t c = 0; c < C; ++c) {
+    std::vector<uint16_t> col(N);
+    for (uint32_t s = 0; s < N; ++s) col[s] = t->next[static_cast<size_t>(s) * C + c];
+    newc[c] = colid.emplace(std::move(col), static_cast<uint32_t>(colid.size())).first->second;
+  }
+  const uint32_t C2 = static_cast<uint32_t>(colid.size());
+  if (C2 == C) return;
+  std::vector<uint16_t> nx(static_cast<size_t>(N) * C2);
+  for (uint32_t s = 0; s < N; ++s)
+    for (uint32_t c = 0; c < C; ++c) nx[static_cast<size_t>(s) * C2 + newc[c]] = t->next[static_cast<size_t>(s) * C + c];
+  t->next.swap(nx);
+  for (int b = 0; b < 256; ++b) t->byte_class[b] = static_cast<uint8_t>(newc[t->byte_class[b]]);
+  t->nclasses = C2;
+}
+
 bool make_scan_dfa(const Nfa& nfa, int s0, uint32_t maxb, ScanDfa* out, std::string* err) {
   RawDfa raw;
   if (!determinize(nfa, s0, true, -1, kScanStateCap, &raw)) { *err = "scan DFA exceeds state cap"; return false; }
@@ -803,6 +827,7 @@ bool make_scan_dfa(const Nfa& nfa, int s0, uint32_t maxb, ScanDfa* out, std::str
     out->out_off.push_back(static_cast<uint32_t>(out->out_ids.size()));
   }
   out->max_pattern_bytes = maxb;
+  merge_classes(&out->t);
   return true;
 }
 
