@@ -1190,6 +1190,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
   hipStream_t s = ln.compute;
+  const auto t_seg0 = std::chrono::steady_clock::now();   // TSG_HOST_PROFILE: where a segment's GPU time goes
   if (!ensure(&ln.d_off, &ln.d_off_cap, in.nfiles + 1, err)) return false;
   HIP_OK(hipMemcpyAsync(ln.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * dt.kw_words;
@@ -1281,6 +1282,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     HIP_OK(hipMemcpyAsync(ln.h_bh.data(), ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(ln.h_bh.data() + nregions, ln.d_cnt + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
+    const double t_k1_sync = ms_since(t_seg0);
     float k1 = 0;
     HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
     st->k1_ms += k1;
@@ -1352,6 +1354,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), ln.d_nl, nchunks * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
       st->d2h_ms += ms_since(t_d2h);
+      if (host_profile_)
+        std::fprintf(stderr, "[tsg seg] %.1f MB %u files: wall to K1 done %.3f ms (K1 %.3f), K2 %.3f ms, d2h %.3f ms, "
+                     "total %.3f ms\n", total / 1e6, in.nfiles, t_k1_sync, k1, k2, ms_since(t_d2h), ms_since(t_seg0));
       st->candidates += c2;
       if (ln.d_k2s) {
         std::vector<unsigned long long> h(4 * pf_.rules.size());
