@@ -81,8 +81,8 @@ class Engine {
  private:
   Engine() = default;
   struct Segment;
-  bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, ScanStats* st, GpuOut* out,
-                   std::string* err);
+  bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, const uint64_t* d_off_up,
+                   ScanStats* st, GpuOut* out, std::string* err);
   void confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Secret* results, uint64_t* nconf,
                        uint64_t* nfind, bool gpu_in_flight);
   Lane* acquire_lane(DeviceTables& dt, std::string* err);

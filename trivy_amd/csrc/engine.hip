@@ -783,9 +783,16 @@ struct Lane {
   hipStream_t compute = nullptr, copy = nullptr;
   hipEvent_t ev[4] = {};                        // K1 start/end, K2 start/end (compute stream)
   hipEvent_t up_begin[2] = {}, up_done[2] = {}; // upload ring slot: H2D start / done (copy stream)
+  hipEvent_t anchor = nullptr;                   // TSG_HOST_PROFILE: start of a scan() on the copy stream
   uint8_t* ring[2] = {nullptr, nullptr};
   size_t ring_cap[2] = {0, 0};
   uint64_t* d_off = nullptr; size_t d_off_cap = 0;
+  // uploaded data: the segment's offsets travel on the copy stream with its
+  // bytes, from pinned staging (a pageable copy of >~64 KB on the compute
+  // stream is staged through the copy engine and queues behind the next
+  // segment's upload: measured, config 1's first K1 waited 8.8 ms)
+  uint64_t* off_slot[2] = {nullptr, nullptr}; size_t off_slot_cap[2] = {0, 0};
+  uint64_t* h_off_pin[2] = {nullptr, nullptr}; size_t h_off_pin_cap[2] = {0, 0};
   uint32_t* d_kw = nullptr; size_t d_kw_cap = 0;
   unsigned long long* d_hits = nullptr; size_t d_hits_cap = 0;
   unsigned long long* d_over = nullptr; size_t d_over_cap = 0;   // hits past a full region (any workgroup)
@@ -840,9 +847,11 @@ Lane::~Lane() {
   hipSetDevice(device);
   if (compute) hipStreamSynchronize(compute);
   if (copy) hipStreamSynchronize(copy);
-  void* ps[] = {ring[0], ring[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s, d_cr};
+  for (uint64_t* h : h_off_pin) if (h) hipHostFree(h);
+  void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s, d_cr};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
+  if (anchor) hipEventDestroy(anchor);
   for (int i = 0; i < 2; ++i) {
     if (up_begin[i]) hipEventDestroy(up_begin[i]);
     if (up_done[i]) hipEventDestroy(up_done[i]);
@@ -1138,6 +1147,7 @@ Lane* Engine::acquire_lane(DeviceTables& dt, std::string* err) {
       return nullptr;
     }
   }
+  if (hipEventCreate(&l->anchor) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
   for (int i = 0; i < 2; ++i) {
     if (hipEventCreate(&l->up_begin[i]) != hipSuccess || hipEventCreate(&l->up_done[i]) != hipSuccess) {
       *err = "hipEventCreate failed";
@@ -1177,8 +1187,8 @@ void Engine::release_call(CallCtx* cc) {
 // K1 + K2 + candidate D2H of one segment whose bytes are at d_data on the
 // lane's device (resident, or landed by the lane's upload), on the lane's
 // compute stream.  Returns when the segment's results are on the host.
-bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, ScanStats* st,
-                         GpuOut* out, std::string* err) {
+bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, const uint64_t* d_off_up,
+                         ScanStats* st, GpuOut* out, std::string* err) {
   const BatchInput& in = sg.in;
   HIP_OK(hipSetDevice(dt.device));
   const uint64_t total = in.offsets[in.nfiles];
@@ -1191,8 +1201,13 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   out->chunk = kChunk;
   hipStream_t s = ln.compute;
   const auto t_seg0 = std::chrono::steady_clock::now();   // TSG_HOST_PROFILE: where a segment's GPU time goes
-  if (!ensure(&ln.d_off, &ln.d_off_cap, in.nfiles + 1, err)) return false;
-  HIP_OK(hipMemcpyAsync(ln.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  // offsets: landed with the upload (d_off_up), or copied here (resident data)
+  uint64_t* d_off = const_cast<uint64_t*>(d_off_up);
+  if (!d_off) {
+    if (!ensure(&ln.d_off, &ln.d_off_cap, in.nfiles + 1, err)) return false;
+    HIP_OK(hipMemcpyAsync(ln.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    d_off = ln.d_off;
+  }
   const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * dt.kw_words;
   if (!ensure(&ln.d_kw, &ln.d_kw_cap, kw_n, err)) return false;
   const unsigned long long nchunks = (total + kChunk - 1) / kChunk;
@@ -1270,7 +1285,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
       uint32_t a_rcap = region_cap;
       uint32_t a_tail = k1_tail_rounds_;
-      void* args[] = {&a_data, &a_total, &ln.d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
+      void* args[] = {&a_data, &a_total, &d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
                       &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
@@ -1312,12 +1327,12 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
         const uint64_t per_block = 256ull * k2_hits_per_thread_;
         const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(256, (maxr + per_block - 1) / per_block)));
         if (ln.d_k2s)
-          hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+          hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
                              ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
                              dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt,
                              static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
         else
-          hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+          hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
                              ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
                              dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt,
                              static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
@@ -1325,12 +1340,12 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
         if (nover > 0) {                               // the overflow pool as one more region
           const uint32_t osub = static_cast<uint32_t>(std::min<uint64_t>(4096, (nover + 1023) / 1024));
           if (ln.d_k2s)
-            hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(osub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+            hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles,
                                ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
                                dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
                                ln.d_cnt, static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
           else
-            hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(osub), dim3(256), 0, s, d_data, ln.d_off, in.nfiles,
+            hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles,
                                ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
                                dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
                                ln.d_cnt, static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
@@ -1386,7 +1401,7 @@ bool Engine::prefilter_only(const BatchInput& in, std::vector<std::vector<std::v
   Segment sg;
   sg.in = in;
   GpuOut out;
-  const bool ok = run_segment(dt, *ln, sg, in.d_data, st, &out, err);
+  const bool ok = run_segment(dt, *ln, sg, in.d_data, nullptr, st, &out, err);
   release_lane(dt, ln);
   if (!ok) return false;
   const size_t nr = rs_->rules.size();   // real rules only (exclude pseudo-rules follow)
@@ -1718,7 +1733,11 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     }
   }
   uint64_t max_seg = 0;
-  for (const Segment& sg : segs) max_seg = std::max(max_seg, sg.bytes);
+  size_t max_seg_files = 0;
+  for (const Segment& sg : segs) {
+    max_seg = std::max(max_seg, sg.bytes);
+    max_seg_files = std::max<size_t>(max_seg_files, sg.in.nfiles);
+  }
 
   struct Job {
     size_t seg = 0;
@@ -1739,13 +1758,29 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     bool ok = ln != nullptr;
     if (ok && hipSetDevice(dt->device) != hipSuccess) { ok = false; e = "hipSetDevice failed"; }
     if (ok && !resident) {
-      for (int i = 0; i < 2 && ok; ++i) ok = ensure(&ln->ring[i], &ln->ring_cap[i], max_seg + 64, &e);
+      for (int i = 0; i < 2 && ok; ++i) {
+        ok = ensure(&ln->ring[i], &ln->ring_cap[i], max_seg + 64, &e) &&
+             ensure(&ln->off_slot[i], &ln->off_slot_cap[i], max_seg_files + 1, &e);
+        if (ok && ln->h_off_pin_cap[i] < max_seg_files + 1) {
+          if (ln->h_off_pin[i]) hipHostFree(ln->h_off_pin[i]);
+          ln->h_off_pin[i] = nullptr;
+          ln->h_off_pin_cap[i] = 0;
+          if (hipHostMalloc(reinterpret_cast<void**>(&ln->h_off_pin[i]), (max_seg_files + 1) * sizeof(uint64_t),
+                            hipHostMallocDefault) != hipSuccess) { ok = false; e = "pinned offsets staging"; }
+          else ln->h_off_pin_cap[i] = max_seg_files + 1;
+        }
+      }
     }
     // upload of segment `si` into ring slot `slot` (copy stream)
     auto upload = [&](size_t si, int slot) -> bool {
       const Segment& sg = segs[si];
       std::string* err = &e;
       HIP_OK(hipEventRecord(ln->up_begin[slot], ln->copy));
+      // the slot's staging was last read by the upload two segments back,
+      // complete since that segment's kernels waited on it
+      std::memcpy(ln->h_off_pin[slot], sg.in.offsets, (sg.in.nfiles + 1) * sizeof(uint64_t));
+      HIP_OK(hipMemcpyAsync(ln->off_slot[slot], ln->h_off_pin[slot], (sg.in.nfiles + 1) * sizeof(uint64_t),
+                            hipMemcpyHostToDevice, ln->copy));
       HIP_OK(hipMemcpyAsync(ln->ring[slot], sg.in.h_data, sg.bytes, hipMemcpyHostToDevice, ln->copy));
       HIP_OK(hipMemsetAsync(ln->ring[slot] + sg.bytes, 0, 64, ln->copy));   // K1 reads 16-B words past the end
       HIP_OK(hipEventRecord(ln->up_done[slot], ln->copy));
@@ -1753,6 +1788,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     };
     size_t cur = ok ? next_seg.fetch_add(1) : segs.size();
     int slot = 0;
+    if (ok && host_profile_) hipEventRecord(ln->anchor, ln->copy);
     if (ok && cur < segs.size() && !resident) ok = upload(cur, slot);
     while (ok && cur < segs.size() && !q.aborted()) {
       const size_t nxt = next_seg.fetch_add(1);
@@ -1772,8 +1808,20 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       std::unique_ptr<Job> job(new Job());
       job->seg = cur;
       ScanStats sst;
-      ok = run_segment(*dt, *ln, segs[cur], d_data, &sst, &job->out, &e);
+      const double h_start = ms_since(t_feed0);
+      ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e);
       if (!ok) break;
+      if (host_profile_ && !resident) {
+        // GPU timeline of this segment from the scan's anchor event
+        float ub = 0, ud = 0, k1a = 0, k1b = 0, k2b = 0;
+        hipEventElapsedTime(&ub, ln->anchor, ln->up_begin[slot]);
+        hipEventElapsedTime(&ud, ln->anchor, ln->up_done[slot]);
+        hipEventElapsedTime(&k1a, ln->anchor, ln->ev[0]);
+        hipEventElapsedTime(&k1b, ln->anchor, ln->ev[1]);
+        hipEventElapsedTime(&k2b, ln->anchor, ln->ev[3]);
+        std::fprintf(stderr, "[tsg tl] seg %zu: host %.3f-%.3f ms; gpu upload %.3f-%.3f, K1 %.3f-%.3f, K2 done %.3f\n",
+                     cur, h_start, ms_since(t_feed0), ub, ud, k1a, k1b, k2b);
+      }
       if (!resident) {
         float h2d = 0;
         if (hipEventElapsedTime(&h2d, ln->up_begin[slot], ln->up_done[slot]) == hipSuccess) sst.h2d_ms += h2d;
