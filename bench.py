@@ -596,6 +596,7 @@ def main():
     torch.cuda.synchronize()
     stats = []
     last = None
+    free_s = 0.0
     t0 = time.perf_counter()
     for k in range(args.steps):
         res, st = step()
@@ -603,7 +604,9 @@ def main():
         if k == args.steps - 1:
             last = res
         else:
+            tf = time.perf_counter()
             L.tsg_result_free(res)
+            free_s += time.perf_counter() - tf
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -708,6 +711,7 @@ def main():
         "breakdown_ms": {"segments": segments, "chunk_bytes": stats[-1]["chunk_bytes"], "k1": round(k1_ms, 3), "k2": round(k2_ms, 3),
                          "h2d": round(h2d_ms, 3), "host_confirm": round(host_ms, 3),
                          "feed": round(mean("feed_ms"), 3), "engine_total": round(mean("total_ms"), 3),
+                         "result_free": round(free_s / max(1, args.steps - 1) * 1e3, 3),
                          "hits": stats[-1]["hits"], "candidates": stats[-1]["candidates"],
                          "confirm_files": stats[-1]["confirm_files"], "findings": findings,
                          "rules_with_findings": len(rules_hit)},

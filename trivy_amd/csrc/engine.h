@@ -113,7 +113,7 @@ class Engine {
   uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)
   double first_piece_ = 0.7;            // resident data: share of the first piece (TSG_FIRST_PIECE)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
-  uint64_t segment_min_ = 256ull << 20;  // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN)
+  uint64_t segment_min_ = 128ull << 20;  // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1)
   uint64_t segment_tail_ = 0;           // uploaded data: a short last segment (TSG_SEGMENT_TAIL; 0 = none: the
                                         // rest after the full segments is one launch, K1 keeps its large-launch rate)
   uint64_t segment_ = 4ull << 30;       // uploaded data: bytes per pipeline segment (TSG_SEGMENT_BYTES);

@@ -1693,7 +1693,11 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         const uint64_t rest = total - in.offsets[f];
         const uint64_t tail = std::min(segment_tail_, segment_ / 8);
         uint64_t target;
-        if (rest > segment_ + tail) target = in.offsets[f] + segment_;
+        // (geometric batches start halving once less than two full segments
+        // are left: a full segment's confirmation then hides behind the next
+        // half-size upload; r3t config 5: 4.3+4.3+0.7+... GB left 16 ms after
+        // the last upload, the second segment's 25 ms confirmation)
+        if (geometric ? rest >= 2 * segment_ : rest > segment_ + tail) target = in.offsets[f] + segment_;
         else if (geometric && rest / 2 >= segment_min_) target = in.offsets[f] + rest / 2;
         else if (tail > 0 && rest > 2 * tail) target = total - tail;
         else break;
