@@ -192,8 +192,8 @@ int tsg_result_json(const tsg_result* r, char** json, size_t* len);
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 /* Raw GPU candidates of file i for rule j (sorted starts); for tests. */
 int tsg_result_candidates(const tsg_result* r, uint32_t file, uint32_t rule, const uint64_t** starts, size_t* n);
-/* Frees a result; one of >= 4096 files is handed to a background thread
-   (its memory returns shortly after the call). */
+/* Frees a result; one of >= 4096 files + findings is handed to a background
+   thread (its memory returns shortly after the call). */
 void tsg_result_free(tsg_result* r);
 void tsg_free(void* p);
 

@@ -778,6 +778,23 @@ struct DeviceTables {
 // One in-flight call's resources on one device: its own streams (compute +
 // copy), timing events, the two-slot upload ring and every per-batch scratch
 // buffer, so concurrent calls never share mutable GPU state.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+bool ensure_pinned(PinnedBuf* b, size_t bytes, std::string* err) {
+  if (b->p && b->cap >= bytes) return true;
+  if (b->p) HIP_OK(hipHostFree(b->p));
+  b->p = nullptr;
+  b->cap = 0;
+  const size_t want = std::max<size_t>(bytes + bytes / 4, 256);
+  HIP_OK(hipHostMalloc(&b->p, want, hipHostMallocDefault));
+  b->cap = want;
+  return true;
+}
+
 struct Lane {
   int device = 0;
   hipStream_t compute = nullptr, copy = nullptr;
@@ -793,6 +810,10 @@ struct Lane {
   // segment's upload: measured, config 1's first K1 waited 8.8 ms)
   uint64_t* off_slot[2] = {nullptr, nullptr}; size_t off_slot_cap[2] = {0, 0};
   uint64_t* h_off_pin[2] = {nullptr, nullptr}; size_t h_off_pin_cap[2] = {0, 0};
+  // readbacks land in pinned memory (a pageable D2H is staged through a copy
+  // engine and at times waited behind the next segment's upload: r3q/r3u
+  // config 2, up to 22 ms between K2 done and the results on the host)
+  PinnedBuf rb_bh, rb_c2, rb_cands, rb_ff, rb_nl;
   uint32_t* d_kw = nullptr; size_t d_kw_cap = 0;
   unsigned long long* d_hits = nullptr; size_t d_hits_cap = 0;
   unsigned long long* d_over = nullptr; size_t d_over_cap = 0;   // hits past a full region (any workgroup)
@@ -804,7 +825,6 @@ struct Lane {
   unsigned long long* d_k2s = nullptr;              // TSG_K2_STATS: per-rule K2 counters (4 per rule)
   unsigned int* d_cnt = nullptr;
   uint8_t* d_cr = nullptr; size_t d_cr_cap = 0;     // CR strip scratch (crstrip.hip)
-  std::vector<uint32_t> h_bh;
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
   ~Lane();
 };
@@ -848,6 +868,7 @@ Lane::~Lane() {
   if (compute) hipStreamSynchronize(compute);
   if (copy) hipStreamSynchronize(copy);
   for (uint64_t* h : h_off_pin) if (h) hipHostFree(h);
+  for (PinnedBuf* b : {&rb_bh, &rb_c2, &rb_cands, &rb_ff, &rb_nl}) if (b->p) hipHostFree(b->p);
   void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s, d_cr};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
@@ -1293,9 +1314,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       ++launches;
     }
     HIP_OK(hipEventRecord(ln.ev[1], s));
-    ln.h_bh.resize(nregions + 2);
-    HIP_OK(hipMemcpyAsync(ln.h_bh.data(), ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(ln.h_bh.data() + nregions, ln.d_cnt + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (!ensure_pinned(&ln.rb_bh, (nregions + 2) * sizeof(uint32_t), err)) return false;
+    uint32_t* h_bh = ln.rb_bh.as<uint32_t>();
+    HIP_OK(hipMemcpyAsync(h_bh, ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(h_bh + nregions, ln.d_cnt + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     const double t_k1_sync = ms_since(t_seg0);
     float k1 = 0;
@@ -1304,9 +1326,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     st->k1_launches += launches;
     uint64_t nhits = 0;
     uint32_t maxr = 0;
-    for (uint32_t r = 0; r < nregions; ++r) { nhits += ln.h_bh[r]; maxr = std::max(maxr, std::min(ln.h_bh[r], region_cap)); }
-    if (ln.h_bh[nregions + 1] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
-    const uint32_t nover = ln.h_bh[nregions];
+    for (uint32_t r = 0; r < nregions; ++r) { nhits += h_bh[r]; maxr = std::max(maxr, std::min(h_bh[r], region_cap)); }
+    if (h_bh[nregions + 1] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
+    const uint32_t nover = h_bh[nregions];
     if (nover > ln.over_cap) {
       // the overflow pool (shared by every workgroup) was too small: grow it
       // to the exact need and run K1 again.  Growth follows the batch's total
@@ -1353,21 +1375,25 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
         }
       }
       HIP_OK(hipEventRecord(ln.ev[3], s));
-      unsigned int c2 = 0;
-      HIP_OK(hipMemcpyAsync(&c2, ln.d_cnt + 1, 4, hipMemcpyDeviceToHost, s));
+      if (!ensure_pinned(&ln.rb_c2, 4, err)) return false;
+      HIP_OK(hipMemcpyAsync(ln.rb_c2.p, ln.d_cnt + 1, 4, hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
+      const unsigned int c2 = *ln.rb_c2.as<unsigned int>();
       float k2 = 0;
       HIP_OK(hipEventElapsedTime(&k2, ln.ev[2], ln.ev[3]));
       st->k2_ms += k2;
       if (c2 > ln.cand_cap) { ln.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
       auto t_d2h = std::chrono::steady_clock::now();
-      out->cands.resize(c2);
-      if (c2) HIP_OK(hipMemcpyAsync(out->cands.data(), ln.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, s));
-      out->ff.resize(in.nfiles);
-      if (in.nfiles) HIP_OK(hipMemcpyAsync(out->ff.data(), ln.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      out->nl.resize(nchunks);
-      if (nchunks) HIP_OK(hipMemcpyAsync(out->nl.data(), ln.d_nl, nchunks * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+      if (!ensure_pinned(&ln.rb_cands, c2 * sizeof(CandDev), err) ||
+          !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
+          !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err)) return false;
+      if (c2) HIP_OK(hipMemcpyAsync(ln.rb_cands.p, ln.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, s));
+      if (in.nfiles) HIP_OK(hipMemcpyAsync(ln.rb_ff.p, ln.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      if (nchunks) HIP_OK(hipMemcpyAsync(ln.rb_nl.p, ln.d_nl, nchunks * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
+      out->cands.assign(ln.rb_cands.as<CandDev>(), ln.rb_cands.as<CandDev>() + c2);
+      out->ff.assign(ln.rb_ff.as<uint32_t>(), ln.rb_ff.as<uint32_t>() + in.nfiles);
+      out->nl.assign(ln.rb_nl.as<uint16_t>(), ln.rb_nl.as<uint16_t>() + nchunks);
       st->d2h_ms += ms_since(t_d2h);
       if (host_profile_)
         std::fprintf(stderr, "[tsg seg] %.1f MB %u files: wall to K1 done %.3f ms (K1 %.3f), K2 %.3f ms, d2h %.3f ms, "
