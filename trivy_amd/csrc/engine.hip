@@ -46,6 +46,20 @@ struct RuleDev { uint32_t mode, gate_on_gpu, always_gate, kw_begin, kw_count, ve
 struct VDfaDev { uint32_t next_off, acc_off, cls_off, nclasses, dead, pad0, pad1, pad2; };
 struct CandDev { uint32_t file, rule; unsigned long long start; };
 
+// Readback of a segment's results into host-mapped, fine-grained pinned
+// memory with plain vector stores over PCIe: no copy engine, so a readback
+// never queues behind an upload, and no DMA setup latency per small copy.
+// Copies nwords dwords, or min(*count * per_count, nwords) with a count
+// (16-byte granules: both buffers carry slack past the end).
+__global__ __launch_bounds__(256) void tsg_readback(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                    uint32_t nwords, const uint32_t* __restrict__ count,
+                                                    uint32_t per_count) {
+  uint32_t n = nwords;
+  if (count) n = min(n, *count * per_count);
+  const uint32_t n4 = (n + 3) / 4;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 #define HIP_OK(expr)                                                              \
   do {                                                                            \
     hipError_t e_ = (expr);                                                       \
@@ -779,19 +793,33 @@ struct DeviceTables {
 // copy), timing events, the two-slot upload ring and every per-batch scratch
 // buffer, so concurrent calls never share mutable GPU state.
 struct PinnedBuf {
-  void* p = nullptr;
+  void* p = nullptr;     // host address
+  void* d = nullptr;     // the same memory as the device sees it
   size_t cap = 0;
   template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
+// host-mapped, coherent (fine-grained) pinned memory for tsg_readback
 bool ensure_pinned(PinnedBuf* b, size_t bytes, std::string* err) {
   if (b->p && b->cap >= bytes) return true;
   if (b->p) HIP_OK(hipHostFree(b->p));
-  b->p = nullptr;
+  b->p = b->d = nullptr;
   b->cap = 0;
-  const size_t want = std::max<size_t>(bytes + bytes / 4, 256);
-  HIP_OK(hipHostMalloc(&b->p, want, hipHostMallocDefault));
+  const size_t want = (std::max<size_t>(bytes + bytes / 4, 256) + 63) & ~size_t(63);
+  HIP_OK(hipHostMalloc(&b->p, want + 64, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_OK(hipHostGetDevicePointer(&b->d, b->p, 0));
   b->cap = want;
+  return true;
+}
+
+// dwords of src (device) into b (host-mapped) on stream s
+bool readback(const void* src, const PinnedBuf& b, size_t nwords, const uint32_t* d_count, uint32_t per_count,
+              hipStream_t s, std::string* err) {
+  if (nwords == 0) return true;
+  const uint32_t blocks = static_cast<uint32_t>(std::min<size_t>(1024, (nwords / 4 + 256) / 256));
+  hipLaunchKernelGGL(tsg_readback, dim3(blocks), dim3(256), 0, s, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(b.d), static_cast<uint32_t>(nwords), d_count, per_count);
+  HIP_OK(hipGetLastError());
   return true;
 }
 
@@ -1314,11 +1342,18 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       ++launches;
     }
     HIP_OK(hipEventRecord(ln.ev[1], s));
-    if (!ensure_pinned(&ln.rb_bh, (nregions + 2) * sizeof(uint32_t), err)) return false;
-    uint32_t* h_bh = ln.rb_bh.as<uint32_t>();
-    HIP_OK(hipMemcpyAsync(h_bh, ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(h_bh + nregions, ln.d_cnt + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    // K1's outputs to the host: per-region hit counts, the overflow count and
+    // LDS check (d_cnt[2..3]), and the final file flags and newline counts
+    if (!ensure_pinned(&ln.rb_bh, nregions * sizeof(uint32_t), err) || !ensure_pinned(&ln.rb_c2, 16, err) ||
+        !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
+        !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err) ||
+        !readback(ln.d_bh, ln.rb_bh, nregions, nullptr, 0, s, err) ||
+        !readback(ln.d_cnt, ln.rb_c2, 4, nullptr, 0, s, err) ||
+        !readback(ln.d_ff, ln.rb_ff, in.nfiles, nullptr, 0, s, err) ||
+        !readback(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2, nullptr, 0, s, err)) return false;
     HIP_OK(hipStreamSynchronize(s));
+    const uint32_t* h_bh = ln.rb_bh.as<const uint32_t>();
+    const uint32_t* h_cnt = ln.rb_c2.as<const uint32_t>();
     const double t_k1_sync = ms_since(t_seg0);
     float k1 = 0;
     HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
@@ -1327,8 +1362,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     uint64_t nhits = 0;
     uint32_t maxr = 0;
     for (uint32_t r = 0; r < nregions; ++r) { nhits += h_bh[r]; maxr = std::max(maxr, std::min(h_bh[r], region_cap)); }
-    if (h_bh[nregions + 1] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
-    const uint32_t nover = h_bh[nregions];
+    if (h_cnt[3] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
+    const uint32_t nover = h_cnt[2];
     if (nover > ln.over_cap) {
       // the overflow pool (shared by every workgroup) was too small: grow it
       // to the exact need and run K1 again.  Growth follows the batch's total
@@ -1375,22 +1410,18 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
         }
       }
       HIP_OK(hipEventRecord(ln.ev[3], s));
-      if (!ensure_pinned(&ln.rb_c2, 4, err)) return false;
-      HIP_OK(hipMemcpyAsync(ln.rb_c2.p, ln.d_cnt + 1, 4, hipMemcpyDeviceToHost, s));
+      // the candidates (as many as fit) and their count, in one round trip
+      if (!ensure_pinned(&ln.rb_cands, ln.cand_cap * sizeof(CandDev), err) ||
+          !readback(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4,
+                    s, err) ||
+          !readback(ln.d_cnt, ln.rb_c2, 4, nullptr, 0, s, err)) return false;
       HIP_OK(hipStreamSynchronize(s));
-      const unsigned int c2 = *ln.rb_c2.as<unsigned int>();
+      const unsigned int c2 = h_cnt[1];
       float k2 = 0;
       HIP_OK(hipEventElapsedTime(&k2, ln.ev[2], ln.ev[3]));
       st->k2_ms += k2;
       if (c2 > ln.cand_cap) { ln.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
       auto t_d2h = std::chrono::steady_clock::now();
-      if (!ensure_pinned(&ln.rb_cands, c2 * sizeof(CandDev), err) ||
-          !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
-          !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err)) return false;
-      if (c2) HIP_OK(hipMemcpyAsync(ln.rb_cands.p, ln.d_cands, c2 * sizeof(CandDev), hipMemcpyDeviceToHost, s));
-      if (in.nfiles) HIP_OK(hipMemcpyAsync(ln.rb_ff.p, ln.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      if (nchunks) HIP_OK(hipMemcpyAsync(ln.rb_nl.p, ln.d_nl, nchunks * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-      HIP_OK(hipStreamSynchronize(s));
       out->cands.assign(ln.rb_cands.as<CandDev>(), ln.rb_cands.as<CandDev>() + c2);
       out->ff.assign(ln.rb_ff.as<uint32_t>(), ln.rb_ff.as<uint32_t>() + in.nfiles);
       out->nl.assign(ln.rb_nl.as<uint16_t>(), ln.rb_nl.as<uint16_t>() + nchunks);
