@@ -17,6 +17,8 @@ layout:
   phase     freq + every state's row start placed so its bank phase
             ((row dword) mod 32) is chosen greedily against the states that
             are live together, with padding in LDS
+  rootrep   current + the root row replicated per lane in a transposed
+            layout (a root-state lane always reads its own bank)
 
   python tools/lds_bank_sim.py [--mb 64] [--waves 64] [--layouts current,freq,phase]
 """
@@ -141,6 +143,13 @@ def main():
         tot = 0.0
         for st, cl in waves:
             dw = (256 + 2 * rows[st] + 2 * perm[cl]) // 4
+            if name == "rootrep":
+                # the root row replicated per lane, transposed: lane l reads
+                # class c of the root at dword base + (c / 2) * 32 + l % 32
+                # (bank l % 32 always); other states as current
+                lane = np.arange(dw.shape[1])[None, :] % 32
+                rootdw = (1 << 20) + (perm[cl] // 2) * 32 + lane
+                dw = np.where(st == 0, rootdw, dw)
             tot += cycles(dw)
         results[name] = (tot / len(waves), size * 2)
         print("%-8s LDS cycles per transition read (2 groups, 2.0 = conflict-free): %.3f   table %d B" % (

@@ -854,6 +854,8 @@ struct Lane {
   unsigned int* d_cnt = nullptr;
   uint8_t* d_cr = nullptr; size_t d_cr_cap = 0;     // CR strip scratch (crstrip.hip)
   size_t hit_cap = 1 << 20, cand_cap = 1 << 18, over_cap = 1 << 18;
+  double k2_maxr_per_byte = 0;                       // K2 grid of the next segment: the last one's fullest region
+  uint64_t k2_over_est = 0;                          // per byte, and its overflow hit count
   ~Lane();
 };
 
@@ -1342,93 +1344,92 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       ++launches;
     }
     HIP_OK(hipEventRecord(ln.ev[1], s));
-    // K1's outputs to the host: per-region hit counts, the overflow count and
-    // LDS check (d_cnt[2..3]), and the final file flags and newline counts
-    if (!ensure_pinned(&ln.rb_bh, nregions * sizeof(uint32_t), err) || !ensure_pinned(&ln.rb_c2, 16, err) ||
-        !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
-        !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err) ||
-        !readback(ln.d_bh, ln.rb_bh, nregions, nullptr, 0, s, err) ||
-        !readback(ln.d_cnt, ln.rb_c2, 4, nullptr, 0, s, err) ||
-        !readback(ln.d_ff, ln.rb_ff, in.nfiles, nullptr, 0, s, err) ||
-        !readback(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2, nullptr, 0, s, err)) return false;
-    HIP_OK(hipStreamSynchronize(s));
-    const uint32_t* h_bh = ln.rb_bh.as<const uint32_t>();
-    const uint32_t* h_cnt = ln.rb_c2.as<const uint32_t>();
-    const double t_k1_sync = ms_since(t_seg0);
-    float k1 = 0;
-    HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
-    st->k1_ms += k1;
     st->k1_launches += launches;
-    uint64_t nhits = 0;
-    uint32_t maxr = 0;
-    for (uint32_t r = 0; r < nregions; ++r) { nhits += h_bh[r]; maxr = std::max(maxr, std::min(h_bh[r], region_cap)); }
-    if (h_cnt[3] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
-    const uint32_t nover = h_cnt[2];
-    if (nover > ln.over_cap) {
-      // the overflow pool (shared by every workgroup) was too small: grow it
-      // to the exact need and run K1 again.  Growth follows the batch's total
-      // hit count, not the fullest region times the region count.
-      ln.over_cap = static_cast<size_t>(nover) * 5 / 4 + 1024;
-      if (!ensure(&ln.d_over, &ln.d_over_cap, ln.over_cap, err)) return false;
-      continue;
-    }
-    st->hits += nhits;
-    // K2 (re-run only if the candidate buffer overflows)
-    for (int a2 = 0; a2 < 3; ++a2) {
+    // K2 follows K1 on the stream without a host round trip: its grid is
+    // sized from the lane's previous segment (or the segment's bytes), and
+    // it reads the per-region hit counts and the overflow count on the
+    // device; one readback + sync per segment.  An overflowed hit pool or
+    // candidate buffer is seen afterwards and re-run (grown).
+    bool rerun_k1 = false;
+    for (int a2 = 0; a2 < 3 && !rerun_k1; ++a2) {
       if (!ensure(&ln.d_cands, &ln.d_cands_cap, ln.cand_cap, err)) return false;
       HIP_OK(hipMemsetAsync(ln.d_cnt + 1, 0, 4, s));
       HIP_OK(hipEventRecord(ln.ev[2], s));
-      if (nhits > 0) {
-        // (region, sub-block) grid: k2_hits_per_thread_ hits of the fullest
-        // region per thread (K2 is latency-bound: more threads in flight)
-        const uint64_t per_block = 256ull * k2_hits_per_thread_;
-        const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(256, (maxr + per_block - 1) / per_block)));
-        if (ln.d_k2s)
-          hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
-                             ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
-                             dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt,
-                             static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
-        else
-          hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
-                             ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
-                             dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt,
-                             static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
-        HIP_OK(hipGetLastError());
-        if (nover > 0) {                               // the overflow pool as one more region
-          const uint32_t osub = static_cast<uint32_t>(std::min<uint64_t>(4096, (nover + 1023) / 1024));
-          if (ln.d_k2s)
-            hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles,
-                               ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
-                               dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
-                               ln.d_cnt, static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
-          else
-            hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles,
-                               ln.d_over, ln.d_cnt + 2, static_cast<uint32_t>(ln.over_cap), 1u, dt.anchors, dt.rules,
-                               dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands,
-                               ln.d_cnt, static_cast<uint32_t>(ln.cand_cap), ln.d_k2s);
-          HIP_OK(hipGetLastError());
-        }
+      const uint64_t per_block = 256ull * k2_hits_per_thread_;
+      const uint64_t maxr_est = ln.k2_maxr_per_byte > 0 ? static_cast<uint64_t>(ln.k2_maxr_per_byte * total) + 1
+                                                        : 2 * (total / 2048) / nregions + 1;
+      const uint32_t nsub = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(256, (maxr_est + per_block - 1) / per_block)));
+      const uint32_t osub = static_cast<uint32_t>(std::max<uint64_t>(16, std::min<uint64_t>(4096, (ln.k2_over_est + 1023) / 1024)));
+      const uint32_t ccap = static_cast<uint32_t>(ln.cand_cap);
+      const uint32_t ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
+      // the region grid, then the overflow pool as one more region
+      if (ln.d_k2s) {
+        hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
+                           ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
+                           dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+        hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles, ln.d_over,
+                           ln.d_cnt + 2, ocap, 1u, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa,
+                           dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+      } else {
+        hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
+                           ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
+                           dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+        hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles, ln.d_over,
+                           ln.d_cnt + 2, ocap, 1u, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa,
+                           dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
       }
+      HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));
-      // the candidates (as many as fit) and their count, in one round trip
-      if (!ensure_pinned(&ln.rb_cands, ln.cand_cap * sizeof(CandDev), err) ||
+      // everything to the host in one round trip: per-region hit counts, the
+      // counters (candidates, overflow hits, LDS check), file flags, newline
+      // counts and the candidates (as many as fit)
+      if (!ensure_pinned(&ln.rb_bh, nregions * sizeof(uint32_t), err) || !ensure_pinned(&ln.rb_c2, 16, err) ||
+          !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
+          !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err) ||
+          !ensure_pinned(&ln.rb_cands, ln.cand_cap * sizeof(CandDev), err) ||
+          !readback(ln.d_bh, ln.rb_bh, nregions, nullptr, 0, s, err) ||
+          !readback(ln.d_cnt, ln.rb_c2, 4, nullptr, 0, s, err) ||
+          !readback(ln.d_ff, ln.rb_ff, in.nfiles, nullptr, 0, s, err) ||
+          !readback(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2, nullptr, 0, s, err) ||
           !readback(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4,
-                    s, err) ||
-          !readback(ln.d_cnt, ln.rb_c2, 4, nullptr, 0, s, err)) return false;
+                    s, err)) return false;
       HIP_OK(hipStreamSynchronize(s));
-      const unsigned int c2 = h_cnt[1];
-      float k2 = 0;
+      const double t_k1_sync = ms_since(t_seg0);
+      const uint32_t* h_bh = ln.rb_bh.as<const uint32_t>();
+      const uint32_t* h_cnt = ln.rb_c2.as<const uint32_t>();
+      if (h_cnt[3] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
+      float k1 = 0, k2 = 0;
+      HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
       HIP_OK(hipEventElapsedTime(&k2, ln.ev[2], ln.ev[3]));
+      if (a2 == 0) st->k1_ms += k1;
       st->k2_ms += k2;
+      const uint32_t nover = h_cnt[2];
+      if (nover > ln.over_cap) {
+        // the overflow pool (shared by every workgroup) was too small: grow it
+        // to the exact need and run K1 again.  Growth follows the batch's
+        // total hit count, not the fullest region times the region count.
+        ln.over_cap = static_cast<size_t>(nover) * 5 / 4 + 1024;
+        if (!ensure(&ln.d_over, &ln.d_over_cap, ln.over_cap, err)) return false;
+        rerun_k1 = true;
+        break;
+      }
+      const unsigned int c2 = h_cnt[1];
       if (c2 > ln.cand_cap) { ln.cand_cap = static_cast<size_t>(c2) * 5 / 4 + 1024; continue; }
+      uint64_t nhits = 0;
+      uint32_t maxr = 0;
+      for (uint32_t r = 0; r < nregions; ++r) { nhits += h_bh[r]; maxr = std::max(maxr, std::min(h_bh[r], region_cap)); }
+      ln.k2_maxr_per_byte = total ? static_cast<double>(maxr) * 1.25 / static_cast<double>(total) : 0.0;
+      ln.k2_over_est = nover;
+      st->hits += nhits;
       auto t_d2h = std::chrono::steady_clock::now();
       out->cands.assign(ln.rb_cands.as<CandDev>(), ln.rb_cands.as<CandDev>() + c2);
       out->ff.assign(ln.rb_ff.as<uint32_t>(), ln.rb_ff.as<uint32_t>() + in.nfiles);
       out->nl.assign(ln.rb_nl.as<uint16_t>(), ln.rb_nl.as<uint16_t>() + nchunks);
       st->d2h_ms += ms_since(t_d2h);
       if (host_profile_)
-        std::fprintf(stderr, "[tsg seg] %.1f MB %u files: wall to K1 done %.3f ms (K1 %.3f), K2 %.3f ms, d2h %.3f ms, "
-                     "total %.3f ms\n", total / 1e6, in.nfiles, t_k1_sync, k1, k2, ms_since(t_d2h), ms_since(t_seg0));
+        std::fprintf(stderr, "[tsg seg] %.1f MB %u files: wall to results %.3f ms (K1 %.3f, K2 %.3f, K2 grid %u+%u), "
+                     "copy-out %.3f ms, total %.3f ms\n", total / 1e6, in.nfiles, t_k1_sync, k1, k2, nregions * nsub,
+                     osub, ms_since(t_d2h), ms_since(t_seg0));
       st->candidates += c2;
       if (ln.d_k2s) {
         std::vector<unsigned long long> h(4 * pf_.rules.size());
@@ -1440,6 +1441,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       }
       return true;
     }
+    if (rerun_k1) continue;
     *err = "candidate buffer overflow persisted";
     return false;
   }
