@@ -1127,6 +1127,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // K1 measurement builds (kAbl bits)
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
+  if (e->host_profile_) g_scan_prof_on = true;
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
     const int v = std::atoi(c);
     if (v >= 0 && v <= 16) e->k1_tail_rounds_ = static_cast<uint32_t>(v);
@@ -1668,10 +1669,15 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
     work_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(b - a).count());
     light_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - b).count());
   });
-  if (host_profile_)
+  if (host_profile_) {
+    uint64_t ph[5];
+    for (int k = 0; k < 5; ++k) ph[k] = g_scan_prof[k].exchange(0);
     std::fprintf(stderr, "[tsg host] files %u (work %zu, light %zu) cands %zu: setup %.2f ms, wall %.2f ms, "
-                 "work %.1f + light %.1f thread-ms on %d threads\n", in.nfiles, work.size(), light.size(),
-                 g.cands.size(), t_setup, ms_since(t_begin), work_us.load() / 1e3, light_us.load() / 1e3, active);
+                 "work %.1f + light %.1f thread-ms on %d threads; scan_file thread-ms: keywords %.1f, find %.1f, "
+                 "blocks %.1f, findings %.1f, sort %.1f\n", in.nfiles, work.size(), light.size(),
+                 g.cands.size(), t_setup, ms_since(t_begin), work_us.load() / 1e3, light_us.load() / 1e3, active,
+                 ph[0] / 1e6, ph[1] / 1e6, ph[2] / 1e6, ph[3] / 1e6, ph[4] / 1e6);
+  }
   *nconf_out += nconf.load();
   *nfind_out += nfind.load();
 }

@@ -6,6 +6,7 @@
 #include "prefilter.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -576,8 +577,8 @@ class CensoredView {
   uint64_t count_nl(size_t a, size_t b) const {
     if (b <= a) return 0;
     uint64_t n = orig_nl(a, b);
-    for (const Loc& l : iv_) {
-      size_t x = std::max<size_t>(a, l.start), y = std::min<size_t>(b, l.end);
+    for (auto it = first_ending_after(a); it != iv_.end() && static_cast<size_t>(it->start) < b; ++it) {
+      size_t x = std::max<size_t>(a, it->start), y = std::min<size_t>(b, it->end);
       if (x < y) n -= orig_nl(x, y);
     }
     return n;
@@ -612,8 +613,8 @@ class CensoredView {
   }
   std::string str(size_t a, size_t b) const {
     std::string s(reinterpret_cast<const char*>(c_) + a, b - a);
-    for (const Loc& l : iv_) {
-      size_t x = std::max<size_t>(a, l.start), y = std::min<size_t>(b, l.end);
+    for (auto it = first_ending_after(a); it != iv_.end() && static_cast<size_t>(it->start) < b; ++it) {
+      size_t x = std::max<size_t>(a, it->start), y = std::min<size_t>(b, it->end);
       for (size_t k = x; k < y; ++k) s[k - a] = '*';
     }
     return s;
@@ -629,6 +630,10 @@ class CensoredView {
   uint64_t off_ = 0, first_ = 0;
   uint32_t ch_ = 4096;
 
+  // the merged spans are sorted and disjoint: the first one ending after a
+  std::vector<Loc>::const_iterator first_ending_after(size_t a) const {
+    return std::upper_bound(iv_.begin(), iv_.end(), static_cast<long>(a), [](long v, const Loc& l) { return v < l.end; });
+  }
   uint64_t prefix_at(uint64_t g) const {   // '\n' in data_[first_*ch_, g)
     const uint64_t k = g / ch_;
     uint64_t n = local_[k - first_];
@@ -784,8 +789,29 @@ bool keywords_match_raw(const Rule& r, const uint8_t* content, size_t len, Lower
 
 }  // namespace
 
+bool g_scan_prof_on = false;
+std::atomic<uint64_t> g_scan_prof[5];
+
+namespace {
+struct PhaseClock {
+  bool on = g_scan_prof_on;
+  uint64_t acc[5] = {0, 0, 0, 0, 0};
+  std::chrono::steady_clock::time_point t = on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+  void lap(int k) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    acc[k] += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count());
+    t = n;
+  }
+  ~PhaseClock() {
+    if (on) for (int k = 0; k < 5; ++k) if (acc[k]) g_scan_prof[k].fetch_add(acc[k], std::memory_order_relaxed);
+  }
+};
+}  // namespace
+
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl) {
+  PhaseClock pc;
   Secret out;
   if (global_allow_path(rs, path)) { out.file_path = path; return out; }   // scanner.go:381-386
   std::string lower;
@@ -812,13 +838,16 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
     if (kind == kPlanSkip) continue;
     // a host-gated rule matches only at GPU candidate starts: none, no match
     if (kind == kPlanCandHostGate && (!starts || starts->empty())) continue;
-    if ((kind == kPlanFull || kind == kPlanCandHostGate) && !keywords_match_raw(rule, content, len, lowered)) continue;
-    if (kind == kPlanNoMatch) continue;
+    pc.lap(0);
+    const bool kw_ok = !(kind == kPlanFull || kind == kPlanCandHostGate) || keywords_match_raw(rule, content, len, lowered);
+    pc.lap(0);
+    if (!kw_ok || kind == kPlanNoMatch) continue;
     locs.clear();
     static const std::vector<uint64_t> kEmpty;
     const std::vector<uint64_t>* use = nullptr;
     if (kind == kPlanCandidates || kind == kPlanCandHostGate) use = starts ? starts : &kEmpty;
     find_locations(rs, rule, content, len, use, &locs, &out.error);
+    pc.lap(1);
     if (locs.empty()) continue;
     Blocks lblocks(content, len, rule.exclude_block, plan, rs.rules.size() + rule.exclude_base);
     for (const Loc& l : locs) {
@@ -826,6 +855,7 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
       if (gblocks.match(l) || lblocks.match(l)) continue;
       matched.push_back({&rule, l});                  // censorLocation: applied virtually below
     }
+    pc.lap(2);
   }
   if (matched.empty()) return out;                    // types.Secret{}
   std::vector<Loc> spans;
@@ -843,6 +873,7 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
       f.match = put(&out.arena, "Binary file " + go_quote(path) + " matches a rule " + go_quote(m.rule->title));
     }
   }
+  pc.lap(3);
   auto& fs = out.findings;
   const std::string& ar = out.arena;
   GoSort<FindingRec>(&fs, [&fs, &ar](size_t i, size_t j) {
@@ -850,6 +881,7 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
     return ar.compare(fs[i].match.off, fs[i].match.len, ar, fs[j].match.off, fs[j].match.len) < 0;
   }).run();
   out.file_path = path;
+  pc.lap(4);
   return out;
 }
 

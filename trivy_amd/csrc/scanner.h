@@ -3,6 +3,7 @@
 // GPU prefilter produces.  With no plan this is the reference algorithm
 // (every rule's keyword gate and full find-all evaluated on the host).
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -134,6 +135,10 @@ std::string go_str_to_lower(const std::string& s);
 std::string go_quote(const std::string& s);
 
 // Scanner.Scan (scanner.go:377-463).  plan == nullptr: reference algorithm.
+// TSG_HOST_PROFILE: scan_file's time per phase (ns, summed over threads):
+// 0 keyword gate, 1 find_locations, 2 exclude blocks, 3 censor + findings, 4 sort
+extern bool g_scan_prof_on;
+extern std::atomic<uint64_t> g_scan_prof[5];
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl = nullptr);
 
