@@ -833,15 +833,17 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
       while (cand_i < plan->cands.size() && plan->cands[cand_i].rule < ri) ++cand_i;
       if (cand_i < plan->cands.size() && plan->cands[cand_i].rule == ri) starts = &plan->cands[cand_i].starts;
     }
+    // rules the plan rules out (gate false, no match possible, or a
+    // host-gated rule without candidate starts) add nothing whatever their
+    // path filters say: skipped before the path regexes
+    if (kind == kPlanSkip || kind == kPlanNoMatch) continue;
+    if (kind == kPlanCandHostGate && (!starts || starts->empty())) continue;
     if (rule.path && !rule.path->match_string(reinterpret_cast<const uint8_t*>(path.data()), path.size())) continue;
     if (allow_path(rule.allow_rules, path)) continue;
-    if (kind == kPlanSkip) continue;
-    // a host-gated rule matches only at GPU candidate starts: none, no match
-    if (kind == kPlanCandHostGate && (!starts || starts->empty())) continue;
     pc.lap(0);
     const bool kw_ok = !(kind == kPlanFull || kind == kPlanCandHostGate) || keywords_match_raw(rule, content, len, lowered);
     pc.lap(0);
-    if (!kw_ok || kind == kPlanNoMatch) continue;
+    if (!kw_ok) continue;
     locs.clear();
     static const std::vector<uint64_t> kEmpty;
     const std::vector<uint64_t>* use = nullptr;
