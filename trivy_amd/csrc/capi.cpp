@@ -6,6 +6,7 @@
 #include <atomic>
 #include <chrono>
 #include <memory>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -467,6 +468,11 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   const uint32_t ch = 2048;
   const uint64_t total = nfiles ? offsets[nfiles] : 0;
   std::vector<uint16_t> chunk_nl((total + ch - 1) / ch, 0);   // exactly K1's chunk count
+  // TSG_HOST_PROFILE=1: the confirmer's time per phase on stderr (the same
+  // scan_file the engine runs, here on one thread, for CPU profiling)
+  const bool prof = std::getenv("TSG_HOST_PROFILE") && std::atoi(std::getenv("TSG_HOST_PROFILE")) != 0;
+  if (prof) { g_scan_prof_on = true; for (auto& a : g_scan_prof) a.store(0); }
+  uint64_t conf_ns = 0;
   for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += data[x] == '\n';
   for (uint32_t f = 0; f < nfiles; ++f) {
     const uint8_t* c = data + offsets[f];
@@ -482,7 +488,14 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
     nls.data = data;
     nls.file_off = offsets[f];
     nls.chunk = ch;
+    const auto t_conf = std::chrono::steady_clock::now();
     r->files[f] = scan_file(*rs->rs, path_of(paths, path_lens, f), c, len, binary ? binary[f] != 0 : false, &plan, &nls);
+    conf_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_conf).count();
+  }
+  if (prof) {
+    std::fprintf(stderr, "[tsg model] confirm %.1f ms: keywords %.1f, find %.1f, blocks %.1f, findings %.1f, sort %.1f\n",
+                 conf_ns / 1e6, g_scan_prof[0].load() / 1e6, g_scan_prof[1].load() / 1e6, g_scan_prof[2].load() / 1e6,
+                 g_scan_prof[3].load() / 1e6, g_scan_prof[4].load() / 1e6);
   }
   *out = r;
   return TSG_OK;
