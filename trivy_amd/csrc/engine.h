@@ -110,8 +110,8 @@ class Engine {
   bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr
   std::mutex k2s_mu_;
   std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
-  uint32_t pieces_ = 2;                 // resident data: pipeline pieces (TSG_PIECES)
-  double first_piece_ = 0.7;            // resident data: share of the first piece (TSG_FIRST_PIECE)
+  uint32_t pieces_ = 4;                 // resident data: pipeline pieces (TSG_PIECES; r3za config 2: 4 pieces, first 10%: 1286 GB/s, 2 at 70/30: 919)
+  double first_piece_ = 0.1;            // resident data: share of the first piece (TSG_FIRST_PIECE)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
   uint64_t segment_min_ = 128ull << 20;  // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1)
   uint64_t segment_tail_ = 0;           // uploaded data: a short last segment (TSG_SEGMENT_TAIL; 0 = none: the
