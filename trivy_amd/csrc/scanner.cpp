@@ -628,13 +628,16 @@ class CensoredView {
     }
     return n_;
   }
-  std::string str(size_t a, size_t b) const {
-    std::string s(reinterpret_cast<const char*>(c_) + a, b - a);
+  // the censored bytes [a, b) appended to `arena` (no temporary string)
+  StrRef put(std::string* arena, size_t a, size_t b) const {
+    StrRef r{static_cast<uint32_t>(arena->size()), static_cast<uint32_t>(b - a)};
+    arena->append(reinterpret_cast<const char*>(c_) + a, b - a);
+    char* d = &(*arena)[r.off];
     for (auto it = first_ending_after(a); it != iv_.end() && static_cast<size_t>(it->start) < b; ++it) {
       size_t x = std::max<size_t>(a, it->start), y = std::min<size_t>(b, it->end);
-      for (size_t k = x; k < y; ++k) s[k - a] = '*';
+      for (size_t k = x; k < y; ++k) d[k - a] = '*';
     }
-    return s;
+    return r;
   }
   size_t size() const { return n_; }
 
@@ -682,7 +685,7 @@ void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlin
     line_start = (static_cast<long>(start) - static_cast<long>(line_start) - 30 < 0) ? line_start : start - 30;
     line_end = (end + 20 > line_end) ? line_end : end + 20;
   }
-  f.match = put(&out->arena, cv.str(line_start, line_end));
+  f.match = cv.put(&out->arena, line_start, line_end);
   const size_t end_line = start_line + cv.count_nl(start, end);
   const size_t code_start = start_line >= 2 ? start_line - 2 : 0;
   const size_t code_end = std::min<size_t>(end_line + 2, nlines);
@@ -719,8 +722,8 @@ void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlin
     const bool in_cause = k >= start_line && k <= end_line;
     LineRec ln;
     ln.number = static_cast<int>(k + 1);
-    if (e - b > 100) ln.content = in_cause ? f.match : put(&out->arena, cv.str(b, b + 100));
-    else ln.content = put(&out->arena, cv.str(b, e));
+    if (e - b > 100) ln.content = in_cause ? f.match : cv.put(&out->arena, b, b + 100);
+    else ln.content = cv.put(&out->arena, b, e);
     ln.is_cause = in_cause;
     ln.first_cause = !found_first && in_cause;
     found_first = found_first || in_cause;
