@@ -6,6 +6,7 @@
 #include "prefilter.h"
 
 #include <algorithm>
+#include <emmintrin.h>
 #include <chrono>
 #include <cstring>
 #include <functional>
@@ -754,16 +755,31 @@ bool ascii_ci_find(const uint8_t* s, size_t n, const std::string& kw) {
   const uint8_t k0 = static_cast<uint8_t>(kw[0]);
   const bool alpha0 = k0 >= 'a' && k0 <= 'z';
   const uint8_t u0 = alpha0 ? static_cast<uint8_t>(k0 - 32) : k0;
-  for (size_t i = 0; i + m <= n; ++i) {
-    const uint8_t c = s[i];
-    if (c != k0 && c != u0) continue;
-    size_t j = 1;
-    for (; j < m; ++j) {
+  auto at = [&](size_t i) {
+    for (size_t j = 1; j < m; ++j) {
       uint8_t b = s[i + j];
       if (b >= 'A' && b <= 'Z') b = static_cast<uint8_t>(b + 32);
-      if (b != static_cast<uint8_t>(kw[j])) break;
+      if (b != static_cast<uint8_t>(kw[j])) return false;
     }
-    if (j == m) return true;
+    return true;
+  };
+  const size_t last = n - m;                     // candidate starts 0..last
+  size_t i = 0;
+  // 16 starts at a time: positions whose byte is the first keyword byte in
+  // either case (SSE2 compares), then the rest of the keyword
+  const __m128i v0 = _mm_set1_epi8(static_cast<char>(k0)), v1 = _mm_set1_epi8(static_cast<char>(u0));
+  for (; i + 16 <= last + 1; i += 16) {
+    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
+    uint32_t mask = static_cast<uint32_t>(_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, v0), _mm_cmpeq_epi8(x, v1))));
+    while (mask) {
+      const size_t k = i + static_cast<size_t>(__builtin_ctz(mask));
+      if (at(k)) return true;
+      mask &= mask - 1;
+    }
+  }
+  for (; i <= last; ++i) {
+    const uint8_t c = s[i];
+    if ((c == k0 || c == u0) && at(i)) return true;
   }
   return false;
 }
