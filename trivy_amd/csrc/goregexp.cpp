@@ -6,6 +6,7 @@
 #include <unordered_map>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cstring>
 
@@ -865,6 +866,82 @@ class Machine {
     return matched_;
   }
 
+  // Go's backtrack.go for an anchored leftmost-first match whose threads
+  // consume at most `window` bytes past pos0: every (pc, pos) pair is
+  // explored once, in priority order (the Pike VM's thread order), so the
+  // first Match reached is the VM's match with the same submatches.
+  // Returns 1 match, 0 none, -1 a thread ran past the window (caller: VM).
+  int backtrack(const uint8_t* s, size_t len, size_t pos0, size_t window, Cap* caps_out) {
+    const size_t end = std::min(len, pos0 + window);
+    const size_t npos = end - pos0 + 1;
+    visited_.assign((p_.inst.size() * npos + 31) / 32, 0u);
+    const int nc = std::max(ncap_, 2);
+    bcap_.assign(nc, -1);
+    jobs_.clear();
+    jobs_.push_back({p_.start, pos0, -1, 0});
+    while (!jobs_.empty()) {
+      const BJob j = jobs_.back();
+      jobs_.pop_back();
+      if (j.slot >= 0) { bcap_[j.slot] = j.old; continue; }
+      uint32_t pc = j.pc;
+      size_t pos = j.pos;
+      for (;;) {
+        if (pc == 0) break;
+        const size_t bit = static_cast<size_t>(pc) * npos + (pos - pos0);
+        if (visited_[bit >> 5] & (1u << (bit & 31))) break;
+        visited_[bit >> 5] |= 1u << (bit & 31);
+        const Inst& in = p_.inst[pc];
+        bool fail = false;
+        switch (in.op) {
+          case IOp::Fail: fail = true; break;
+          case IOp::Alt: case IOp::AltMatch:
+            jobs_.push_back({in.arg, pos, -1, 0});
+            pc = in.out;
+            break;
+          case IOp::Nop: pc = in.out; break;
+          case IOp::Capture:
+            if (static_cast<int>(in.arg) < ncap_) {
+              jobs_.push_back({0, 0, static_cast<int>(in.arg), bcap_[in.arg]});
+              bcap_[in.arg] = static_cast<Cap>(pos);
+            }
+            pc = in.out;
+            break;
+          case IOp::Empty: {
+            int32_t r; int w;
+            decode_rune(s + pos, len - pos, &r, &w);
+            const uint8_t flag = empty_context(pos == 0 ? -1 : rune_before(s, pos), r);
+            if (in.arg & ~flag) fail = true; else pc = in.out;
+            break;
+          }
+          case IOp::Match:
+            bcap_[0] = static_cast<Cap>(pos0);
+            bcap_[1] = static_cast<Cap>(pos);
+            if (caps_out && ncap_ > 0) std::copy(bcap_.begin(), bcap_.begin() + ncap_, caps_out);
+            return 1;
+          default: {   // Rune*: consume one rune
+            int32_t c; int w;
+            decode_rune(s + pos, len - pos, &c, &w);
+            bool ok = false;
+            switch (in.op) {
+              case IOp::Rune: ok = rune_match(p_, in, c); break;
+              case IOp::Rune1: ok = c == static_cast<int32_t>(in.arg); break;
+              case IOp::RuneAny: ok = c >= 0; break;
+              case IOp::RuneAnyNotNL: ok = c >= 0 && c != '\n'; break;
+              default: break;
+            }
+            if (!ok) { fail = true; break; }
+            if (pos + w > end) return -1;
+            pos += w;
+            pc = in.out;
+            break;
+          }
+        }
+        if (fail) break;
+      }
+    }
+    return 0;
+  }
+
  private:
   const Prog& p_;
   int ncap_;
@@ -877,6 +954,10 @@ class Machine {
   uint8_t first_[256] = {0};
   struct Frame { uint32_t pc; int slot; Cap old; };
   std::vector<Frame> stack_;
+  struct BJob { uint32_t pc; size_t pos; int slot; Cap old; };   // slot >= 0: a capture restore
+  std::vector<BJob> jobs_;
+  std::vector<uint32_t> visited_;
+  std::vector<Cap> bcap_;
 
   bool contains(int q, uint32_t pc) const {
     uint32_t j = sparse_[q][pc];
@@ -1274,6 +1355,55 @@ int span_shape(const Node& ast, std::string* l1, std::string* l2) {
 
 static bool begins_with_text_start(const Node& n);
 
+// Longest match of n in bytes, -1 when unbounded.  A rune node takes at most
+// the UTF-8 length of its largest rune (an invalid byte decodes to U+FFFD
+// with width 1, never more).
+static long max_width(const Node& n) {
+  auto rune_bytes = [](uint32_t r) -> long { return r < 0x80 ? 1 : r < 0x800 ? 2 : r < 0x10000 ? 3 : 4; };
+  switch (n.op) {
+    case Op::NoMatch: case Op::EmptyMatch: case Op::BeginLine: case Op::EndLine: case Op::BeginText:
+    case Op::EndText: case Op::WordBoundary: case Op::NoWordBoundary:
+      return 0;
+    case Op::Literal: return rune_bytes(n.rune);
+    case Op::CharClass: {
+      uint32_t hi = 0;
+      for (const Range& r : n.ranges) hi = std::max(hi, r.hi);
+      return n.ranges.empty() ? 0 : rune_bytes(hi);
+    }
+    case Op::AnyChar: case Op::AnyCharNotNL: return 4;
+    case Op::Capture: case Op::Quest: return n.sub.empty() ? 0 : max_width(*n.sub[0]);
+    case Op::Star: case Op::Plus: {
+      const long w = n.sub.empty() ? 0 : max_width(*n.sub[0]);
+      return w == 0 ? 0 : -1;
+    }
+    case Op::Repeat: {
+      const long w = n.sub.empty() ? 0 : max_width(*n.sub[0]);
+      if (w < 0) return -1;
+      if (w == 0) return 0;
+      return n.max < 0 ? -1 : w * n.max;
+    }
+    case Op::Concat: {
+      long t = 0;
+      for (const auto& c : n.sub) {
+        const long w = max_width(*c);
+        if (w < 0) return -1;
+        t += w;
+      }
+      return t;
+    }
+    case Op::Alternate: {
+      long t = 0;
+      for (const auto& c : n.sub) {
+        const long w = max_width(*c);
+        if (w < 0) return -1;
+        t = std::max(t, w);
+      }
+      return t;
+    }
+  }
+  return -1;
+}
+
 std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string* err) {
   static std::atomic<uint64_t> next_id{1};
   auto re = std::unique_ptr<Regexp>(new Regexp());
@@ -1293,6 +1423,7 @@ std::unique_ptr<Regexp> Regexp::compile(const std::string& pattern, std::string*
   compute_first(&re->prog_);
   re->span_shape_ = span_shape(*re->ast_, &re->span_l1_, &re->span_l2_);
   re->start_anchored_ = begins_with_text_start(*re->ast_);
+  re->max_width_ = max_width(*re->ast_);
   return re;
 }
 
@@ -1310,6 +1441,16 @@ bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored
   if (slot.first != id_ || !slot.second) {
     slot.second.reset(new Machine(prog_, 2 * (prog_.num_cap + 1)));
     slot.first = id_;
+  }
+  // TSG_RE_NO_BACKTRACK=1: the Pike VM only (differential tests)
+  static const bool no_bt = std::getenv("TSG_RE_NO_BACKTRACK") && std::atoi(std::getenv("TSG_RE_NO_BACKTRACK")) != 0;
+  if (!no_bt && anchored && max_width_ >= 0 && pos <= len) {
+    // Go's bit-state limit: (program size) x (window + 1) <= 256 Kbit
+    const size_t window = std::min<size_t>(static_cast<size_t>(max_width_), len - pos);
+    if (prog_.inst.size() * (window + 1) <= 256 * 1024) {
+      const int r = slot.second->backtrack(text, len, pos, window, caps);
+      if (r >= 0) return r == 1;
+    }
   }
   return slot.second->match(text, len, pos, anchored, caps);
 }

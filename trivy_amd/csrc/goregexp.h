@@ -169,6 +169,8 @@ class Regexp {
   // anchored leftmost-first end is the last (greedy) / first (lazy) L2 after L1
   int span_shape_ = 0;               // 0 none, 1 greedy star, 2 lazy star
   std::string span_l1_, span_l2_;
+  long max_width_ = -1;              // longest match in bytes (-1: unbounded); anchored submatches of a
+                                     // bounded regexp take the backtracker (Go's backtrack.go)
 };
 
 }  // namespace re
