@@ -1068,8 +1068,14 @@ class LazyDfa {
   // -1: no match; -2: state budget exceeded (caller falls back to the VM)
   long match_end(const uint8_t* s, size_t len, size_t pos) {
     const int32_t pr = pos == 0 ? -1 : rune_before(s, pos);
-    seeds_.assign(1, p_.start);
-    int st = intern(seeds_, cat(pr));
+    const uint8_t c0 = cat(pr);
+    int st = start_[c0];                             // the start state per previous-rune category
+    if (st < 0) {
+      seeds_.assign(1, p_.start);
+      st = intern(seeds_, c0);
+      if (st < 0) return -2;                         // state budget exceeded
+      start_[c0] = st;
+    }
     long end = -1;
     size_t p = pos;
     for (;;) {
@@ -1101,6 +1107,7 @@ class LazyDfa {
     int8_t eot = -1;
   };
   static constexpr size_t kMaxStates = 4096;
+  int start_[4] = {-1, -1, -1, -1};
   const Prog& p_;
   std::vector<uint32_t> rinst_;
   int ascii_cls_[128];
