@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256) void tsg_readback(const uint4* __restrict__ sr
                                                     uint32_t nwords, const uint32_t* __restrict__ count,
                                                     uint32_t per_count) {
   uint32_t n = nwords;
-  if (count) n = min(n, *count * per_count);
+  if (count) n = static_cast<uint32_t>(min(static_cast<unsigned long long>(n),
+                                           static_cast<unsigned long long>(*count) * per_count));
   const uint32_t n4 = (n + 3) / 4;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) dst[i] = src[i];
 }
