@@ -221,6 +221,16 @@ int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, ui
  * Pike VM (vm_end).  Never used by tsg_scan_batch. */
 int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
                     int64_t* dfa_end, int64_t* vm_end);
+/* Test hook for the Go sort.Slice restatement (gosort.h, pdqsort_func of
+ * go1.23 sort/zsortfunc.go as scanner.go:452-457 uses it): order[] = 0..n-1
+ * sorted by keys[order[i]] < keys[order[j]] -- unstable, so ties keep Go's
+ * order only if the algorithm is Go's.  Never used by tsg_scan_batch. */
+int tsg_test_go_sort(const uint32_t* keys, size_t n, uint32_t* order);
+/* Test hook for the engine's readback kernel (tsg_readback, engine.hip) on
+ * HIP device 0: copies min(nwords, count * per_count) dwords (the product in
+ * 64 bits) of a device buffer filled with 1, 2, ... into host-mapped memory;
+ * *copied = the dwords that arrived.  Never used by tsg_scan_batch. */
+int tsg_test_readback(uint32_t nwords, uint32_t count, uint32_t per_count, uint32_t* copied);
 
 /* ---- host feed ----
  * Batched SecretAnalyzer.Required + Analyze content preparation, replacing the

@@ -204,8 +204,8 @@ def _raw_header(name, size, typeflag):
     return bytes(h)
 
 
-def _pax_layer(size_value, body=b"A" * 700):
-    rec = b"size=" + size_value + b"\n"
+def _pax_layer(size_value, body=b"A" * 700, key=b"size"):
+    rec = key + b"=" + size_value + b"\n"
     n = len(rec) + len(str(len(rec) + 3)) + 1            # "%d " + record, the length counting itself
     rec = b"%d " % n + rec
     pad = lambda b: b + bytes(-len(b) % 512)
@@ -232,3 +232,18 @@ def test_pax_size_overrides_header_size():
     # PAX size past the end of the archive: unexpected EOF, not an over-read
     with pytest.raises(S.WalkError, match="unexpected EOF"):
         S.PrepareLayerTar(S.Scanner(None), _pax_layer(b"%d" % (1 << 40), body))
+
+
+@pytest.mark.parametrize("key", [b"path", b"linkpath", b"uname", b"gname"])
+def test_pax_nul_in_value_is_header_error(key):
+    # archive/tar validPAXRecord: the values of path, linkpath, uname and
+    # gname may not hold a NUL (ErrHeader -> the layer fails to extract)
+    with pytest.raises(S.WalkError, match="failed to extract the archive"):
+        S.PrepareLayerTar(S.Scanner(None), _pax_layer(b"a\0b", key=key))
+
+
+def test_pax_nul_in_other_value_is_accepted():
+    # ... any other record may carry a NUL in its value (only its key is checked)
+    got, walk = S.PrepareLayerTar(S.Scanner(None), _pax_layer(b"a\0b", body=b"ghp_" + b"x" * 300,
+                                                              key=b"comment"))
+    assert walk["files"] == ["f.txt"]

@@ -134,3 +134,27 @@ def test_nested_repeat_product_limit():
                 "(a{1001,})", "(x{2,3}y{3}){400}"):
         with pytest.raises(Exception, match="invalid repeat count"):
             _probe(bad, b"a")
+
+
+def test_lazy_dfa_state_budget_start_state():
+    # (a|b)*a(a|b){20} has ~2^21 DFA states: a walk over random a/b text adds
+    # one state per byte until the 4096-state budget.  For some text length the
+    # first walk (start category: begin of text) ends with the cache exactly
+    # full; the next position's start state (previous rune 'a' or 'b', a word
+    # character) then cannot be interned: match_end must fall back to the Pike
+    # VM (goregexp.cpp LazyDfa::match_end, the budget check on the start
+    # state), not read a state that was never created.  Every length around
+    # the budget is probed, each position compared with the VM.
+    rng = random.Random(4096)
+    pattern = r"(a|b)*a(a|b){20}"
+    for n in range(4080, 4112):
+        text = "".join(rng.choice("ab") for _ in range(n)).encode()
+        L = _lib.lib()
+        buf = np.frombuffer(text + b"\0", dtype=np.uint8)
+        pos = np.array([0, 1, 2, n // 2, 0, n], dtype=np.uint64)
+        d = np.zeros(len(pos), dtype=np.int64)
+        v = np.zeros(len(pos), dtype=np.int64)
+        _lib.check(L.tsg_regex_probe(pattern.encode(), buf.ctypes.data, len(text), pos.ctypes.data, len(pos),
+                                     d.ctypes.data, v.ctypes.data))
+        assert (d == v).all(), (n, d, v)
+        assert v[0] >= 0

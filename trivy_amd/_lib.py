@@ -74,6 +74,9 @@ SIGNATURES = [
                                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
     ("tsg_result_free", None, [ctypes.c_void_p]),
     ("tsg_free", None, [ctypes.c_void_p]),
+    ("tsg_test_go_sort", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("tsg_test_readback", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.POINTER(ctypes.c_uint32)]),
     ("tsg_scan_host_reference", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                 c_char_pp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_void_p)]),

@@ -17,6 +17,7 @@
 #include <pthread.h>
 
 #include "engine.h"
+#include "gosort.h"
 #include "feed.h"
 #include "tar.h"
 #include "prefilter.h"
@@ -32,6 +33,18 @@ extern "C" const char* tsg_builtin_json_ptr();   // scanner.cpp
 namespace {
 thread_local std::string g_err;
 int fail(int code, const std::string& m) { g_err = m; return code; }
+// No C++ exception crosses the C ABI: an allocation failure (a huge batch,
+// a hostile size field) or any other escaping exception becomes an error code
+// with its message in tsg_last_error().
+#define TSG_API_TRY try {
+#define TSG_API_CATCH                                                                          \
+  } catch (const std::bad_alloc&) {                                                            \
+    return fail(TSG_ERR_INTERNAL, "out of memory");                                            \
+  } catch (const std::exception& ex_) {                                                        \
+    return fail(TSG_ERR_INTERNAL, std::string("internal error: ") + ex_.what());                \
+  } catch (...) {                                                                              \
+    return fail(TSG_ERR_INTERNAL, "internal error");                                           \
+  }
 }  // namespace
 
 struct tsg_ruleset {
@@ -67,6 +80,7 @@ const char* tsg_last_error(void) { return g_err.c_str(); }
 const char* tsg_version(void) { return "trivy-secret-mi355x 0.1 (gfx950)"; }
 
 int tsg_ruleset_compile(const char* config_json, size_t config_len, tsg_ruleset** out) {
+  TSG_API_TRY
   if (!out) return fail(TSG_ERR_INVALID, "out is NULL");
   std::string err;
   auto rs = std::make_shared<Ruleset>();
@@ -80,6 +94,7 @@ int tsg_ruleset_compile(const char* config_json, size_t config_len, tsg_ruleset*
   }
   *out = new tsg_ruleset{rs};
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 void tsg_ruleset_free(tsg_ruleset* rs) { delete rs; }
@@ -92,13 +107,16 @@ const char* tsg_ruleset_rule_id(const tsg_ruleset* rs, int i) {
 }
 
 int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len) {
+  TSG_API_TRY
   if (!rs) return fail(TSG_ERR_INVALID, "ruleset is NULL");
   return global_allow_path(*rs->rs, reinterpret_cast<const uint8_t*>(path), len) ? 1 : 0;
+  TSG_API_CATCH
 }
 
 int tsg_device_count(void) { return device_count(); }
 
 int tsg_engine_create(const tsg_ruleset* rs, uint64_t device_mask, tsg_engine** out) {
+  TSG_API_TRY
   if (!rs || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string err;
   const int n = device_count();
@@ -121,6 +139,7 @@ int tsg_engine_create(const tsg_ruleset* rs, uint64_t device_mask, tsg_engine** 
   e->eng = std::move(eng);
   *out = e;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 void tsg_engine_destroy(tsg_engine* e) { delete e; }
@@ -154,18 +173,23 @@ static int do_scan(tsg_engine* e, const void* d_data, const uint8_t* h_data, con
 
 int tsg_scan_batch(tsg_engine* e, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                    const char* const* paths, const uint32_t* path_lens, const uint8_t* binary, tsg_result** out) {
+  TSG_API_TRY
   return do_scan(e, nullptr, data, offsets, nfiles, paths, path_lens, binary, out);
+  TSG_API_CATCH
 }
 
 int tsg_scan_batch_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data, const uint64_t* offsets,
                             uint32_t nfiles, const char* const* paths, const uint32_t* path_lens,
                             const uint8_t* binary, tsg_result** out) {
+  TSG_API_TRY
   if (!d_data) return fail(TSG_ERR_INVALID, "d_data is NULL");
   return do_scan(e, d_data, h_data, offsets, nfiles, paths, path_lens, binary, out);
+  TSG_API_CATCH
 }
 
 int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data, const uint64_t* offsets,
                            uint32_t nfiles, tsg_result** out) {
+  TSG_API_TRY
   if (!e || !out || !offsets) return fail(TSG_ERR_INVALID, "NULL argument");
   BatchInput in;
   in.h_data = h_data;
@@ -178,32 +202,39 @@ int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_d
   r->files.resize(nfiles);
   *out = r;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_feed_probe(tsg_engine* e, const uint8_t* data, uint64_t bytes, double* ms) {
+  TSG_API_TRY
   if (!e || !ms || (bytes && !data)) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string err;
   if (!e->eng->feed_probe(data, bytes, ms, &err)) return fail(TSG_ERR_HIP, err);
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_strip_cr_device(tsg_engine* e, const void* d_src, const uint64_t* d_offsets, uint32_t nfiles, uint64_t total,
                         void* d_dst, uint64_t* d_new_offsets, uint64_t* out_total, double* ms) {
+  TSG_API_TRY
   if (!e || !d_offsets || !d_new_offsets || !out_total) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string err;
   if (!e->eng->strip_cr(d_src, d_offsets, nfiles, total, d_dst, d_new_offsets, out_total, ms, &err))
     return fail(err.find("CR strip:") == 0 || err.find("aligned") != std::string::npos ? TSG_ERR_INVALID : TSG_ERR_HIP,
                 err);
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 uint32_t tsg_result_num_files(const tsg_result* r) { return r ? static_cast<uint32_t>(r->files.size()) : 0; }
 
 int tsg_result_file_path(const tsg_result* r, uint32_t f, const char** path, size_t* len) {
+  TSG_API_TRY
   if (!r || f >= r->files.size()) return fail(TSG_ERR_INVALID, "file index out of range");
   *path = r->files[f].file_path.data();
   *len = r->files[f].file_path.size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 uint32_t tsg_result_num_findings(const tsg_result* r, uint32_t f) {
@@ -212,11 +243,14 @@ uint32_t tsg_result_num_findings(const tsg_result* r, uint32_t f) {
 }
 
 int tsg_result_file_error(const tsg_result* r, uint32_t f) {
+  TSG_API_TRY
   if (!r || f >= r->files.size()) return 0;
   return r->files[f].error;
+  TSG_API_CATCH
 }
 
 int tsg_result_finding(const tsg_result* r, uint32_t f, uint32_t k, tsg_finding* out) {
+  TSG_API_TRY
   if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
   const Secret& sec = r->files[f];
   const FindingRec& x = sec.findings[k];
@@ -231,9 +265,11 @@ int tsg_result_finding(const tsg_result* r, uint32_t f, uint32_t k, tsg_finding*
   out->match = sec.ptr(x.match); out->match_len = x.match.len;
   out->num_lines = x.line_count;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_result_line(const tsg_result* r, uint32_t f, uint32_t k, uint32_t l, tsg_line* out) {
+  TSG_API_TRY
   if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
   const Secret& sec = r->files[f];
   const FindingRec& x = sec.findings[k];
@@ -248,6 +284,7 @@ int tsg_result_line(const tsg_result* r, uint32_t f, uint32_t k, uint32_t l, tsg
   out->first_cause = ln.first_cause;
   out->last_cause = ln.last_cause;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 static void json_bytes(std::string* o, const char* data, size_t n) {
@@ -280,6 +317,7 @@ static void json_bytes(std::string* o, const char* data, size_t n) {
 static void json_str(std::string* o, const std::string& s) { json_bytes(o, s.data(), s.size()); }
 
 int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
+  TSG_API_TRY
   if (!r || !json) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string o = "[";
   for (size_t f = 0; f < r->files.size(); ++f) {
@@ -334,9 +372,11 @@ int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
   *json = buf;
   if (len) *len = o.size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_result_stats(const tsg_result* r, tsg_stats* out) {
+  TSG_API_TRY
   if (!r || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   const ScanStats& s = r->stats;
   out->k1_ms = s.k1_ms; out->k2_ms = s.k2_ms; out->h2d_ms = s.h2d_ms; out->d2h_ms = s.d2h_ms;
@@ -351,13 +391,16 @@ int tsg_result_stats(const tsg_result* r, tsg_stats* out) {
   out->devices = s.devices;
   out->feed_ms = s.feed_ms;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_result_candidates(const tsg_result* r, uint32_t f, uint32_t rule, const uint64_t** starts, size_t* n) {
+  TSG_API_TRY
   if (!r || f >= r->cands.size() || rule >= r->cands[f].size()) { *starts = nullptr; *n = 0; return TSG_OK; }
   *starts = r->cands[f][rule].data();
   *n = r->cands[f][rule].size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 // Large results are freed on a reaper thread.  A config-5 result (297k
@@ -393,14 +436,24 @@ struct Reaper {
     if (th.joinable()) th.join();
   }
 };
-Reaper* g_reaper = nullptr;
+Reaper* g_reaper = nullptr;       // guarded by g_reaper_mu
+bool g_reaper_closed = false;      // static destruction has begun: results are deleted inline
 std::mutex g_reaper_mu;
 // a forked child has no reaper thread (and maybe a held mutex): leak the
 // parent's state there and start afresh on first use
 void reaper_atfork_child() { g_reaper = nullptr; new (&g_reaper_mu) std::mutex(); }
 struct ReaperOwner {
   ReaperOwner() { pthread_atfork(nullptr, nullptr, reaper_atfork_child); }
-  ~ReaperOwner() { delete g_reaper; g_reaper = nullptr; }
+  ~ReaperOwner() {
+    Reaper* rp = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(g_reaper_mu);
+      rp = g_reaper;
+      g_reaper = nullptr;
+      g_reaper_closed = true;
+    }
+    delete rp;                     // drains its queue, then joins
+  }
 } g_reaper_owner;
 constexpr size_t kReapInlineFiles = 4096;
 }  // namespace
@@ -410,17 +463,18 @@ void tsg_result_free(tsg_result* r) {
   size_t weight = r->files.size();
   for (size_t i = 0; i < r->files.size() && weight < kReapInlineFiles; ++i) weight += r->files[i].findings.size();
   if (weight < kReapInlineFiles) { delete r; return; }
+  std::lock_guard<std::mutex> lk(g_reaper_mu);
+  if (g_reaper_closed) { delete r; return; }
+  if (!g_reaper) {
+    Reaper* rp = new Reaper();
+    rp->th = std::thread([rp] { rp->loop(); });
+    g_reaper = rp;
+  }
   {
-    std::lock_guard<std::mutex> lk(g_reaper_mu);
-    if (!g_reaper) {
-      Reaper* rp = new Reaper();
-      rp->th = std::thread([rp] { rp->loop(); });
-      g_reaper = rp;
-    }
     std::lock_guard<std::mutex> lq(g_reaper->mu);
     g_reaper->q.push_back(r);
   }
-  g_reaper->cv.notify_one();
+  g_reaper->cv.notify_one();       // under g_reaper_mu: the owner cannot delete the reaper meanwhile
 }
 void tsg_free(void* p) { free(p); }
 
@@ -431,6 +485,7 @@ static std::string path_of(const char* const* paths, const uint32_t* lens, uint3
 int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                             const char* const* paths, const uint32_t* path_lens, const uint8_t* binary, int threads,
                             tsg_result** out) {
+  TSG_API_TRY
   if (!rs || !out || !offsets || (nfiles && (!paths || !data))) return fail(TSG_ERR_INVALID, "NULL argument");
   auto* r = new tsg_result();
   r->rs = rs->rs;
@@ -451,11 +506,13 @@ int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const ui
   for (auto& t : pool) t.join();
   *out = r;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                          const char* const* paths, const uint32_t* path_lens, const uint8_t* binary,
                          tsg_result** out) {
+  TSG_API_TRY
   if (!rs || !out || !offsets || (nfiles && (!paths || !data))) return fail(TSG_ERR_INVALID, "NULL argument");
   Prefilter pf;
   std::string err;
@@ -471,7 +528,7 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   // TSG_HOST_PROFILE=1: the confirmer's time per phase on stderr (the same
   // scan_file the engine runs, here on one thread, for CPU profiling)
   const bool prof = std::getenv("TSG_HOST_PROFILE") && std::atoi(std::getenv("TSG_HOST_PROFILE")) != 0;
-  if (prof) { g_scan_prof_on = true; for (auto& a : g_scan_prof) a.store(0); }
+  if (prof) { g_scan_prof_on.store(true, std::memory_order_relaxed); for (auto& a : g_scan_prof) a.store(0); }
   uint64_t conf_ns = 0;
   for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += data[x] == '\n';
   for (uint32_t f = 0; f < nfiles; ++f) {
@@ -499,9 +556,11 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   }
   *out = r;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
+  TSG_API_TRY
   if (!rs || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   Prefilter pf;
   std::string err;
@@ -510,10 +569,12 @@ int tsg_prefilter_report(const tsg_ruleset* rs, char** out) {
   memcpy(buf, pf.report.c_str(), pf.report.size() + 1);
   *out = buf;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, uint8_t** byte_class, uint32_t* nstates,
                       uint32_t* nclasses, uint32_t* first_out) {
+  TSG_API_TRY
   if (!rs || !next || !byte_class || !nstates || !nclasses || !first_out) return fail(TSG_ERR_INVALID, "NULL argument");
   Prefilter pf;
   std::string err;
@@ -531,6 +592,7 @@ int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, ui
   *nclasses = d.t.nclasses;
   *first_out = d.first_out_state;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 const char* tsg_builtin_rules_json(void) { return tsg_builtin_json_ptr(); }
@@ -560,6 +622,7 @@ const char* tsg_secret_rules_metadata_json(void) {
 }
 
 int tsg_go_json_string(const uint8_t* s, size_t n, int escape_html, char** out, size_t* len) {
+  TSG_API_TRY
   if ((n && !s) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string o;
   go_json_string(&o, reinterpret_cast<const char*>(s), n, escape_html != 0);
@@ -570,10 +633,12 @@ int tsg_go_json_string(const uint8_t* s, size_t n, int escape_html, char** out, 
   *out = buf;
   if (len) *len = o.size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, int* gated, int* plain,
                           int* has_gate) {
+  TSG_API_TRY
   if (!pattern || (len && !text) || !gated || !plain || !has_gate) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string err;
   auto rx = re::Regexp::compile(pattern, &err);
@@ -589,10 +654,12 @@ int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, 
   }
   *gated = rx->match_string(text, len) ? 1 : 0;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
                     int64_t* dfa_end, int64_t* vm_end) {
+  TSG_API_TRY
   if (!pattern || (len && !text) || (n && (!pos || !dfa_end || !vm_end))) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string err;
   auto rx = re::Regexp::compile(pattern, &err);
@@ -604,6 +671,28 @@ int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const 
     vm_end[i] = rx->match_at(text, len, pos[i], true, 0, caps.data()) ? caps[1] : -1;
   }
   return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_test_go_sort(const uint32_t* keys, size_t n, uint32_t* order) {
+  TSG_API_TRY
+  if (n && (!keys || !order)) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::vector<uint32_t> v(n);
+  for (size_t i = 0; i < n; ++i) v[i] = static_cast<uint32_t>(i);
+  GoSort<uint32_t>(&v, [&v, keys](size_t i, size_t j) { return keys[v[i]] < keys[v[j]]; }).run();
+  std::copy(v.begin(), v.end(), order);
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_test_readback(uint32_t nwords, uint32_t count, uint32_t per_count, uint32_t* copied) {
+  TSG_API_TRY
+  if (!copied) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::string err;
+  if (!tsg::readback_probe(nwords, count, per_count, copied, &err))
+    return fail(tsg::device_count() > 0 ? TSG_ERR_HIP : TSG_ERR_NO_DEVICE, err);
+  return TSG_OK;
+  TSG_API_CATCH
 }
 
 static std::string cstr(const char* p) { return p ? std::string(p) : std::string(); }
@@ -612,6 +701,7 @@ static std::string cstr(const char* p) { return p ? std::string(p) : std::string
 // names), so report assembly can be checked against the reference's own
 // types.Secret fixtures (e.g. applier/docker_test.go).
 int tsg_result_from_json(const char* json, size_t len, tsg_result** out) {
+  TSG_API_TRY
   if (!json || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   JValue doc;
   std::string err;
@@ -665,9 +755,11 @@ int tsg_result_from_json(const char* json, size_t len, tsg_result** out) {
   }
   *out = r;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_result_to_proto(const tsg_result* r, size_t file, const tsg_layer* layers, char** out, size_t* len) {
+  TSG_API_TRY
   if (!r || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   if (file >= r->files.size()) return fail(TSG_ERR_INVALID, "file index out of range");
   const Secret& s = r->files[file];
@@ -685,9 +777,11 @@ int tsg_result_to_proto(const tsg_result* r, size_t file, const tsg_layer* layer
   *out = buf;
   if (len) *len = msg.size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_result_from_proto(const char* const* msgs, const size_t* lens, size_t n, tsg_result** out) {
+  TSG_API_TRY
   if ((n && (!msgs || !lens)) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   auto r = std::make_unique<tsg_result>();
   r->own_rules = std::make_shared<std::deque<Rule>>();
@@ -702,10 +796,12 @@ int tsg_result_from_proto(const char* const* msgs, const size_t* lens, size_t n,
   }
   *out = r.release();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_report_json(const tsg_result* const* layers, const tsg_layer* layer_refs, uint32_t nlayers,
                     const tsg_result* image_config, const tsg_report_opts* opts, char** out, size_t* len) {
+  TSG_API_TRY
   if ((nlayers && !layers) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   std::vector<const std::vector<Secret>*> ls;
   std::vector<LayerRef> refs;
@@ -752,9 +848,11 @@ int tsg_report_json(const tsg_result* const* layers, const tsg_layer* layer_refs
   *out = buf;
   if (len) *len = doc.size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_image_config_content(const char* config_json, size_t config_len, char** out, size_t* len) {
+  TSG_API_TRY
   if (!config_json || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   std::string doc, err;
   if (!image_config_content(std::string(config_json, config_len), &doc, &err)) return fail(TSG_ERR_INVALID, err);
@@ -765,10 +863,12 @@ int tsg_image_config_content(const char* config_json, size_t config_len, char** 
   *out = buf;
   if (len) *len = doc.size();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_guess_base_layers(const char* config_json, size_t config_len, const char* const* diff_ids, uint32_t n,
                           uint8_t* is_base) {
+  TSG_API_TRY
   if (!config_json || (n && (!diff_ids || !is_base))) return fail(TSG_ERR_INVALID, "NULL argument");
   std::vector<std::string> ids, base;
   for (uint32_t i = 0; i < n; ++i) ids.push_back(cstr(diff_ids[i]));
@@ -776,13 +876,16 @@ int tsg_guess_base_layers(const char* config_json, size_t config_len, const char
   if (!guess_base_layers(std::string(config_json, config_len), ids, &base, &err)) return fail(TSG_ERR_INVALID, err);
   for (uint32_t i = 0; i < n; ++i) is_base[i] = std::find(base.begin(), base.end(), ids[i]) != base.end();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_go_time_rfc3339(const char* in, char* out, size_t cap) {
+  TSG_API_TRY
   std::string t;
   if (!in || !out || !go_time_rfc3339(in, &t) || t.size() + 1 > cap) return fail(TSG_ERR_INVALID, "not an RFC 3339 time");
   memcpy(out, t.c_str(), t.size() + 1);
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 }  // extern "C"
@@ -790,6 +893,7 @@ int tsg_go_time_rfc3339(const char* in, char* out, size_t cap) {
 int tsg_prepare_batch(const tsg_ruleset* rs, const char* config_path, const uint8_t* raw, const uint64_t* raw_offsets,
                       uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
                       tsg_prepared** out) {
+  TSG_API_TRY
   if (!rs || !out || !raw_offsets || (nfiles && (!raw || !paths))) return fail(TSG_ERR_INVALID, "NULL argument");
   auto* p = new tsg_prepared();
   std::string err;
@@ -801,10 +905,12 @@ int tsg_prepare_batch(const tsg_ruleset* rs, const char* config_path, const uint
   }
   *out = p;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_t** offsets, const uint32_t** index,
                       const uint8_t** binary, uint32_t* nkept) {
+  TSG_API_TRY
   if (!p || !data || !offsets || !index || !binary || !nkept) return fail(TSG_ERR_INVALID, "NULL argument");
   *data = p->b.data.get();
   *offsets = p->b.offsets.data();
@@ -812,6 +918,7 @@ int tsg_prepared_view(const tsg_prepared* p, const uint8_t** data, const uint64_
   *binary = p->b.binary.data();
   *nkept = static_cast<uint32_t>(p->b.index.size());
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 void tsg_prepared_free(tsg_prepared* p) { delete p; }
@@ -842,6 +949,7 @@ void json_str_array(std::string* js, const std::vector<std::string>& v) {
 int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const uint8_t* tar, size_t len,
                           const char* const* skip_files, uint32_t nskip_files, const char* const* skip_dirs,
                           uint32_t nskip_dirs, int threads, int pinned, tsg_prepared** out) {
+  TSG_API_TRY
   tsg_feed_opts o{};
   o.config_path = config_path;
   o.skip_files = skip_files;
@@ -851,6 +959,7 @@ int tsg_prepare_layer_tar(const tsg_ruleset* rs, const char* config_path, const 
   o.threads = threads;
   o.pinned = pinned;
   return tsg_prepare_layer_tar_opts(rs, tar, len, &o, out);
+  TSG_API_CATCH
 }
 
 namespace {
@@ -893,6 +1002,7 @@ void set_scan_paths(tsg_prepared* p, const std::vector<std::string>& paths, cons
 int tsg_prepare_batch_opts(const tsg_ruleset* rs, const uint8_t* raw, const uint64_t* raw_offsets, uint32_t nfiles,
                            const char* const* paths, const uint32_t* path_lens, const tsg_feed_opts* opts,
                            tsg_prepared** out) {
+  TSG_API_TRY
   if (!rs || !out || !raw_offsets || (nfiles && (!raw || !paths))) return fail(TSG_ERR_INVALID, "NULL argument");
   FeedOpts fo;
   std::vector<std::string> sf, sd;
@@ -908,10 +1018,12 @@ int tsg_prepare_batch_opts(const tsg_ruleset* rs, const uint8_t* raw, const uint
   }
   *out = p;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_prepare_layer_tar_opts(const tsg_ruleset* rs, const uint8_t* tar, size_t len, const tsg_feed_opts* opts,
                                tsg_prepared** out) {
+  TSG_API_TRY
   if (!rs || !out || (len && !tar)) return fail(TSG_ERR_INVALID, "NULL argument");
   FeedOpts fo;
   std::vector<std::string> sf, sd;
@@ -947,9 +1059,11 @@ int tsg_prepare_layer_tar_opts(const tsg_ruleset* rs, const uint8_t* tar, size_t
   js += "}";
   *out = p;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_opts* opts, tsg_prepared** out) {
+  TSG_API_TRY
   if (!rs || !out || !root) return fail(TSG_ERR_INVALID, "NULL argument");
   FeedOpts fo;
   std::vector<std::string> sf, sd;
@@ -1028,14 +1142,17 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
   js += "}";
   *out = p;
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens) {
+  TSG_API_TRY
   if (!p || !paths || !lens) return fail(TSG_ERR_INVALID, "NULL argument");
   if (p->path_ptrs.size() != p->b.index.size()) return fail(TSG_ERR_INVALID, "not a layer-tar or fs-tree batch");
   *paths = p->path_ptrs.data();
   *lens = p->path_lens.data();
   return TSG_OK;
+  TSG_API_CATCH
 }
 
 const char* tsg_prepared_walk_json(const tsg_prepared* p) { return p ? p->walk_json.c_str() : nullptr; }

@@ -122,4 +122,9 @@ class Engine {
 
 int device_count();
 
+// Test hook (tsg_test_readback): tsg_readback of min(nwords, count * per_count)
+// dwords of a device buffer holding 1, 2, ... into host-mapped memory on
+// device 0; *copied = the dwords that arrived.
+bool readback_probe(uint32_t nwords, uint32_t count, uint32_t per_count, uint32_t* copied, std::string* err);
+
 }  // namespace tsg

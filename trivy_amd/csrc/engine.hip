@@ -918,6 +918,39 @@ int device_count() {
   return n;
 }
 
+bool readback_probe(uint32_t nwords, uint32_t count, uint32_t per_count, uint32_t* copied, std::string* err) {
+  if (device_count() <= 0) { *err = "no HIP device available"; return false; }
+  if (nwords == 0 || nwords > (64u << 20)) { *err = "nwords out of range"; return false; }
+  HIP_OK(hipSetDevice(0));
+  const size_t n4 = (static_cast<size_t>(nwords) + 3) & ~size_t(3);   // the kernel moves 16-byte granules
+  std::vector<uint32_t> h(n4 + 4);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = static_cast<uint32_t>(i + 1);
+  uint32_t* d_src = nullptr;
+  uint32_t* d_cnt = nullptr;
+  PinnedBuf dst;
+  bool ok = false;
+  std::string e2;
+  do {
+    if (hipMalloc(&d_src, h.size() * 4) != hipSuccess || hipMalloc(&d_cnt, 4) != hipSuccess) { e2 = "hipMalloc"; break; }
+    if (hipMemcpy(d_src, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_cnt, &count, 4, hipMemcpyHostToDevice) != hipSuccess) { e2 = "hipMemcpy"; break; }
+    if (!ensure_pinned(&dst, h.size() * 4, &e2)) break;
+    std::memset(dst.p, 0, dst.cap);
+    if (!readback(d_src, dst, nwords, d_cnt, per_count, nullptr, &e2)) break;
+    if (hipDeviceSynchronize() != hipSuccess) { e2 = "hipDeviceSynchronize"; break; }
+    const uint32_t* got = dst.as<const uint32_t>();
+    uint32_t n = 0;
+    while (n < n4 && got[n] == n + 1) ++n;
+    *copied = n;
+    ok = true;
+  } while (false);
+  if (d_src) hipFree(d_src);
+  if (d_cnt) hipFree(d_cnt);
+  if (dst.p) hipHostFree(dst.p);
+  if (!ok) *err = e2;
+  return ok;
+}
+
 namespace {
 
 // Upload the prefilter's tables to one device.
@@ -1128,7 +1161,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // K1 measurement builds (kAbl bits)
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
-  if (e->host_profile_) g_scan_prof_on = true;
+  if (e->host_profile_) g_scan_prof_on.store(true, std::memory_order_relaxed);
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
     const int v = std::atoi(c);
     if (v >= 0 && v <= 16) e->k1_tail_rounds_ = static_cast<uint32_t>(v);

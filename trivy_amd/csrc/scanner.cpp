@@ -819,12 +819,12 @@ bool keywords_match_raw(const Rule& r, const uint8_t* content, size_t len, Lower
 
 }  // namespace
 
-bool g_scan_prof_on = false;
+std::atomic<bool> g_scan_prof_on{false};
 std::atomic<uint64_t> g_scan_prof[5];
 
 namespace {
 struct PhaseClock {
-  bool on = g_scan_prof_on;
+  bool on = g_scan_prof_on.load(std::memory_order_relaxed);
   uint64_t acc[5] = {0, 0, 0, 0, 0};
   std::chrono::steady_clock::time_point t = on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   void lap(int k) {

@@ -137,7 +137,7 @@ std::string go_quote(const std::string& s);
 // Scanner.Scan (scanner.go:377-463).  plan == nullptr: reference algorithm.
 // TSG_HOST_PROFILE: scan_file's time per phase (ns, summed over threads):
 // 0 keyword gate, 1 find_locations, 2 exclude blocks, 3 censor + findings, 4 sort
-extern bool g_scan_prof_on;
+extern std::atomic<bool> g_scan_prof_on;
 extern std::atomic<uint64_t> g_scan_prof[5];
 Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl = nullptr);

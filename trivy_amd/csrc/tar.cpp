@@ -90,9 +90,11 @@ bool parse_pax(const uint8_t* p, size_t n, std::string* path, bool* has_path, in
     const size_t eq = rec.find('=');
     if (eq == std::string::npos) return false;
     const std::string key = rec.substr(0, eq), val = rec.substr(eq + 1);
-    // validPAXRecord: a non-empty key; no NUL in a path value or in any other key
+    // validPAXRecord: a non-empty key; no NUL in the value of path, linkpath,
+    // uname or gname, nor in the key of any other record
     if (key.empty()) return false;
-    if (key == "path" ? val.find('\0') != std::string::npos : key.find('\0') != std::string::npos) return false;
+    const bool value_checked = key == "path" || key == "linkpath" || key == "uname" || key == "gname";
+    if ((value_checked ? val : key).find('\0') != std::string::npos) return false;
     if (key == "path") { *path = val; *has_path = true; }
     else if (key == "size") {
       // strconv.ParseInt(v, 10, 64): optional sign, decimal digits, range
