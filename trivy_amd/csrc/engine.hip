@@ -175,6 +175,7 @@ struct K1Ctx {
   unsigned long long item_base; // first byte of the wave's current item
   uint32_t* w_hitcnt;           // and its fill count
   uint32_t* __restrict__ fflags;
+  uint32_t s0;                  // the start state's value: 0 (K1), the start's packed value (K1c)
 };
 
 // One transition: `s` is the current state's row offset (state * stride, in
@@ -193,6 +194,22 @@ typedef __attribute__((address_space(3))) const uint16_t k1_lds16_t;
 typedef __attribute__((address_space(3))) const uint8_t k1_lds8_t;
 __device__ __forceinline__ uint32_t k1_lds16(uint32_t a) { return *reinterpret_cast<k1_lds16_t*>(a); }
 __device__ __forceinline__ uint32_t k1_lds8(uint32_t a) { return *reinterpret_cast<k1_lds8_t*>(a); }
+typedef __attribute__((address_space(3))) const uint32_t k1_lds32_t;
+typedef __attribute__((address_space(3))) const v4u k1_lds128_t;
+__device__ __forceinline__ uint32_t k1_lds32(uint32_t a) { return *reinterpret_cast<k1_lds32_t*>(a); }
+__device__ __forceinline__ v4u k1_lds128(uint32_t a) { return *reinterpret_cast<k1_lds128_t*>(a); }
+
+// K1c step (prefilter.h CompressedScan): the row entry and the DESC record are
+// both addressed from the packed state, so the two LDS reads issue together;
+// the record's four class slots (class * 4, 0xff = none) pick target A (slots
+// 0-1), target B (slots 2-3) or the row entry.  rep = c4 * 0x01010101.
+__device__ __forceinline__ uint32_t k1c_next(uint32_t s, uint32_t c4, uint32_t rep) {
+  const uint32_t f = k1_lds32(((s >> 16) << 2) + c4);
+  const v4u d = k1_lds128(s & 0xfff0u);
+  const uint32_t x = d.x ^ rep;
+  const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
+  return (z & 0x8080u) ? d.y : ((z & 0x80800000u) ? d.z : f);
+}
 __device__ __forceinline__ bool k1_lds_base_ok(const uint8_t* smem) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((k1_lds8_t*)(smem))) == 0;
 }
@@ -248,7 +265,37 @@ __device__ __forceinline__ void k1_out_v3(const K1Ctx& x, K1Stream& t, uint32_t 
   }
 }
 
+// K1c outputs of output state `st` (packed value; only its DESC address is
+// used): the record's output index selects an OutMeta in global memory
+// (L2-resident; K1c keeps every LDS byte for the table).
+__device__ __forceinline__ void k1_out_c(const K1Ctx& x, K1Stream& t, uint32_t st, unsigned long long q) {
+  const uint32_t oi = k1_lds32((st & 0xfff0u) + 12u);
+  const OutMeta m = x.meta[oi];
+  t.kw0 |= m.kw0;
+  t.kw1 |= m.kw1;
+  for (uint32_t j = 0; j < m.list_count; ++j) {
+    const uint32_t id = x.list[m.list_begin + j];
+    if (id < x.nkw) {
+      or_bits(x.kwbits + static_cast<size_t>(t.f) * x.kw_words + (id >> 5), 1u << (id & 31));
+    } else {
+      const uint32_t li2 = atomicAdd(x.w_hitcnt, 1u);
+      if (li2 < x.wave_hits) {
+        x.w_hits[li2] = (static_cast<uint32_t>(q - x.item_base) << kAnchorBits) | (id - x.nkw);
+      } else {
+        const uint32_t gi = atomicAdd(x.b_hitcnt, 1u);
+        if (gi < x.region_cap) {
+          x.hits[gi] = (q << 24) | (id - x.nkw);
+        } else {
+          const uint32_t oi2 = atomicAdd(x.over_cnt, 1u);
+          if (oi2 < x.over_cap) x.over[oi2] = (q << 24) | (id - x.nkw);
+        }
+      }
+    }
+  }
+}
+
 // One 16-byte word of one stream with file-boundary and stream-end checks.
+template <bool kC>
 __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4], uint32_t S = 0) {
   const unsigned long long end = k1_end(x, t);
   unsigned long long fend = x.offsets[t.f + 1];
@@ -259,14 +306,21 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
     if (q >= fend) {
       flush_kw(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
       do { ++t.f; fend = x.offsets[t.f + 1]; } while (q >= fend);
-      t.s = 0;
+      t.s = x.s0;
       t.p12 = 0;
     }
     const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-    t.s = k1_step(x.next, t.s, x.cls[b]);
+    if constexpr (kC) {
+      const uint32_t c4 = x.cls[b];
+      t.s = k1c_next(t.s, c4, __builtin_amdgcn_perm(0u, c4, 0u));
+    } else {
+      t.s = k1_step(x.next, t.s, x.cls[b]);
+    }
     if (q >= t.emit) {
       t.nl += (b == 0x0au);
-      if (t.s >= x.first_out) {
+      if constexpr (kC) {
+        if (t.s & 1u) k1_out_c(x, t, t.s, q);
+      } else if (t.s >= x.first_out) {
         k1_out_v3(x, t, t.s, q, S);
       }
     }
@@ -280,7 +334,7 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
 __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned long long c0, uint32_t warm_bytes) {
   t.emit = c0;
   t.p = c0 > warm_bytes ? c0 - warm_bytes : 0;   // c0 is a multiple of 128
-  t.s = 0;
+  t.s = x.s0;
   t.p12 = 0;
   t.nl = 0;
   t.kw0 = t.kw1 = 0;
@@ -457,15 +511,19 @@ __device__ __noinline__ bool k1_line_special(const uint8_t* __restrict__ p, uint
   return hit;
 }
 
+// a parked output: (offset from the range start << 16) | state (K1: row
+// offset; K1c: DESC address)
+template <bool kC>
 __device__ __forceinline__ void k1_drain(const K1Ctx& x, K1Stream& t, OutBuf& ob, uint32_t S) {
   for (uint32_t i = 0; i < ob.n; ++i) {
     const uint32_t e = ob.p[i * ob.stride];
-    k1_out_v3(x, t, e & 0xffffu, t.emit + (e >> 16), S);
+    if constexpr (kC) k1_out_c(x, t, e & 0xfff0u, t.emit + (e >> 16));
+    else k1_out_v3(x, t, e & 0xffffu, t.emit + (e >> 16), S);
   }
   ob.n = 0;
 }
 
-template <int kAbl>
+template <int kAbl, bool kC>
 __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& ob, const uint8_t* smem, uint32_t S,
                                            uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   constexpr uint32_t kTabOff = 256;
@@ -486,7 +544,8 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
   uint32_t s = t.s;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (kAbl & kAblPtrAddr) s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 2) + c2[k]);
+    if constexpr (kC) s = k1c_next(s, c2[k], __builtin_amdgcn_perm(0u, c2[k], 0u));   // K1c: class * 4 in every byte
+    else if (kAbl & kAblPtrAddr) s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 2) + c2[k]);
     else s = k1_lds16((s << 2) + c2[k] + kTabOff);
     st[k] = s;
   }
@@ -506,13 +565,18 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
       // at them one by one; each output position costs one LDS round trip
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (max(max(st[4 * j], st[4 * j + 1]), max(st[4 * j + 2], st[4 * j + 3])) >= x.first_out) {
+        const bool any = kC ? ((st[4 * j] | st[4 * j + 1] | st[4 * j + 2] | st[4 * j + 3]) & 1u) != 0
+                            : max(max(st[4 * j], st[4 * j + 1]), max(st[4 * j + 2], st[4 * j + 3])) >= x.first_out;
+        if (any) {
 #pragma unroll
           for (int k = 4 * j; k < 4 * j + 4; ++k) {
-            if (st[k] >= x.first_out) {
+            if (kC ? (st[k] & 1u) != 0 : st[k] >= x.first_out) {
               if ((kAbl & kAblDefer) && ob.n < kOutSlots) {
-                ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k - t.emit) << 16) | st[k];
+                const uint32_t tag = kC ? (st[k] & 0xfff0u) : st[k];
+                ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(t.p + k - t.emit) << 16) | tag;
                 ++ob.n;
+              } else if constexpr (kC) {
+                k1_out_c(x, t, st[k], t.p + k);
               } else {
                 k1_out_v3(x, t, st[k], t.p + k, S);
               }
@@ -526,7 +590,60 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
   t.p += 16;
 }
 
-template <int kThreads, int kAbl>
+// K1c's 16-byte word: two halves of 8 bytes (8 class reads, then the 8
+// dependent steps, then their outputs), so the two-read step's registers fit
+// the 128-VGPR budget of 1024-thread workgroups without spilling.
+__device__ __forceinline__ void k1_word_c(const K1Ctx& x, K1Stream& t, OutBuf& ob, const uint8_t* smem,
+                                          uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const bool emit = t.p >= t.emit;
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t s = t.s;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t c4[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c4[k] = smem[(w[2 * h + (k >> 2)] >> ((k & 3) * 8)) & 0xffu];
+    uint32_t st[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s = k1c_next(s, c4[k], __builtin_amdgcn_perm(0u, c4[k], 0u));   // c4 in every byte
+      st[k] = s;
+    }
+    if (emit) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if ((st[4 * j] | st[4 * j + 1] | st[4 * j + 2] | st[4 * j + 3]) & 1u) {
+#pragma unroll
+          for (int k = 4 * j; k < 4 * j + 4; ++k) {
+            if (st[k] & 1u) {
+              const unsigned long long q = t.p + 8 * h + k;
+              if (ob.n < kOutSlots) {
+                ob.p[ob.n * ob.stride] = (static_cast<uint32_t>(q - t.emit) << 16) | (st[k] & 0xfff0u);
+                ++ob.n;
+              } else {
+                k1_out_c(x, t, st[k], q);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  t.s = s;
+  if (emit) {
+    uint32_t u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t xx = w[j] ^ 0x0a0a0a0au;
+      u[j] = ((xx & 0x7f7f7f7fu) + 0x7f7f7f7fu) | xx | 0x7f7f7f7fu;   // bit 7 of a byte: not '\n'
+    }
+    t.nl += 128u - (__popc(u[0]) + __popc(u[1]) + __popc(u[2]) + __popc(u[3]));
+  }
+  t.p12 = (w3 >> 24) | ((w3 >> 8) & 0xff00u);
+  t.p += 16;
+}
+
+template <int kThreads, int kAbl, bool kC>
 __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const uint8_t* __restrict__ data, unsigned long long total,
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
@@ -548,8 +665,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   }
   const uint32_t padded = (table_words16 * 2 + 15) & ~15u;
   const uint32_t meta_off = kTabOff + padded;
-  const uint32_t list_off = meta_off;            // output metadata is inline in the table rows
-  const uint32_t hits_off = (list_off + nlist * 4 + 15) & ~15u;
+  const uint32_t list_off = meta_off;            // output metadata is inline in the table rows (K1c: in global memory)
+  const uint32_t hits_off = (list_off + (kC ? 0u : nlist * 4) + 15) & ~15u;
   uint32_t S = (nclasses + 2) & ~1u;             // k1_row_stride(nclasses): the silent-row stride
   if (((S / 2) & 1u) == 0) S += 2;
   uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + hits_off);
@@ -562,8 +679,10 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff);
     for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[i] = g_cls[i];
-    uint32_t* s_list = reinterpret_cast<uint32_t*>(smem + list_off);
-    for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
+    if (!kC) {
+      uint32_t* s_list = reinterpret_cast<uint32_t*>(smem + list_off);
+      for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
+    }
   }
   K1Ctx x;
   x.data = data; x.total = total; x.chunk = chunk;
@@ -571,8 +690,9 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
   x.cls = smem;
   x.first_out = first_out; x.nclasses = nclasses; x.wave_hits = wave_hits;
-  x.meta = nullptr;
-  x.list = reinterpret_cast<const uint32_t*>(smem + list_off);
+  x.meta = kC ? g_meta : nullptr;
+  x.list = kC ? g_list : reinterpret_cast<const uint32_t*>(smem + list_off);
+  x.s0 = kC ? first_out : 0u;                    // K1c: first_out carries the start state's packed value
   x.nkw = nkw;
   x.kwbits = kwbits; x.kwmask = kwbits + kw_base / 32; x.kw_words = kw_words; x.primary = primary != 0;
   x.hits = hits + static_cast<size_t>(blockIdx.x) * region_cap; x.region_cap = region_cap; x.b_hitcnt = s_block;
@@ -650,10 +770,16 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             // one copy of the word body: the uniform word index selects
             // cur[i] by register indexing
 #pragma unroll 1
-            for (int i = 0; i < kW; ++i) k1_word_v3<kAbl>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+            for (int i = 0; i < kW; ++i) {
+              if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+              else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+            }
           } else {
 #pragma unroll
-            for (int i = 0; i < kW; ++i) k1_word_v3<kAbl>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+            for (int i = 0; i < kW; ++i) {
+              if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+              else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+            }
           }
           if (have) {
 #pragma unroll
@@ -662,7 +788,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
         } else {
           // a line with a file boundary or the chunk end (rare): word by word
           have = false;
-          if (kAbl & kAblDefer) k1_drain(x, t, ob, S);     // parked outputs belong to file t.f
+          if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);     // parked outputs belong to file t.f
           for (int i = 0; i < kW && t.p < k1_end(x, t); ++i) {
             if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
               if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
@@ -672,11 +798,11 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            k1_word_slow(x, t, w, S);
+            k1_word_slow<kC>(x, t, w, S);
           }
         }
       }
-      if (kAbl & kAblDefer) k1_drain(x, t, ob, S);
+      if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
       if (kAbl & kAblLoadOnly) {
         t.nl = static_cast<uint32_t>(t.kw1);
         t.kw1 = 0;
@@ -713,15 +839,22 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
 }
 
-// K1 builds: the default (464) and the measurement builds kept for the
-// DESIGN.md 4.1 ablations (kAbl bits; tools/k1_probe.py --variants 3:ABL)
-const void* k1_kernel(int abl) {
+// K1 builds: the product's default (464, K1 and K1c).  The measurement
+// builds of the DESIGN.md 4.1 ablations (kAbl bits; tools/k1_probe.py
+// --variants 3:ABL) exist only in the probe library
+// (python -m trivy_amd.build --probe -> libtrivysecret_probe.so, -DTSG_K1_PROBE).
+constexpr int kK1Default = 464;
+const void* k1_kernel(int abl, bool compressed) {
+  if (compressed) return abl == kK1Default ? reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, kK1Default, true>) : nullptr;
   switch (abl) {
-#define TSG_K1_V3(A) case (A): return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, (A)>);
+#define TSG_K1_V3(A) case (A): return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, (A), false>);
+    TSG_K1_V3(kK1Default)
+#ifdef TSG_K1_PROBE
     TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(32) TSG_K1_V3(48)
-    TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448) TSG_K1_V3(464)
+    TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448)
     TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
     TSG_K1_V3(2448) TSG_K1_V3(2512)
+#endif
 #undef TSG_K1_V3
     default: return nullptr;
   }
@@ -769,6 +902,7 @@ struct K1Group {
   uint32_t kw_base = 0, warm_lines = 0, warm_lines64 = 0;
   size_t meta_bytes = 0;
   bool in_lds = false;
+  bool compressed = false;     // K1c table (prefilter.h CompressedScan): first_out holds the start state's value
 };
 
 // The compiled rule tables on one device plus that device's pool of lanes.
@@ -960,7 +1094,37 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
   if (hipGetDeviceProperties(&prop, dt->device) == hipSuccess) dt->sms = prop.multiProcessorCount;
   if (pf.anchors.size() >= (1u << kAnchorBits)) { *err = "too many anchor literals for K1's hit encoding"; return false; }
   dt->kw_words = std::max<uint32_t>(1, (pf.nkw + 31) / 32);
+  if (pf.compressed.ok) {
+    // K1c: every pattern in one compressed table, one pass (replaces the groups)
+    const CompressedScan& c = pf.compressed;
+    K1Group g;
+    g.compressed = true;
+    g.nclasses = c.nclasses;
+    g.stride = c.row_stride;
+    g.first_out = c.state_val[0];
+    g.kw_base = 0;
+    const uint32_t warm = c.max_pattern_bytes > 0 ? c.max_pattern_bytes - 1 : 0;
+    g.warm_lines = (warm + 127) / 128;
+    g.warm_lines64 = (warm + 63) / 64;
+    std::vector<uint32_t> img = c.image;
+    img.resize((img.size() + 3) & ~size_t(3), 0);
+    g.table_words16 = static_cast<uint32_t>(img.size() * 2);
+    g.nmeta = static_cast<uint32_t>(c.outs.size());
+    g.nlist = static_cast<uint32_t>(c.out_list.size());
+    g.meta_bytes = 0;                                        // outputs stay in global memory
+    g.in_lds = kK1HitLdsMin + 256 + img.size() * 4 <= kLdsBytes;
+    std::vector<OutMeta> meta;
+    for (const auto& o : c.outs) meta.push_back(OutMeta{o.kw0, o.kw1, o.list_begin, o.list_count});
+    std::vector<uint8_t> cls(c.cls4, c.cls4 + 256);
+    if (!dev_upload(img, reinterpret_cast<uint32_t**>(&g.next), err) || !dev_upload(cls, &g.cls, err) ||
+        !dev_upload(meta, &g.meta, err) || !dev_upload(c.out_list, &g.list, err)) {
+      return false;
+    }
+    dt->kw_words = std::max<uint32_t>(dt->kw_words, 4);
+    dt->k1g.push_back(g);
+  }
   for (const ScanDfa& sd : pf.groups) {
+    if (pf.compressed.ok) break;
     K1Group g;
     // scan table with an odd dword row stride: next[s*stride + c] then spreads
     // the same class of different states over different LDS banks (a 64-class
@@ -1340,10 +1504,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       return h;
     };
     auto lds_of = [&](const K1Group& g) -> size_t { return lds_for(g, hits_of(g)); };
-    const void* kfn = k1_kernel(k1_abl_);
-    if (!kfn) { *err = "unsupported K1 build (TSG_K1_ABL)"; return false; }
     for (uint32_t gi = 0; gi < ngroups; ++gi) {
       const K1Group& g = dt.k1g[gi];
+      const void* kfn = k1_kernel(k1_abl_, g.compressed);
+      if (!kfn) { *err = "unsupported K1 build (TSG_K1_ABL; the measurement builds are in the probe library)"; return false; }
       if (!g.in_lds || lds_of(g) > kLdsBytes) { *err = "K1 LDS budget exceeded"; return false; }
       HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_of(g))));
     }
@@ -1375,7 +1539,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
                       &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
-      HIP_OK(hipLaunchKernel(kfn, dim3(blocks), dim3(nthr), args, lds, s));
+      HIP_OK(hipLaunchKernel(k1_kernel(k1_abl_, g.compressed), dim3(blocks), dim3(nthr), args, lds, s));
       ++launches;
     }
     HIP_OK(hipEventRecord(ln.ev[1], s));

@@ -939,15 +939,17 @@ bool build_group(const std::vector<Pattern>& ps, ScanDfa* out, std::string* err)
 // each group is one K1 pass over the data, so fewer groups is the lever on a
 // large ruleset's K1 time.  A run that still does not fit at many runs is
 // halved until it does.
-bool make_groups(Prefilter* pf, std::vector<Pattern> pats, std::string* err) {
+bool make_groups(Prefilter* pf, std::vector<Pattern> pats, ScanDfa* all_out, std::string* err) {
   pf->groups.clear();
   std::string e;
   {
-    ScanDfa all;
+    ScanDfa& all = *all_out;
     if (build_group(pats, &all, &e) && k1_fits(all)) {
       pf->groups.push_back(std::move(all));
+      *all_out = ScanDfa();
       return true;
     }
+    if (!e.empty()) *all_out = ScanDfa();                       // no one-group DFA (state cap)
     if (std::getenv("TSG_PREFILTER_DEBUG"))
       fprintf(stderr, "one-group scan DFA: %u states x %u classes (%u silent), %zu table words, LDS %zu B\n",
               all.t.nstates, all.t.nclasses, all.first_out_state, static_cast<size_t>(k1_table_words16(all)),
@@ -1015,9 +1017,189 @@ bool make_groups(Prefilter* pf, std::vector<Pattern> pats, std::string* err) {
   return true;
 }
 
+// ------------------------------------------------------ K1c compressed table
+// Exceptions of state s against full state f: the classes whose next state
+// differs.  Representable in one DESC record when there are at most four such
+// classes going to at most two targets, and when there are two targets each
+// takes at most two of the four class slots.
+struct Exc { uint32_t n = 0; uint32_t cls[4]; uint16_t tgt[4]; };
+
+bool exceptions(const DfaTable& t, uint32_t s, uint32_t f, Exc* e) {
+  const uint32_t C = t.nclasses;
+  const uint16_t* a = &t.next[static_cast<size_t>(s) * C];
+  const uint16_t* b = &t.next[static_cast<size_t>(f) * C];
+  e->n = 0;
+  for (uint32_t c = 0; c < C; ++c) {
+    if (a[c] == b[c]) continue;
+    if (e->n == 4) return false;
+    e->cls[e->n] = c;
+    e->tgt[e->n] = a[c];
+    ++e->n;
+  }
+  uint16_t tg[2] = {0, 0};
+  uint32_t cnt[2] = {0, 0}, nt = 0;
+  for (uint32_t i = 0; i < e->n; ++i) {
+    uint32_t k = 0;
+    while (k < nt && tg[k] != e->tgt[i]) ++k;
+    if (k == nt) {
+      if (nt == 2) return false;
+      tg[nt++] = e->tgt[i];
+    }
+    ++cnt[k];
+  }
+  return nt <= 1 || (cnt[0] <= 2 && cnt[1] <= 2);
+}
+
+// The DFA of all scan patterns as a K1c table (prefilter.h).  Full rows are
+// chosen greedily: the start state, then, while some state has no full state
+// it can be expressed against, the shallowest such states.  Every (state,
+// class) transition and every output flag is checked against the DFA before
+// the table is accepted.
+bool compress_scan(const ScanDfa& d, uint32_t nkw, size_t lds_budget, CompressedScan* out, std::string* why) {
+  const DfaTable& t = d.t;
+  const uint32_t N = t.nstates, C = t.nclasses;
+  *out = CompressedScan();
+  if (N == 0 || C == 0 || C > 63) { *why = "classes"; return false; }
+  std::vector<uint32_t> depth(N, UINT32_MAX);
+  {
+    std::vector<uint32_t> fr{0}, nf;
+    depth[0] = 0;
+    while (!fr.empty()) {
+      nf.clear();
+      for (uint32_t s : fr)
+        for (uint32_t c = 0; c < C; ++c) {
+          const uint32_t x = t.next[static_cast<size_t>(s) * C + c];
+          if (depth[x] == UINT32_MAX) { depth[x] = depth[s] + 1; nf.push_back(x); }
+        }
+      fr.swap(nf);
+    }
+  }
+  for (uint32_t s = 0; s < N; ++s) if (depth[s] == UINT32_MAX) depth[s] = 0xfffffu;   // unreachable: keep anyway
+  std::vector<uint8_t> is_full(N, 0);
+  std::vector<uint32_t> full{0}, def(N, UINT32_MAX);
+  is_full[0] = 1;
+  Exc e;
+  for (;;) {
+    std::vector<uint32_t> bad;
+    for (uint32_t s = 0; s < N; ++s) {
+      if (is_full[s]) continue;
+      if (def[s] != UINT32_MAX && exceptions(t, s, def[s], &e)) continue;
+      def[s] = UINT32_MAX;
+      uint32_t best = UINT32_MAX, bestn = 5;
+      for (uint32_t f : full) {
+        if (exceptions(t, s, f, &e) && e.n < bestn) {
+          best = f;
+          bestn = e.n;
+          if (bestn == 0) break;
+        }
+      }
+      if (best == UINT32_MAX) bad.push_back(s);
+      else def[s] = best;
+    }
+    if (bad.empty()) break;
+    uint32_t md = UINT32_MAX;
+    for (uint32_t s : bad) md = std::min(md, depth[s]);
+    for (uint32_t s : bad)
+      if (depth[s] == md) { is_full[s] = 1; full.push_back(s); }
+    if (full.size() > 8192) { *why = "too many full rows"; return false; }
+  }
+  // records: 0 = no exceptions, then every compact state and every output state
+  const uint32_t fo = d.first_out_state;
+  std::vector<uint32_t> rec(N, 0);
+  uint32_t ndesc = 1;
+  for (uint32_t s = 0; s < N; ++s) if (!is_full[s] || s >= fo) rec[s] = ndesc++;
+  if (256 + 16ull * ndesc > 0x10000) { *why = "too many DESC records for 16-bit addresses"; return false; }
+  uint32_t stride = C | 1u;                                     // odd dword stride: a class spreads over banks
+  const uint64_t desc_dw = 4ull * ndesc;
+  const uint64_t full_base_dw = 64 + desc_dw;                   // LDS dword address of the first full row
+  const uint64_t image_dw = desc_dw + static_cast<uint64_t>(full.size()) * stride;
+  if (full_base_dw + static_cast<uint64_t>(full.size()) * stride > 0x10000) { *why = "full rows beyond 256 KiB"; return false; }
+  if (256 + image_dw * 4 > lds_budget) {
+    *why = "table " + std::to_string(256 + image_dw * 4) + " B > LDS budget " + std::to_string(lds_budget) + " B";
+    return false;
+  }
+  std::vector<uint32_t> row_of(N, 0);                           // full row index of each full state
+  for (size_t i = 0; i < full.size(); ++i) row_of[full[i]] = static_cast<uint32_t>(i);
+  std::vector<uint32_t> val(N);
+  for (uint32_t s = 0; s < N; ++s) {
+    const uint32_t f = is_full[s] ? s : def[s];
+    val[s] = (static_cast<uint32_t>(full_base_dw + static_cast<uint64_t>(row_of[f]) * stride) << 16) |
+             (256u + 16u * rec[s]) | (s >= fo ? 1u : 0u);
+  }
+  out->image.assign(image_dw, 0);
+  uint32_t* desc = out->image.data();
+  desc[0] = kK1cNoRecord; desc[1] = desc[2] = 0; desc[3] = kK1cNoRecord;
+  for (uint32_t s = 0; s < N; ++s) {
+    if (rec[s] == 0) continue;
+    uint32_t* r = desc + 4ull * rec[s];
+    uint8_t slot[4] = {0xff, 0xff, 0xff, 0xff};
+    uint32_t tA = 0, tB = 0;
+    if (!is_full[s]) {
+      if (!exceptions(t, s, def[s], &e)) { *why = "internal: exception set"; return false; }
+      // group the classes by target: target 1 in slots 0-1, target 2 in slots 2-3 (one target: slots 0-3)
+      uint16_t first = e.n ? e.tgt[0] : 0;
+      uint32_t na = 0, nb = 0;
+      bool two = false;
+      for (uint32_t i = 0; i < e.n; ++i) two |= e.tgt[i] != first;
+      for (uint32_t i = 0; i < e.n; ++i) {
+        const uint8_t c4 = static_cast<uint8_t>(e.cls[i] * 4);
+        if (!two) { slot[na++] = c4; continue; }
+        if (e.tgt[i] == first) slot[na++] = c4;
+        else { slot[2 + nb++] = c4; tB = val[e.tgt[i]]; }
+      }
+      if (e.n) tA = val[first];
+      if (!two) tB = tA;
+    }
+    r[0] = static_cast<uint32_t>(slot[0]) | (static_cast<uint32_t>(slot[1]) << 8) |
+           (static_cast<uint32_t>(slot[2]) << 16) | (static_cast<uint32_t>(slot[3]) << 24);
+    r[1] = tA;
+    r[2] = tB;
+    r[3] = kK1cNoRecord;
+    if (s >= fo) {
+      // outputs: keyword ids < 128 in two masks, the others (anchors, keywords >= 128) listed
+      const uint32_t o = s - fo;
+      CompressedScan::Out om{0, 0, static_cast<uint32_t>(out->out_list.size()), 0};
+      for (uint32_t k = d.out_off[o]; k < d.out_off[o + 1]; ++k) {
+        const uint32_t id = d.out_ids[k];
+        if (id < nkw && id < 64) om.kw0 |= 1ull << id;
+        else if (id < nkw && id < 128) om.kw1 |= 1ull << (id - 64);
+        else out->out_list.push_back(id);
+      }
+      om.list_count = static_cast<uint32_t>(out->out_list.size()) - om.list_begin;
+      r[3] = static_cast<uint32_t>(out->outs.size());
+      out->outs.push_back(om);
+    }
+  }
+  for (size_t i = 0; i < full.size(); ++i) {
+    uint32_t* row = out->image.data() + desc_dw + i * stride;
+    for (uint32_t c = 0; c < C; ++c) row[c] = val[t.next[static_cast<size_t>(full[i]) * C + c]];
+  }
+  for (int b = 0; b < 256; ++b) out->cls4[b] = static_cast<uint8_t>(t.byte_class[b] * 4);
+  out->nclasses = C;
+  out->row_stride = stride;
+  out->ndesc = ndesc;
+  out->nfull = static_cast<uint32_t>(full.size());
+  out->nstates = N;
+  out->state_val = val;
+  out->max_pattern_bytes = d.max_pattern_bytes;
+  // exhaustive self-check against the DFA: every transition, every output flag
+  for (uint32_t s = 0; s < N; ++s) {
+    if (((val[s] & 1u) != 0) != (s >= fo)) { *why = "internal: output flag"; return false; }
+    for (int b = 0; b < 256; ++b) {
+      const uint32_t want = val[t.next[static_cast<size_t>(s) * C + t.byte_class[b]]];
+      if (k1c_step(*out, val[s], static_cast<uint32_t>(b)) != want) {
+        *why = "internal: transition check failed at state " + std::to_string(s) + " byte " + std::to_string(b);
+        return false;
+      }
+    }
+  }
+  out->ok = true;
+  return true;
+}
+
 // Keyword ids are renumbered so that each group's keywords are contiguous:
 // K1 then ORs them into register masks relative to the group's kw_base.
-void renumber_keywords(Prefilter* pf) {
+void renumber_keywords(Prefilter* pf, ScanDfa* all) {
   std::vector<uint32_t> newid(pf->nkw, 0xffffffffu);
   uint32_t next = 0;
   for (auto& g : pf->groups) {
@@ -1036,6 +1218,7 @@ void renumber_keywords(Prefilter* pf) {
     g.kw_base = lo == 0xffffffffu ? 0 : (lo & ~31u);
   }
   remap(&pf->host_scan.out_ids);
+  remap(&all->out_ids);
   remap(&pf->rule_kw);
   std::vector<std::string> text(pf->nkw);
   for (uint32_t k = 0; k < pf->nkw; ++k) text[newid[k]] = pf->kw_text[k];
@@ -1242,9 +1425,15 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
            std::to_string(pf->verify[gi.verify_dfa].nclasses) +
            " classes, limit " + std::to_string(gi.verify_limit) + note + " {" + seqs_str(ch.lits) + "}\n";
   }
-  if (!make_groups(pf, pats, err)) return false;
+  ScanDfa all;
+  if (!make_groups(pf, pats, &all, err)) return false;
   if (!make_scan_dfa(host, h0, hmaxb, &pf->host_scan, err)) return false;
-  renumber_keywords(pf);
+  renumber_keywords(pf, &all);
+  std::string k1c_note;
+  const char* k1c_env = std::getenv("TSG_K1C");
+  if (pf->groups.size() > 1 && all.t.nstates > 0 && !(k1c_env && std::atoi(k1c_env) == 0)) {
+    if (!compress_scan(all, pf->nkw, kK1LdsBytes - kK1HitLdsMin, &pf->compressed, &k1c_note)) pf->compressed = CompressedScan();
+  }
   std::string grep;
   for (size_t g = 0; g < pf->groups.size(); ++g) {
     const ScanDfa& d = pf->groups[g];
@@ -1254,6 +1443,15 @@ bool build_prefilter(const Ruleset& rs, Prefilter* pf, std::string* err) {
             std::to_string(d.first_out_state) + " silent), keyword base " + std::to_string(d.kw_base) +
             ", max pattern " + std::to_string(d.max_pattern_bytes) + " B, LDS " +
             std::to_string(k1_lds_table_bytes(d)) + " B\n";
+  }
+  if (pf->compressed.ok) {
+    const CompressedScan& c = pf->compressed;
+    grep += "K1c one-pass table: " + std::to_string(c.nstates) + " states x " + std::to_string(c.nclasses) +
+            " classes, " + std::to_string(c.nfull) + " full rows (stride " + std::to_string(c.row_stride) + "), " +
+            std::to_string(c.ndesc) + " DESC records, " + std::to_string(c.outs.size()) + " output records, LDS " +
+            std::to_string(c.lds_bytes()) + " B\n";
+  } else if (pf->groups.size() > 1) {
+    grep += "K1c one-pass table: not used (" + (k1c_note.empty() ? std::string("disabled") : k1c_note) + ")\n";
   }
   pf->report = "host variant DFA: " + std::to_string(pf->host_scan.t.nstates) + " states x " +
                std::to_string(pf->host_scan.t.nclasses) + " classes\n" +

@@ -61,6 +61,49 @@ uint64_t k1_table_words16(const ScanDfa& d);        // silent rows then output r
 size_t k1_lds_table_bytes(const ScanDfa& d);        // scan table + class map + output metadata
 bool k1_fits(const ScanDfa& d);
 
+// K1c: the scan DFA of ALL patterns as one compressed LDS table, for rule
+// sets whose full table does not fit K1's LDS (config 5: 4020 states x 53
+// classes = 426 KB as a full table, 3 K1 passes; compressed ~140 KB, 1 pass).
+//
+// A few states keep a FULL row (uint32 packed next states per class); every
+// other state is its "default" full state's row plus at most four classes
+// that go elsewhere (at most two targets, each reached by at most two of the
+// four classes when there are two), kept in a 16-byte DESC record.  A state
+// is one packed uint32:
+//   bit   0      the state has outputs (its DESC record holds the output index)
+//   bits  4..15  LDS byte address of its DESC record (256 = the shared record
+//                with no exceptions; records are 16-byte aligned, below 64 KiB)
+//   bits 16..31  LDS dword address of its full row (its own, or its default's)
+// so one byte is: the row entry FULL[row + class] and the record DESC[idx],
+// both addressed from the state alone (issued together, one LDS round trip),
+// then the record's classes decide between its targets and the row entry.
+// LDS image: [class map 256 B][DESC ndesc x 16 B][FULL nfull x row_stride x 4 B].
+struct CompressedScan {
+  bool ok = false;
+  uint32_t nclasses = 0, row_stride = 0;      // row_stride: odd number of dwords >= nclasses
+  uint32_t ndesc = 0, nfull = 0, nstates = 0;
+  uint8_t cls4[256] = {0};                    // byte -> class * 4
+  std::vector<uint32_t> image;                // DESC then FULL, dwords (LDS bytes 256 ..)
+  std::vector<uint32_t> state_val;            // packed value of every DFA state (state 0 = start)
+  // per output record (indexed by DESC .w): keyword ids < 128 as two masks, then a list
+  struct Out { uint64_t kw0, kw1; uint32_t list_begin, list_count; };
+  std::vector<Out> outs;
+  std::vector<uint32_t> out_list;
+  uint32_t max_pattern_bytes = 1;
+  size_t lds_bytes() const { return 256 + image.size() * 4; }
+};
+constexpr uint32_t kK1cNoRecord = 0xffffffffu;
+
+// One K1c step on the host (the kernel's arithmetic; tests and self-checks).
+inline uint32_t k1c_step(const CompressedScan& c, uint32_t s, uint32_t b) {
+  const uint32_t c4 = c.cls4[b];
+  const uint32_t f = c.image[(s >> 16) - 64 + c4 / 4];       // the image starts at LDS byte 256 = dword 64
+  const uint32_t* d = c.image.data() + ((s & 0xfff0u) - 256) / 4;
+  const uint32_t x = d[0] ^ (c4 * 0x01010101u);
+  const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
+  return (z & 0x8080u) ? d[1] : (z & 0x80800000u) ? d[2] : f;
+}
+
 struct AnchorInfo {                    // one literal of one rule
   uint32_t rule;
   uint32_t min_len, max_len;           // byte length range of the literal
@@ -94,7 +137,11 @@ struct Prefilter {
   // outputs of one DFA over all patterns.  The builtin rules need one group;
   // large custom rule sets (config 5) are split until every group fits K1.
   std::vector<ScanDfa> groups;
-  ScanDfa host_scan;                   // host: + U+0130/U+212A/U+017F alternatives (fold-special files)
+  // K1c: all groups' patterns as one compressed table (ok only when there is
+  // more than one group and it fits); the engine then runs one K1c pass
+  // instead of one K1 pass per group.  TSG_K1C=0 disables it.
+  CompressedScan compressed;
+  ScanDfa host_scan;                  // host: + U+0130/U+212A/U+017F alternatives (fold-special files)
   std::vector<AnchorInfo> anchors;
   std::vector<AnchorInfo> host_anchors;   // same ids; byte lengths of the variant forms
   std::vector<RuleGpuInfo> rules;
