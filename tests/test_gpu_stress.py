@@ -11,10 +11,13 @@
   the tokens at the right line, and a 4 MB variant equals the host reference;
 * the largest K1 chunk TSG_K1_CHUNK allows gives the default-chunk result.
 """
+import os
 import random
 
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 from _oracle_pool import oracle_scan_many
 from trivy_amd import secret as S
@@ -91,13 +94,27 @@ def test_largest_k1_chunk_gpu(monkeypatch):
     assert sum(len(w["Findings"]) for w in want) > 20
 
 
-@pytest.mark.parametrize("abl,chunk", [("464", "2048"), ("464", "1024"), ("16", "4096"), ("0", "8192"),
-                                       ("2512", "1024"), ("2448", "2048")])
+def test_k1_probe_variants_agree_gpu():
+    # the K1 measurement builds whose layout bits keep results valid (no
+    # deferred outputs, unrolled loop, 128-B register lines, temporal loads,
+    # single-buffered lines) live in the probe library
+    # (libtrivysecret_probe.so, python -m trivy_amd.build --probe); one child
+    # process loads it and checks each against the host confirmer
+    import subprocess
+    import sys
+    probe = os.path.join(ROOT, "trivy_amd", "libtrivysecret_probe.so")
+    assert os.path.exists(probe), "build the probe library: python -m trivy_amd.build --probe"
+    env = dict(os.environ, TSG_LIB="libtrivysecret_probe.so")
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_k1_probe_variants.py"),
+                        "16:4096,0:8192,2512:1024,2448:2048"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("agree") == 4, r.stdout
+
+
+@pytest.mark.parametrize("abl,chunk", [("464", "2048"), ("464", "1024"), ("464", "4096")])
 def test_k1_variants_agree_gpu(monkeypatch, abl, chunk):
-    # every K1 build whose layout bits keep results valid (deferred outputs,
-    # rolled loop, 64-B or 128-B register lines, temporal loads, single- or
-    # double-buffered lines), over every chunk size, gives the host
-    # confirmer's result
+    # the product K1 build over every chunk size gives the host confirmer's
+    # result (the measurement builds: test_k1_probe_variants_agree_gpu)
     c = synth.generate(24_000_000, seed=31, sizes="loguniform", plant_rate=3e-3)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     want = S.scan_host_reference(S.Scanner(None), args, threads=16)

@@ -5,7 +5,9 @@
   python tools/k1_probe.py [--gb 4] [--reps 5] [--sizes loguniform] [--config 2|5]
 
 Prints per-launch K1 / K2 times and GB/s; used for K1 tuning and for
-rocprofv3 runs (a short program with few dispatches).
+rocprofv3 runs (a short program with few dispatches).  Variants other than
+the product build (TSG_K1_ABL != 464) need the probe library
+(python -m trivy_amd.build --probe), selected here through TSG_LIB.
 """
 import argparse
 import ctypes
@@ -34,6 +36,8 @@ def main():
                     help="comma list of ABL[:CHUNK[:NAME=V+NAME=V]] (TSG_K1_ABL build bits / TSG_K1_CHUNK / extra "
                          "TSG_* settings), one engine each")
     args = ap.parse_args()
+    if any(v.split(":")[0] not in ("", "464") for v in args.variants.split(",") if v):
+        os.environ.setdefault("TSG_LIB", "libtrivysecret_probe.so")
     import torch
 
     from trivy_amd import _lib
