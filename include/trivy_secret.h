@@ -314,6 +314,39 @@ int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const u
  * owned by p. */
 const char* tsg_prepared_walk_json(const tsg_prepared* p);
 
+/* ---- streamed feed -> scan: bounded host memory, the
+ * walk / read / prepare of batch k+1 overlapping the scan of batch k.
+ * A reader (an io.Reader): > 0 bytes read into buf (at most cap), 0 at the
+ * end of the data, < 0 on an error. */
+typedef int64_t (*tsg_read_fn)(void* user, uint8_t* buf, size_t cap);
+/* One container layer read from `read` in order: walker.LayerTar.Walk over an
+ * io.Reader (pkg/fanal/walker/tar.go:35-103) -> AnalyzeFile's gate
+ * (analyzer.go:403-419) before a file's content is read -> SecretAnalyzer
+ * .Analyze's preparation (secret.go:103-150) -> Scan, the kept files packed
+ * into batches of about batch_bytes raw bytes (0: 512 MiB; a larger file is a
+ * batch of its own), each scanned on the engine while the next is read.  The
+ * result holds every scanned file in walk order, ScanArgs.FilePath = "/" +
+ * path; tsg_result_walk_json gives Walk's return values and the feed timing.
+ * Layers may be scanned concurrently on one engine (image.go:327's pipeline). */
+int tsg_scan_layer_stream(tsg_engine* e, tsg_read_fn read, void* user, const tsg_feed_opts* opts,
+                          uint64_t batch_bytes, tsg_result** out);
+/* `trivy fs ROOT` streamed: tsg_prepare_fs_tree's walk and gate, the kept files
+ * read in walk order in batches of about batch_bytes, each scanned while the
+ * next is read.  ScanArgs.FilePath = the path relative to the root. */
+int tsg_scan_fs_tree(tsg_engine* e, const char* root, const tsg_feed_opts* opts, uint64_t batch_bytes,
+                     tsg_result** out);
+/* The same two pipelines with the CPU model of the GPU passes as the scan
+ * stage (tsg_scan_table_model's); tests only, never the product path. */
+int tsg_scan_layer_stream_model(const tsg_ruleset* rs, tsg_read_fn read, void* user, const tsg_feed_opts* opts,
+                                uint64_t batch_bytes, tsg_result** out);
+int tsg_scan_fs_tree_model(const tsg_ruleset* rs, const char* root, const tsg_feed_opts* opts, uint64_t batch_bytes,
+                           tsg_result** out);
+/* A streamed result's walk: {"files": [every regular file handed to the
+ * analyzers], "opq_dirs": [...], "wh_files": [...], "stats": {wall_ms,
+ * feed_ms, scan_ms, wait_ms, walked_bytes, read_bytes, scanned_bytes,
+ * batches, files, peak_batch_bytes}}; NULL for other results.  Owned by r. */
+const char* tsg_result_walk_json(const tsg_result* r);
+
 /* Test hook: Regexp.MatchString(text) for `pattern` with the required-literal
  * gate the ruleset compiler sets on path / allow regexes (*gated) and without
  * it (*plain); *has_gate = 1 if a gate was found (2: bounded). */

@@ -123,6 +123,22 @@ SIGNATURES += [
                                            ctypes.POINTER(ctypes.c_void_p)]),
 ]
 
+# tsg_read_fn: int64_t (*)(void* user, uint8_t* buf, size_t cap)
+READ_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+SIGNATURES += [
+    ("tsg_scan_layer_stream", ctypes.c_int, [ctypes.c_void_p, READ_FN, ctypes.c_void_p, ctypes.POINTER(TsgFeedOpts),
+                                             ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_scan_fs_tree", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(TsgFeedOpts),
+                                        ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_scan_layer_stream_model", ctypes.c_int, [ctypes.c_void_p, READ_FN, ctypes.c_void_p,
+                                                   ctypes.POINTER(TsgFeedOpts), ctypes.c_uint64,
+                                                   ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_scan_fs_tree_model", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(TsgFeedOpts),
+                                              ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_result_walk_json", ctypes.c_char_p, [ctypes.c_void_p]),
+]
+
 
 def feed_opts(config_path="", file_patterns=(), skip_files=(), skip_dirs=(), threads=0, pinned=False):
     """A TsgFeedOpts plus the objects its pointers refer to (keep both alive)."""

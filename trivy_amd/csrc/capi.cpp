@@ -22,6 +22,7 @@
 #include "tar.h"
 #include "prefilter.h"
 #include "report.h"
+#include "stream.h"
 #include "scanner.h"
 #include "walkfs.h"
 #include "wire.h"
@@ -72,6 +73,7 @@ struct tsg_result {
   ScanStats stats;
   std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
   std::vector<std::vector<LayerRef>> layers;               // optional [file][finding] (tsg_result_from_proto)
+  std::string walk_json;                                   // streamed results (tsg_result_walk_json)
 };
 
 extern "C" {
@@ -926,7 +928,7 @@ void tsg_prepared_free(tsg_prepared* p) { delete p; }
 namespace {
 thread_local double g_pinned_alloc_ms = 0;   // time spent in pinned_alloc on this thread (feed reports)
 
-uint8_t* pinned_alloc(size_t bytes, void (**free_fn)(uint8_t*)) {
+uint8_t* pinned_alloc(size_t bytes, FeedFree* free_fn) {
   void* p = nullptr;
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = tsg_alloc_pinned(bytes, &p);
@@ -1012,7 +1014,7 @@ int tsg_prepare_batch_opts(const tsg_ruleset* rs, const uint8_t* raw, const uint
   if (!feed_opts(opts, &fo, &sf, &sd, &nt, &pinned, &err)) return fail(TSG_ERR_INVALID, err);
   auto* p = new tsg_prepared();
   if (!prepare_batch(*rs->rs, fo, raw, raw_offsets, nfiles, paths, path_lens, nt, &p->b, &err,
-                     pinned ? pinned_alloc : nullptr)) {
+                     pinned ? FeedAlloc(pinned_alloc) : FeedAlloc())) {
     delete p;
     return fail(TSG_ERR_INVALID, err);
   }
@@ -1042,7 +1044,7 @@ int tsg_prepare_layer_tar_opts(const tsg_ruleset* rs, const uint8_t* tar, size_t
   }
   auto* p = new tsg_prepared();
   if (!prepare_files(*rs->rs, fo, tar, starts.data(), sizes.data(), paths, nt, &p->b, &err,
-                     pinned ? pinned_alloc : nullptr)) {
+                     pinned ? FeedAlloc(pinned_alloc) : FeedAlloc())) {
     delete p;
     return fail(TSG_ERR_INVALID, err);
   }
@@ -1073,54 +1075,34 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
   if (!feed_opts(opts, &fo, &sf, &sd, &nt, &pinned, &err)) return fail(TSG_ERR_INVALID, err);
   const auto t0 = std::chrono::steady_clock::now();
   FsWalk walk;
-  if (!walk_fs_tree(root, sf, sd, nt, &walk, &err)) return fail(TSG_ERR_INVALID, err);
+  std::vector<uint32_t> keep;
+  // walk, d.Info() of every walked file, AnalyzeFile's gate (stream.cpp)
+  if (!plan_fs_tree(*rs->rs, fo, root, sf, sd, nt, &walk, &keep, &err)) return fail(TSG_ERR_INVALID, err);
   const auto t1 = std::chrono::steady_clock::now();
-  // AnalyzeFile's gate before the file is opened (analyzer.go:417-419): the
-  // path part first (in parallel), then Required's size check on info.Size()
-  const uint32_t n = static_cast<uint32_t>(walk.files.size());
-  std::vector<uint8_t> want(n, 0);
-  {
-    std::atomic<uint32_t> next{0};
-    auto run = [&]() {
-      for (;;) {
-        const uint32_t b = next.fetch_add(256);
-        if (b >= n) break;
-        for (uint32_t i = b; i < std::min(n, b + 256); ++i)
-          want[i] = static_cast<uint8_t>(secret_analyzer_wants_path(*rs->rs, fo, walk.files[i].rel));
-      }
-    };
-    std::vector<std::thread> ts;
-    for (int t = 1; t < std::min<int>(nt, static_cast<int>(n / 256) + 1); ++t) ts.emplace_back(run);
-    run();
-    for (auto& th : ts) th.join();
-  }
-  stat_fs_files(&walk, want, nt);
-  std::vector<uint64_t> starts(n, 0);
+  std::vector<uint64_t> starts(keep.size(), 0);
   uint64_t total = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    if (!want[i]) continue;
-    const uint64_t sz = walk.files[i].size;
-    if (sz == UINT64_MAX || (want[i] == 2 && sz < 10)) { want[i] = 0; continue; }   // vanished / secret.go:154-156
-    starts[i] = total;
-    total += sz;
+  for (size_t k = 0; k < keep.size(); ++k) {
+    starts[k] = total;
+    total += walk.files[keep[k]].size;
   }
+  // the whole tree's kept files at once (tsg_scan_fs_tree streams them in bounded batches)
   std::unique_ptr<uint8_t[]> raw(new uint8_t[std::max<uint64_t>(total, 1)]);
   std::vector<uint64_t> got;
-  if (!read_fs_files(walk, want, starts, raw.get(), nt, &got, &err)) return fail(TSG_ERR_INVALID, err);
+  if (!read_fs_files(walk, keep, starts, raw.get(), nt, &got, &err)) return fail(TSG_ERR_INVALID, err);
   const auto t2 = std::chrono::steady_clock::now();
   std::vector<uint64_t> rstarts, rsizes;
   std::vector<std::string> paths;
-  for (uint32_t i = 0; i < n; ++i) {
-    if (!want[i] || got[i] == UINT64_MAX) continue;
-    rstarts.push_back(starts[i]);
-    rsizes.push_back(got[i]);
-    paths.push_back(walk.files[i].rel);
+  for (size_t k = 0; k < keep.size(); ++k) {
+    if (got[k] == UINT64_MAX) continue;
+    rstarts.push_back(starts[k]);
+    rsizes.push_back(got[k]);
+    paths.push_back(walk.files[keep[k]].rel);
   }
   fo.assume_required = true;
   g_pinned_alloc_ms = 0;
   auto* p = new tsg_prepared();
   if (!prepare_files(*rs->rs, fo, raw.get(), rstarts.data(), rsizes.data(), paths, nt, &p->b, &err,
-                     pinned ? pinned_alloc : nullptr)) {
+                     pinned ? FeedAlloc(pinned_alloc) : FeedAlloc())) {
     delete p;
     return fail(TSG_ERR_INVALID, err);
   }
@@ -1144,6 +1126,148 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
   return TSG_OK;
   TSG_API_CATCH
 }
+
+namespace {
+// CPU model of the engine's scan stage for one batch (tsg_scan_table_model's
+// per-file work): tests of the stream pipelines without a GPU.
+bool model_scan_batch(const Ruleset& rs, const Prefilter& pf, const BatchInput& in, std::vector<Secret>* res) {
+  const uint32_t ch = 2048;
+  const uint64_t total = in.nfiles ? in.offsets[in.nfiles] : 0;
+  std::vector<uint16_t> chunk_nl((total + ch - 1) / ch, 0);
+  for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += in.h_data[x] == '\n';
+  res->assign(in.nfiles, Secret());
+  for (uint32_t f = 0; f < in.nfiles; ++f) {
+    const uint8_t* c = in.h_data + in.offsets[f];
+    const size_t len = in.offsets[f + 1] - in.offsets[f];
+    std::vector<std::vector<uint64_t>> cand;
+    std::vector<uint8_t> gate;
+    if (prefilter_reference_file(pf, c, len, &cand, &gate)) prefilter_variant_file(pf, c, len, &cand, &gate);
+    FilePlan plan;
+    plan_from_candidates(pf, &cand, &plan);
+    NlSource nls;
+    nls.chunk_nl = chunk_nl.data();
+    nls.data = in.h_data;
+    nls.file_off = in.offsets[f];
+    nls.chunk = ch;
+    (*res)[f] = scan_file(rs, path_of(in.paths, in.path_lens, f), c, len, in.binary ? in.binary[f] != 0 : false,
+                          &plan, &nls);
+  }
+  return true;
+}
+
+bool stream_opts(const tsg_feed_opts* opts, uint64_t batch_bytes, bool pinned, StreamOpts* so, std::string* err) {
+  int nt;
+  bool pin_unused;
+  if (!feed_opts(opts, &so->feed, &so->skip_files, &so->skip_dirs, &nt, &pin_unused, err)) return false;
+  so->threads = nt;
+  so->pinned = pinned;
+  if (batch_bytes) so->batch_bytes = batch_bytes;
+  return true;
+}
+
+tsg_result* stream_result(std::shared_ptr<const Ruleset> rs, StreamResult&& sr) {
+  auto* r = new tsg_result();
+  r->rs = std::move(rs);
+  r->files = std::move(sr.files);
+  std::string& js = r->walk_json;
+  js = "{\"files\": ";
+  json_str_array(&js, sr.walked);
+  js += ", \"opq_dirs\": ";
+  json_str_array(&js, sr.opq_dirs);
+  js += ", \"wh_files\": ";
+  json_str_array(&js, sr.wh_files);
+  const StreamStats& st = sr.st;
+  char buf[512];
+  std::snprintf(buf, sizeof buf,
+                ", \"stats\": {\"wall_ms\": %.3f, \"feed_ms\": %.3f, \"scan_ms\": %.3f, \"wait_ms\": %.3f, "
+                "\"walked_bytes\": %llu, \"read_bytes\": %llu, \"scanned_bytes\": %llu, \"batches\": %llu, "
+                "\"files\": %llu, \"peak_batch_bytes\": %llu}}",
+                st.wall_ms, st.feed_ms, st.scan_ms, st.wait_ms, static_cast<unsigned long long>(st.walked_bytes),
+                static_cast<unsigned long long>(st.read_bytes), static_cast<unsigned long long>(st.scanned_bytes),
+                static_cast<unsigned long long>(st.batches), static_cast<unsigned long long>(st.files),
+                static_cast<unsigned long long>(st.peak_batch_bytes));
+  js += buf;
+  r->stats.bytes = st.scanned_bytes;
+  r->stats.files = st.files;
+  r->stats.total_ms = st.wall_ms;
+  return r;
+}
+
+BatchScanFn engine_stage(tsg_engine* e) {
+  return [e](const BatchInput& in, std::vector<Secret>* res, std::string* err) {
+    ScanStats st;
+    return e->eng->scan(in, res, &st, err);
+  };
+}
+
+BatchScanFn model_stage(const Ruleset& rs, const Prefilter& pf) {
+  return [&rs, &pf](const BatchInput& in, std::vector<Secret>* res, std::string*) {
+    return model_scan_batch(rs, pf, in, res);
+  };
+}
+}  // namespace
+
+int tsg_scan_layer_stream(tsg_engine* e, tsg_read_fn read, void* user, const tsg_feed_opts* opts,
+                          uint64_t batch_bytes, tsg_result** out) {
+  TSG_API_TRY
+  if (!e || !read || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  StreamOpts so;
+  std::string err;
+  if (!stream_opts(opts, batch_bytes, true, &so, &err)) return fail(TSG_ERR_INVALID, err);
+  StreamResult sr;
+  if (!stream_layer(*e->eng->ruleset(), so, read, user, engine_stage(e), &sr, &err)) return fail(TSG_ERR_INVALID, err);
+  *out = stream_result(e->eng->ruleset(), std::move(sr));
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_scan_fs_tree(tsg_engine* e, const char* root, const tsg_feed_opts* opts, uint64_t batch_bytes,
+                     tsg_result** out) {
+  TSG_API_TRY
+  if (!e || !root || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  StreamOpts so;
+  std::string err;
+  if (!stream_opts(opts, batch_bytes, true, &so, &err)) return fail(TSG_ERR_INVALID, err);
+  StreamResult sr;
+  if (!stream_fs_tree(*e->eng->ruleset(), so, root, engine_stage(e), &sr, &err)) return fail(TSG_ERR_INVALID, err);
+  *out = stream_result(e->eng->ruleset(), std::move(sr));
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_scan_layer_stream_model(const tsg_ruleset* rs, tsg_read_fn read, void* user, const tsg_feed_opts* opts,
+                                uint64_t batch_bytes, tsg_result** out) {
+  TSG_API_TRY
+  if (!rs || !read || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  StreamOpts so;
+  std::string err;
+  if (!stream_opts(opts, batch_bytes, false, &so, &err)) return fail(TSG_ERR_INVALID, err);
+  Prefilter pf;
+  if (!build_prefilter(*rs->rs, &pf, &err)) return fail(TSG_ERR_INTERNAL, err);
+  StreamResult sr;
+  if (!stream_layer(*rs->rs, so, read, user, model_stage(*rs->rs, pf), &sr, &err)) return fail(TSG_ERR_INVALID, err);
+  *out = stream_result(rs->rs, std::move(sr));
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_scan_fs_tree_model(const tsg_ruleset* rs, const char* root, const tsg_feed_opts* opts, uint64_t batch_bytes,
+                           tsg_result** out) {
+  TSG_API_TRY
+  if (!rs || !root || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  StreamOpts so;
+  std::string err;
+  if (!stream_opts(opts, batch_bytes, false, &so, &err)) return fail(TSG_ERR_INVALID, err);
+  Prefilter pf;
+  if (!build_prefilter(*rs->rs, &pf, &err)) return fail(TSG_ERR_INTERNAL, err);
+  StreamResult sr;
+  if (!stream_fs_tree(*rs->rs, so, root, model_stage(*rs->rs, pf), &sr, &err)) return fail(TSG_ERR_INVALID, err);
+  *out = stream_result(rs->rs, std::move(sr));
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+const char* tsg_result_walk_json(const tsg_result* r) { return r && !r->walk_json.empty() ? r->walk_json.c_str() : nullptr; }
 
 int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens) {
   TSG_API_TRY

@@ -142,7 +142,7 @@ bool prepare_core(const Ruleset& rs, const FeedOpts& opts, uint32_t nfiles, File
   // not zero-filled (every byte below offsets[nk] is written in pass 2); only
   // the pad K1 may read past the last file is cleared
   const size_t bytes = out->offsets[nk] + 64;
-  void (*free_fn)(uint8_t*) = nullptr;
+  FeedFree free_fn;
   uint8_t* buf = alloc ? alloc(bytes, &free_fn) : nullptr;
   out->pinned = buf != nullptr;
   if (buf) out->data = std::shared_ptr<uint8_t>(buf, free_fn);

@@ -1,6 +1,7 @@
 // Host feed: batched SecretAnalyzer.Required + content preparation.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -38,25 +39,27 @@ bool secret_analyzer_wants(const Ruleset& rs, const FeedOpts& opts, const std::s
 int secret_analyzer_wants_path(const Ruleset& rs, const FeedOpts& opts, const std::string& path);
 
 // Output buffer for the packed contents: returns memory of `bytes` bytes and
-// sets the deleter, or nullptr (the batch then uses the heap).
-using FeedAlloc = uint8_t* (*)(size_t bytes, void (**free_fn)(uint8_t*));
+// sets the deleter, or nullptr (the batch then uses the heap).  An empty
+// FeedAlloc means the heap.
+using FeedFree = std::function<void(uint8_t*)>;
+using FeedAlloc = std::function<uint8_t*(size_t bytes, FeedFree* free_fn)>;
 
 // keep(i) = (filePatternMatch || Required)(path_i, size_i) && (!IsBinary || ext == ".pyc")
 bool prepare_batch(const Ruleset& rs, const FeedOpts& opts, const uint8_t* raw, const uint64_t* raw_off,
                    uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
-                   PreparedBatch* out, std::string* err, FeedAlloc alloc = nullptr);
+                   PreparedBatch* out, std::string* err, FeedAlloc alloc = {});
 bool prepare_files(const Ruleset& rs, const FeedOpts& opts, const uint8_t* raw, const uint64_t* starts,
                    const uint64_t* sizes, const std::vector<std::string>& paths, int threads, PreparedBatch* out,
-                   std::string* err, FeedAlloc alloc = nullptr);
+                   std::string* err, FeedAlloc alloc = {});
 
 bool prepare_batch(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* raw_off,
                    uint32_t nfiles, const char* const* paths, const uint32_t* path_lens, int threads,
-                   PreparedBatch* out, std::string* err, FeedAlloc alloc = nullptr);
+                   PreparedBatch* out, std::string* err, FeedAlloc alloc = {});
 
 // The same over files at arbitrary places of one buffer (a layer tar):
 // file i is raw[starts[i], starts[i] + sizes[i]) with Required's path paths[i].
 bool prepare_files(const Ruleset& rs, const std::string& config_path, const uint8_t* raw, const uint64_t* starts,
                    const uint64_t* sizes, const std::vector<std::string>& paths, int threads, PreparedBatch* out,
-                   std::string* err, FeedAlloc alloc = nullptr);
+                   std::string* err, FeedAlloc alloc = {});
 
 }  // namespace tsg

@@ -834,10 +834,29 @@ bool make_scan_dfa(const Nfa& nfa, int s0, uint32_t maxb, ScanDfa* out, std::str
 // The two passes on the host over one file with the given scan DFAs (K1 runs
 // each group's DFA over the whole batch; outputs are unioned).
 void two_pass(const Prefilter& pf, const ScanDfa* dfas, size_t ndfa, const std::vector<AnchorInfo>& anchors,
-              const uint8_t* data, size_t len, std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate) {
+              const uint8_t* data, size_t len, std::vector<std::vector<uint64_t>>* cand, std::vector<uint8_t>* gate,
+              const CompressedScan* comp = nullptr) {
   std::vector<uint8_t> kwbit(pf.nkw, 0);
   struct Hit { uint64_t end; uint32_t anchor; };
   std::vector<Hit> hits;
+  if (comp) {
+    // K1c: the compressed table's packed states (k1c_step), outputs through
+    // the state's DESC record -> output record (keyword masks + list)
+    uint32_t s = comp->state_val[0];
+    for (size_t p = 0; p < len; ++p) {
+      s = k1c_step(*comp, s, data[p]);
+      if (!(s & 1u)) continue;
+      const uint32_t oi = comp->image[((s & 0xfff0u) - 256) / 4 + 3];
+      const CompressedScan::Out& o = comp->outs[oi];
+      for (uint32_t k = 0; k < 64; ++k) if ((o.kw0 >> k) & 1u) kwbit[k] = 1;
+      for (uint32_t k = 0; k < 64; ++k) if ((o.kw1 >> k) & 1u) kwbit[64 + k] = 1;
+      for (uint32_t j = 0; j < o.list_count; ++j) {
+        const uint32_t id = comp->out_list[o.list_begin + j];
+        if (id < pf.nkw) kwbit[id] = 1; else hits.push_back({p, id - pf.nkw});
+      }
+    }
+    ndfa = 0;
+  }
   for (size_t g = 0; g < ndfa; ++g) {
     const ScanDfa& sd = dfas[g];
     const DfaTable& t = sd.t;
@@ -1472,7 +1491,10 @@ bool prefilter_reference_file(const Prefilter& pf, const uint8_t* data, size_t l
   for (size_t p = 1; p < len; ++p) {
     if (fold_special_at(p >= 2 ? data[p - 2] : 0, data[p - 1], data[p])) { special = true; break; }
   }
-  two_pass(pf, pf.groups.data(), pf.groups.size(), pf.anchors, data, len, cand, gate);
+  // the tables the engine runs: K1c's compressed one-pass table when the
+  // rule set has one, else the scan-DFA groups
+  two_pass(pf, pf.groups.data(), pf.groups.size(), pf.anchors, data, len, cand, gate,
+           pf.compressed.ok ? &pf.compressed : nullptr);
   return special;
 }
 

@@ -1,0 +1,406 @@
+// Streamed feed -> scan pipeline (stream.h).  Two stages on two threads:
+//   producer (the calling thread): walk -> gate -> read the kept files into a
+//     raw batch -> prepare (Required / IsBinary / CR strip / .pyc printable
+//     runs) into a prepared-batch buffer;
+//   consumer: the scan stage on each prepared batch, in order.
+// Two prepared-batch buffers circulate (one scanned while the next is
+// prepared); the raw batch is reused.  Results come back in walk order.
+#include "stream.h"
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "tar.h"
+
+extern "C" int tsg_alloc_pinned(size_t bytes, void** out);
+extern "C" void tsg_free_pinned(void* p);
+
+namespace tsg {
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double ms_between(Clock::time_point a, Clock::time_point b) {
+  return std::chrono::duration<double, std::milli>(b - a).count();
+}
+
+// The prepared-batch buffers: `n` of them in circulation, grown on demand.
+class BufPool {
+ public:
+  BufPool(bool pinned, size_t n) : pinned_(pinned), n_(n) {}
+  ~BufPool() {
+    for (auto& b : bufs_) release(b.p);
+  }
+  // a buffer of >= bytes (blocks while all are in use); nullptr if allocation failed
+  uint8_t* get(size_t bytes, double* wait_ms) {
+    std::unique_lock<std::mutex> lk(mu_);
+    const auto t0 = Clock::now();
+    cv_.wait(lk, [&] { return bufs_.size() < n_ || std::any_of(bufs_.begin(), bufs_.end(), [](const B& b) { return !b.used; }); });
+    *wait_ms += ms_between(t0, Clock::now());
+    for (auto& b : bufs_) {
+      if (b.used) continue;
+      if (b.cap < bytes) {
+        release(b.p);
+        b.p = alloc(bytes);
+        b.cap = b.p ? bytes : 0;
+      }
+      if (!b.p) return nullptr;
+      b.used = true;
+      return b.p;
+    }
+    B b;
+    b.p = alloc(bytes);
+    if (!b.p) return nullptr;
+    b.cap = bytes;
+    b.used = true;
+    bufs_.push_back(b);
+    return b.p;
+  }
+  void put(uint8_t* p) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& b : bufs_) if (b.p == p) b.used = false;
+    cv_.notify_all();
+  }
+
+ private:
+  struct B { uint8_t* p = nullptr; size_t cap = 0; bool used = false; };
+  uint8_t* alloc(size_t bytes) {
+    if (!pinned_) return static_cast<uint8_t*>(std::malloc(bytes));
+    void* p = nullptr;
+    return tsg_alloc_pinned(bytes, &p) == 0 ? static_cast<uint8_t*>(p) : nullptr;
+  }
+  void release(uint8_t* p) {
+    if (!p) return;
+    if (pinned_) tsg_free_pinned(p);
+    else std::free(p);
+  }
+  bool pinned_;
+  size_t n_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<B> bufs_;
+};
+
+// One prepared batch on its way to the scan stage.
+struct Job {
+  PreparedBatch b;
+  std::vector<std::string> scan_paths;
+};
+
+class Pipeline {
+ public:
+  Pipeline(const Ruleset& rs, const StreamOpts& o, const BatchScanFn& scan, const char* prefix, StreamResult* out)
+      : rs_(rs), o_(o), scan_(scan), prefix_(prefix), out_(out), pool_(o.pinned, 2) {
+    fo_ = o.feed;
+    fo_.assume_required = true;                 // the producer gates each file before reading it
+    limit_ = std::max<uint64_t>(o.batch_bytes, 1);
+    raw_cap_ = std::min<uint64_t>(limit_, 64ull << 20);      // grown as batches fill (up to the limit, or a larger file)
+    raw_.reset(new uint8_t[raw_cap_]);
+    consumer_ = std::thread([this] { consume(); });
+  }
+  ~Pipeline() { finish(); }
+
+  // room for a file of n raw bytes in the current batch (flushing it first
+  // if it does not fit); returns where to put it, nullptr on failure
+  uint8_t* reserve(uint64_t n) {
+    if (!paths_.empty() && used_ + n > limit_ && !flush()) return nullptr;
+    if (used_ + n > raw_cap_) {                 // grow (a file larger than a batch: a buffer of its size)
+      const uint64_t cap = std::max<uint64_t>(used_ + n, std::min<uint64_t>(limit_, 2 * raw_cap_));
+      std::unique_ptr<uint8_t[]> nb(new uint8_t[cap]);
+      std::memcpy(nb.get(), raw_.get(), used_);
+      raw_ = std::move(nb);
+      raw_cap_ = cap;
+    }
+    return raw_.get() + used_;
+  }
+  // the file just written at reserve()'s pointer: n bytes
+  void commit(const std::string& path, uint64_t n) {
+    starts_.push_back(used_);
+    sizes_.push_back(n);
+    paths_.push_back(path);
+    used_ += n;
+    out_->st.read_bytes += n;
+  }
+  // prepare the current batch and hand it to the scan stage
+  bool flush() {
+    if (paths_.empty()) return ok();
+    const auto t0 = Clock::now();
+    auto job = std::make_unique<Job>();
+    std::string err;
+    double wait = 0;
+    BufPool* pool = &pool_;
+    FeedAlloc alloc = [pool, &wait](size_t bytes, FeedFree* free_fn) -> uint8_t* {
+      uint8_t* p = pool->get(bytes, &wait);
+      if (p) *free_fn = [pool](uint8_t* q) { pool->put(q); };
+      return p;
+    };
+    if (!prepare_files(rs_, fo_, raw_.get(), starts_.data(), sizes_.data(), paths_, o_.threads, &job->b, &err, alloc)) {
+      set_error(err);
+      return false;
+    }
+    if (!job->b.data) { set_error("out of memory for a prepared batch"); return false; }
+    for (uint32_t i : job->b.index) job->scan_paths.push_back(prefix_ + paths_[i]);
+    out_->st.peak_batch_bytes = std::max<uint64_t>(out_->st.peak_batch_bytes, used_);
+    out_->st.wait_ms += wait;
+    out_->st.feed_ms -= wait;                   // blocked on a buffer: not feed work
+    starts_.clear();
+    sizes_.clear();
+    paths_.clear();
+    used_ = 0;
+    out_->st.feed_ms += ms_between(t0, Clock::now());
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      q_.push_back(std::move(job));
+    }
+    cv_.notify_all();
+    return ok();
+  }
+  // drain: the last batch, then wait for the scan stage; true if no error
+  bool finish() {
+    if (finished_) return ok();
+    finished_ = true;
+    if (ok()) flush();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_ = true;
+    }
+    cv_.notify_all();
+    if (consumer_.joinable()) consumer_.join();
+    return ok();
+  }
+  bool ok() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return err_.empty();
+  }
+  std::string error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return err_;
+  }
+  void set_error(const std::string& e) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (err_.empty()) err_ = e;
+    cv_.notify_all();
+  }
+
+ private:
+  void consume() {
+    for (;;) {
+      std::unique_ptr<Job> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty() || done_ || !err_.empty(); });
+        if (!err_.empty() || q_.empty()) return;
+        job = std::move(q_.front());
+        q_.pop_front();
+      }
+      const auto t0 = Clock::now();
+      const uint32_t nk = static_cast<uint32_t>(job->b.index.size());
+      std::vector<const char*> pp(nk);
+      std::vector<uint32_t> pl(nk);
+      for (uint32_t k = 0; k < nk; ++k) {
+        pp[k] = job->scan_paths[k].c_str();
+        pl[k] = static_cast<uint32_t>(job->scan_paths[k].size());
+      }
+      BatchInput in;
+      in.h_data = job->b.data.get();
+      in.offsets = job->b.offsets.data();
+      in.nfiles = nk;
+      in.paths = pp.data();
+      in.path_lens = pl.data();
+      in.binary = job->b.binary.data();
+      std::vector<Secret> res;
+      std::string err;
+      if (!scan_(in, &res, &err)) { set_error(err); return; }
+      out_->st.scanned_bytes += job->b.offsets[nk];
+      out_->st.files += nk;
+      out_->st.batches += 1;
+      for (auto& r : res) out_->files.push_back(std::move(r));
+      job.reset();                                // the prepared buffer goes back to the pool
+      out_->st.scan_ms += ms_between(t0, Clock::now());
+    }
+  }
+
+  const Ruleset& rs_;
+  const StreamOpts& o_;
+  const BatchScanFn& scan_;
+  std::string prefix_;
+  StreamResult* out_;
+  FeedOpts fo_;
+  BufPool pool_;
+  std::unique_ptr<uint8_t[]> raw_;
+  uint64_t limit_ = 0, raw_cap_ = 0, used_ = 0;
+  std::vector<uint64_t> starts_, sizes_;
+  std::vector<std::string> paths_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::unique_ptr<Job>> q_;
+  bool done_ = false, finished_ = false;
+  std::string err_;
+  std::thread consumer_;
+};
+
+// a layer from a reader callback
+class ReaderTarInput : public TarInput {
+ public:
+  ReaderTarInput(StreamReadFn fn, void* user) : fn_(fn), user_(user) {}
+  bool read(uint8_t* dst, size_t n, size_t* got, std::string* err) override {
+    *got = 0;
+    if (n == 0 || eof_) return true;
+    const int64_t r = fn_(user_, dst, n);
+    if (r < 0) { *err = "failed to extract the archive: read error"; return false; }
+    if (r == 0) { eof_ = true; return true; }
+    *got = static_cast<size_t>(std::min<int64_t>(r, static_cast<int64_t>(n)));
+    pos += *got;
+    return true;
+  }
+
+ private:
+  StreamReadFn fn_;
+  void* user_;
+  bool eof_ = false;
+};
+
+}  // namespace
+
+bool stream_layer(const Ruleset& rs, const StreamOpts& o, StreamReadFn read, void* user, const BatchScanFn& scan,
+                  StreamResult* out, std::string* err) {
+  *out = StreamResult();
+  const auto t0 = Clock::now();
+  ReaderTarInput in(read, user);
+  LayerWalk walk;
+  const std::string cfg_base = o.feed.config_path;
+  Pipeline pl(rs, o, scan, "/", out);
+  auto t_feed = Clock::now();
+  // processFile (tar.go:94-105) -> AnalyzeFile's gate -> read the content
+  auto on_file = [&](const std::string& path, uint64_t size, TarInput& tin, std::string* e) {
+    out->walked.push_back(path);
+    out->st.walked_bytes += size;
+    if (!secret_analyzer_wants(rs, o.feed, path, size)) return true;     // the walker skips the data
+    uint8_t* dst = pl.reserve(size);
+    if (!dst) { *e = pl.error(); return false; }
+    size_t got = 0;
+    if (!read_full(tin, dst, static_cast<size_t>(size), &got, e)) return false;
+    if (got < size) {
+      *e = "failed to process the file: failed to analyze file: failed to open: unable to read the file: unexpected EOF";
+      return false;
+    }
+    pl.commit(path, size);
+    return true;
+  };
+  std::string werr;
+  const bool wok = walk_layer(in, o.skip_files, o.skip_dirs, &walk, on_file, &werr);
+  out->st.feed_ms += ms_between(t_feed, Clock::now());
+  if (!wok) {
+    pl.set_error(werr);
+    pl.finish();
+    *err = werr;
+    return false;
+  }
+  t_feed = Clock::now();
+  pl.flush();
+  out->st.feed_ms += ms_between(t_feed, Clock::now());
+  if (!pl.finish()) { *err = pl.error(); return false; }
+  out->opq_dirs = std::move(walk.opq_dirs);
+  out->wh_files = std::move(walk.wh_files);
+  out->st.wall_ms = ms_between(t0, Clock::now());
+  return true;
+}
+
+bool plan_fs_tree(const Ruleset& rs, const FeedOpts& fo, const std::string& root,
+                  const std::vector<std::string>& skip_files, const std::vector<std::string>& skip_dirs, int threads,
+                  FsWalk* walk, std::vector<uint32_t>* keep, std::string* err) {
+  keep->clear();
+  walk_fs_tree(root, skip_files, skip_dirs, threads, walk, err);   // an error is kept in walk->err
+  stat_fs_files(walk, threads);                                     // d.Info() of every walked file
+  // AnalyzeFile's gate before the file is opened (analyzer.go:417-419): the
+  // path part first (in parallel), then Required's size check on info.Size()
+  const uint32_t n = static_cast<uint32_t>(walk->files.size());
+  std::vector<uint8_t> want(n, 0);
+  {
+    std::atomic<uint32_t> next{0};
+    auto run = [&]() {
+      for (;;) {
+        const uint32_t b = next.fetch_add(256);
+        if (b >= n) break;
+        for (uint32_t i = b; i < std::min(n, b + 256); ++i)
+          want[i] = static_cast<uint8_t>(secret_analyzer_wants_path(rs, fo, walk->files[i].rel));
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int t = 1; t < std::min<int>(threads, static_cast<int>(n / 256) + 1); ++t) ts.emplace_back(run);
+    run();
+    for (auto& th : ts) th.join();
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!want[i]) continue;
+    const FsFile& f = walk->files[i];
+    // files at or after the walk's first error are never reached in Go
+    if (walk->failed && !walk_order_less(f.rel, walk->err_key)) break;
+    if (f.size == UINT64_MAX || (want[i] == 2 && f.size < 10)) continue;   // secret.go:154-156
+    keep->push_back(i);
+  }
+  if (walk->failed) *err = walk->err;
+  return !walk->failed;
+}
+
+bool stream_fs_tree(const Ruleset& rs, const StreamOpts& o, const std::string& root, const BatchScanFn& scan,
+                    StreamResult* out, std::string* err) {
+  *out = StreamResult();
+  const auto t0 = Clock::now();
+  FsWalk walk;
+  std::vector<uint32_t> keep;
+  std::string perr;
+  const bool planned = plan_fs_tree(rs, o.feed, root, o.skip_files, o.skip_dirs, o.threads, &walk, &keep, &perr);
+  for (const FsFile& f : walk.files) {
+    if (walk.failed && !walk_order_less(f.rel, walk.err_key)) break;
+    out->walked.push_back(f.rel);
+    if (f.size != UINT64_MAX) out->st.walked_bytes += f.size;
+  }
+  Pipeline pl(rs, o, scan, "", out);
+  out->st.feed_ms += ms_between(t0, Clock::now());
+  // batches of consecutive kept files (walk order), each read by the reader
+  // threads straight into the raw batch, then prepared and handed on
+  size_t k = 0;
+  while (k < keep.size()) {
+    const auto t1 = Clock::now();
+    size_t e = k;
+    uint64_t bytes = 0;
+    while (e < keep.size() && (e == k || bytes + walk.files[keep[e]].size <= o.batch_bytes)) bytes += walk.files[keep[e++]].size;
+    uint8_t* dst = pl.reserve(bytes);
+    if (!dst) break;
+    std::vector<uint32_t> idx(keep.begin() + static_cast<long>(k), keep.begin() + static_cast<long>(e));
+    std::vector<uint64_t> starts(idx.size()), got;
+    uint64_t at = 0;
+    for (size_t j = 0; j < idx.size(); ++j) { starts[j] = at; at += walk.files[idx[j]].size; }
+    std::string rerr;
+    if (!read_fs_files(walk, idx, starts, dst, o.threads, &got, &rerr)) {
+      // an open error halts the walk there, unless an earlier walk error did
+      pl.set_error(rerr);
+      pl.finish();
+      *err = rerr;
+      return false;
+    }
+    // commit in order, packing out the files that vanished / shrank
+    uint64_t wpos = 0;
+    for (size_t j = 0; j < idx.size(); ++j) {
+      if (got[j] == UINT64_MAX) continue;
+      if (wpos != starts[j]) std::memmove(dst + wpos, dst + starts[j], got[j]);
+      pl.commit(walk.files[idx[j]].rel, got[j]);
+      wpos += got[j];
+    }
+    out->st.feed_ms += ms_between(t1, Clock::now());
+    if (!pl.flush()) break;
+    k = e;
+  }
+  if (!pl.finish()) { *err = pl.error(); return false; }
+  if (!planned) { *err = perr; return false; }
+  out->st.wall_ms = ms_between(t0, Clock::now());
+  return true;
+}
+
+}  // namespace tsg

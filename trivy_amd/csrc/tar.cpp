@@ -6,6 +6,7 @@
 // opaque-directory and whiteout lists it returns.
 #include "tar.h"
 
+#include <algorithm>
 #include <cstring>
 
 namespace tsg {
@@ -298,8 +299,45 @@ bool doublestar_match(const std::string& pattern, const std::string& name) {
   return false;
 }
 
-bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::string>& skip_files_in,
-                    const std::vector<std::string>& skip_dirs_in, LayerWalk* out, std::string* err) {
+bool TarInput::skip(uint64_t n, uint64_t* got, std::string* err) {
+  uint8_t buf[16384];
+  *got = 0;
+  while (*got < n) {
+    size_t g = 0;
+    if (!read(buf, static_cast<size_t>(std::min<uint64_t>(sizeof(buf), n - *got)), &g, err)) return false;
+    if (g == 0) break;
+    *got += g;
+  }
+  return true;
+}
+
+bool read_full(TarInput& in, uint8_t* dst, size_t n, size_t* got, std::string* err) {
+  *got = 0;
+  while (*got < n) {
+    size_t g = 0;
+    if (!in.read(dst + *got, n - *got, &g, err)) return false;
+    if (g == 0) break;
+    *got += g;
+  }
+  return true;
+}
+
+bool MemTarInput::read(uint8_t* dst, size_t n, size_t* got, std::string*) {
+  const size_t k = static_cast<size_t>(std::min<uint64_t>(n, n_ - pos));
+  std::memcpy(dst, p_ + pos, k);
+  pos += k;
+  *got = k;
+  return true;
+}
+
+bool MemTarInput::skip(uint64_t n, uint64_t* got, std::string*) {
+  *got = std::min<uint64_t>(n, n_ - pos);
+  pos += *got;
+  return true;
+}
+
+bool walk_layer(TarInput& in, const std::vector<std::string>& skip_files_in, const std::vector<std::string>& skip_dirs_in,
+                LayerWalk* out, const TarFileFn& on_file, std::string* err) {
   auto clean_skip = [](const std::vector<std::string>& v) {   // utils.CleanSkipPaths
     std::vector<std::string> r;
     for (const auto& s : v) r.push_back(trim_left_slash(go_path_clean(s)));
@@ -316,19 +354,29 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
     *err = std::string("failed to extract the archive: archive/tar: ") + what;
     return false;
   };
-  size_t pos = 0;
+  // the data of the entry just read (size bytes) plus its block padding
+  auto skip_data = [&](uint64_t n) {
+    uint64_t got = 0;
+    if (!in.skip(n, &got, err)) return false;
+    if (got < n) return fail("unexpected EOF");
+    return true;
+  };
+  constexpr uint64_t kMaxSpecialFileSize = 1 << 20;           // archive/tar maxSpecialFileSize
+  uint8_t h[kBlock];
+  std::vector<uint8_t> special;
   std::string long_name, pax_path;
   bool has_long = false, has_pax_path = false, has_pax_size = false;
   int64_t pax_size = 0;
   for (;;) {
-    if (pos + kBlock > len) {
-      if (pos == len) return true;                          // io.EOF at a block boundary
-      return fail("unexpected EOF");
-    }
-    const uint8_t* h = tar + pos;
+    size_t got = 0;
+    if (!read_full(in, h, kBlock, &got, err)) return false;
+    if (got == 0) return true;                                 // io.EOF at a block boundary
+    if (got < kBlock) return fail("unexpected EOF");
     if (all_zero(h)) {
       // end of archive: a second zero block (or the end of the data) must follow
-      if (pos + 2 * kBlock <= len && !all_zero(h + kBlock)) return fail("invalid tar header");
+      uint8_t h2[kBlock];
+      if (!read_full(in, h2, kBlock, &got, err)) return false;
+      if (got == kBlock && !all_zero(h2)) return fail("invalid tar header");
       return true;
     }
     if (!checksum_ok(h)) return fail("invalid tar header");
@@ -348,11 +396,15 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
       const std::string prefix = field(h + 345, 155);       // POSIX ustar prefix
       if (!prefix.empty()) name = prefix + "/" + name;
     }
-    const uint64_t data_off = pos + kBlock;
     const uint64_t padded = (static_cast<uint64_t>(size) + kBlock - 1) / kBlock * kBlock;
     if (type == 'x' || type == 'g' || type == 'L' || type == 'K') {
-      if (static_cast<uint64_t>(size) > len - data_off) return fail("unexpected EOF");
-      const uint8_t* d = tar + data_off;
+      // readSpecialFile: at most 1 MiB, read whole (a shorter archive is an unexpected EOF)
+      if (static_cast<uint64_t>(size) > kMaxSpecialFileSize) return fail("header field too long");
+      special.resize(static_cast<size_t>(size));
+      if (!read_full(in, special.data(), special.size(), &got, err)) return false;
+      if (got < special.size()) return fail("unexpected EOF");
+      if (!skip_data(padded - static_cast<uint64_t>(size))) return false;
+      const uint8_t* d = special.data();
       if (type == 'x') {
         if (!parse_pax(d, static_cast<size_t>(size), &pax_path, &has_pax_path, &pax_size, &has_pax_size))
           return fail("invalid tar header");
@@ -362,14 +414,12 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
       }
       // 'g' (global PAX) is returned by Next as its own entry: Walk skips it
       // (default case); 'K' (GNU long link name) only affects Linkname
-      pos = data_off + padded;
       continue;
     }
     if (has_long) name = long_name;
     if (has_pax_path) name = pax_path;
     if (has_pax_size) size = pax_size;
     has_long = has_pax_path = has_pax_size = false;
-    const uint64_t padded2 = (static_cast<uint64_t>(size) + kBlock - 1) / kBlock * kBlock;
     char tf = type;
     // Reader.Next: TypeRegA ('\0') becomes TypeDir for names ending in '/', else TypeReg
     if (tf == '\0') tf = (!name.empty() && name.back() == '/') ? '5' : '0';
@@ -377,31 +427,41 @@ bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::strin
     // fifos) consume no data whatever their size field says
     const bool has_data = !(tf == '1' || tf == '2' || tf == '3' || tf == '4' || tf == '5' || tf == '6');
     if (has_data && size < 0) return fail("invalid tar header");   // handleRegularFile: Size < 0 is ErrHeader
-    if (has_data && static_cast<uint64_t>(size) > len - data_off) return fail("unexpected EOF");
-    pos = data_off + (has_data ? padded2 : 0);
+    const uint64_t data_bytes = has_data ? static_cast<uint64_t>(size) : 0;
+    const uint64_t data_padded = has_data ? (data_bytes + kBlock - 1) / kBlock * kBlock : 0;
+    if (data_padded < data_bytes) return fail("invalid tar header");   // size near 2^64: no padded length
     // ---- walker.LayerTar.Walk (tar.go:46-90)
     std::string file_path = trim_left_slash(go_path_clean(name));
     std::string dir, fname;
     go_path_split(file_path, &dir, &fname);
-    if (fname == ".wh..wh..opq") { out->opq_dirs.push_back(dir); continue; }
-    if (fname.rfind(".wh.", 0) == 0) {
-      const std::string rest = fname.substr(4);
-      out->wh_files.push_back(go_path_clean(dir + rest));  // path.Join(fileDir, name)
-      continue;
-    }
-    if (tf == '5') {
+    bool hand = false;
+    if (fname == ".wh..wh..opq") {
+      out->opq_dirs.push_back(dir);
+    } else if (fname.rfind(".wh.", 0) == 0) {
+      out->wh_files.push_back(go_path_clean(dir + fname.substr(4)));   // path.Join(fileDir, name)
+    } else if (tf == '5') {
       if (skip_path(file_path, skip_dirs)) skipped_dirs.push_back(file_path);
-      continue;                                            // a directory reaches AnalyzeFile, which returns at IsDir
-    } else if (tf == '0') {                                // TypeReg
-      if (skip_path(file_path, skip_files)) continue;
-    } else {
-      continue;                                            // Walk's default: links, devices, TypeCont, sparse, ...
+      // a directory reaches AnalyzeFile, which returns at IsDir
+    } else if (tf == '0' && !skip_path(file_path, skip_files)) {   // TypeReg; others: Walk's default
+      hand = true;
+      for (const auto& sd : skipped_dirs) if (!rel_escapes(sd, file_path)) { hand = false; break; }
     }
-    bool under = false;
-    for (const auto& sd : skipped_dirs) if (!rel_escapes(sd, file_path)) { under = true; break; }
-    if (under) continue;
-    out->files.push_back(TarFile{file_path, data_off, static_cast<uint64_t>(size)});
+    uint64_t consumed = 0;
+    if (hand) {
+      out->files.push_back(TarFile{file_path, in.pos, data_bytes});
+      const uint64_t p0 = in.pos;
+      if (on_file && !on_file(file_path, data_bytes, in, err)) return false;
+      consumed = in.pos - p0;
+      if (consumed > data_bytes) { *err = "internal: file reader overran its entry"; return false; }
+    }
+    if (!skip_data(data_padded - consumed)) return false;
   }
+}
+
+bool walk_layer_tar(const uint8_t* tar, size_t len, const std::vector<std::string>& skip_files,
+                    const std::vector<std::string>& skip_dirs, LayerWalk* out, std::string* err) {
+  MemTarInput in(tar, len);
+  return walk_layer(in, skip_files, skip_dirs, out, nullptr, err);
 }
 
 }  // namespace tsg

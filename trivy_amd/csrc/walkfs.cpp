@@ -81,18 +81,6 @@ bool skip_path(const std::string& path, const std::vector<std::string>& pats) { 
   return false;
 }
 
-// Go's WalkDir order is a pre-order DFS with every directory's entries in
-// name order; with '/' ranked below every other byte, a plain comparison of
-// the relative paths gives the same order (names hold no '/' or NUL).
-bool walk_order_less(const std::string& a, const std::string& b) {
-  const size_t n = std::min(a.size(), b.size());
-  for (size_t i = 0; i < n; ++i) {
-    const unsigned char x = a[i] == '/' ? 0 : static_cast<unsigned char>(a[i]);
-    const unsigned char y = b[i] == '/' ? 0 : static_cast<unsigned char>(b[i]);
-    if (x != y) return x < y;
-  }
-  return a.size() < b.size();
-}
 
 // The walk, directories read by several threads (each directory is one task;
 // results are put back into WalkDir's order at the end).  Regular files are
@@ -134,6 +122,10 @@ struct Walker {
       if (type == DT_UNKNOWN) {
         struct stat sb;
         if (::fstatat(dfd, e->d_name, &sb, AT_SYMLINK_NOFOLLOW) != 0) {
+          // os.ReadDir: an entry that vanished between readdir and lstat is
+          // skipped as if it never existed (dir_unix.go); other errors end
+          // the directory's read
+          if (errno == ENOENT) { errno = 0; continue; }
           if (!is_permission(errno)) fail(rel, path + "/" + e->d_name, "lstat: " + go_errno(errno));
           continue;
         }
@@ -192,6 +184,26 @@ struct Walker {
 
 std::string go_filepath_clean(const std::string& p) { return go_path_clean(p); }
 
+// Go's WalkDir order is a pre-order DFS with every directory's entries in
+// name order; with '/' ranked below every other byte, a plain comparison of
+// the relative paths gives the same order (names hold no '/' or NUL).
+bool walk_order_less(const std::string& a, const std::string& b) {
+  const size_t n = std::min(a.size(), b.size());
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned char x = a[i] == '/' ? 0 : static_cast<unsigned char>(a[i]);
+    const unsigned char y = b[i] == '/' ? 0 : static_cast<unsigned char>(b[i]);
+    if (x != y) return x < y;
+  }
+  return a.size() < b.size();
+}
+
+void FsWalk::fail_at(const std::string& key, const std::string& msg) {
+  if (failed && !walk_order_less(key, err_key)) return;
+  failed = true;
+  err = msg;
+  err_key = key;
+}
+
 std::vector<std::string> build_skip_paths(const std::string& base, const std::vector<std::string>& paths) {
   std::vector<std::string> out;
   const std::string abs_base = go_abs(base);
@@ -219,7 +231,8 @@ bool walk_fs_tree(const std::string& root, const std::vector<std::string>& skip_
   struct stat sb;
   if (::lstat(root.c_str(), &sb) != 0) {
     if (is_permission(errno)) return true;
-    *err = "walk dir error: unknown error with " + root + ": lstat " + root + ": " + go_errno(errno);
+    out->fail_at("", "walk dir error: unknown error with " + root + ": lstat " + root + ": " + go_errno(errno));
+    *err = out->err;
     return false;
   }
   if (S_ISREG(sb.st_mode)) {
@@ -230,27 +243,33 @@ bool walk_fs_tree(const std::string& root, const std::vector<std::string>& skip_
   Walker w{skip_files, skip_dirs};
   w.todo.emplace_back(root, ".");
   w.run(std::max(1, threads));
+  out->files = std::move(w.files);
   if (w.failed) {
     // Go stops at the first error in walk order; files after it are not walked
-    *err = w.err;
+    out->fail_at(w.err_key, w.err);
+    *err = out->err;
     return false;
   }
-  out->files = std::move(w.files);
   return true;
 }
 
-bool stat_fs_files(FsWalk* walk, const std::vector<uint8_t>& want, int threads) {
+bool stat_fs_files(FsWalk* walk, int threads) {
   const uint32_t n = static_cast<uint32_t>(walk->files.size());
   std::atomic<uint32_t> next{0};
+  std::vector<int> errs(n, 0);
   auto run = [&]() {
     for (;;) {
       const uint32_t b = next.fetch_add(64);
       if (b >= n) break;
       for (uint32_t i = b; i < std::min(n, b + 64); ++i) {
-        if (!want[i]) continue;
         struct stat sb;
         FsFile& f = walk->files[i];
-        f.size = ::lstat(f.path.c_str(), &sb) == 0 ? static_cast<uint64_t>(sb.st_size) : UINT64_MAX;
+        if (::lstat(f.path.c_str(), &sb) == 0) {
+          f.size = static_cast<uint64_t>(sb.st_size);
+        } else {
+          f.size = UINT64_MAX;
+          errs[i] = errno;
+        }
       }
     }
   };
@@ -259,43 +278,49 @@ bool stat_fs_files(FsWalk* walk, const std::vector<uint8_t>& want, int threads) 
   for (int t = 1; t < nt; ++t) ts.emplace_back(run);
   run();
   for (auto& th : ts) th.join();
-  return true;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!errs[i]) continue;
+    // d.Info() (fs.go:67-70): xerrors-wrapped, so not even a permission error
+    // is ignored by onError -- the walk halts here
+    const FsFile& f = walk->files[i];
+    walk->fail_at(f.rel, "walk dir error: unknown error with " + f.path + ": file info error: lstat " + f.path + ": " +
+                             go_errno(errs[i]));
+    break;                                                        // files are in walk order: the first is the earliest
+  }
+  return !walk->failed;
 }
 
-bool read_fs_files(const FsWalk& walk, const std::vector<uint8_t>& want, const std::vector<uint64_t>& starts,
+bool read_fs_files(const FsWalk& walk, const std::vector<uint32_t>& idx, const std::vector<uint64_t>& starts,
                    uint8_t* buf, int threads, std::vector<uint64_t>* got, std::string* err) {
-  const uint32_t n = static_cast<uint32_t>(walk.files.size());
+  const uint32_t n = static_cast<uint32_t>(idx.size());
   got->assign(n, 0);
   std::atomic<uint32_t> next{0};
-  std::atomic<bool> failed{false};
-  std::string first_err;
-  std::mutex mu;
+  std::atomic<uint32_t> first_bad{UINT32_MAX};                   // earliest failing position in idx
+  std::vector<int> errs(n, 0);
   auto run = [&]() {
     for (;;) {
-      const uint32_t i = next.fetch_add(1);
-      if (i >= n || failed.load(std::memory_order_relaxed)) break;
-      if (!want[i]) continue;
-      const FsFile& f = walk.files[i];
+      const uint32_t k = next.fetch_add(1);
+      if (k >= n || k > first_bad.load(std::memory_order_relaxed)) break;
+      const FsFile& f = walk.files[idx[k]];
       const int fd = ::open(f.path.c_str(), O_RDONLY | O_CLOEXEC);
       if (fd < 0) {
-        if (is_permission(errno)) { (*got)[i] = UINT64_MAX; continue; }   // AnalyzeFile: ErrPermission -> skip
-        std::lock_guard<std::mutex> lk(mu);
-        if (!failed.exchange(true))
-          first_err = "walk dir error: unknown error with " + f.path + ": failed to analyze file: unable to open " +
-                      f.rel + ": open " + f.path + ": " + go_errno(errno);
-        break;
+        if (is_permission(errno)) { (*got)[k] = UINT64_MAX; continue; }   // AnalyzeFile: ErrPermission -> skip
+        errs[k] = errno;
+        uint32_t cur = first_bad.load();
+        while (k < cur && !first_bad.compare_exchange_weak(cur, k)) {}
+        continue;
       }
       uint64_t done = 0;
       bool rerr = false;
       while (done < f.size) {
-        const ssize_t r = ::pread(fd, buf + starts[i] + done, f.size - done, static_cast<off_t>(done));
+        const ssize_t r = ::pread(fd, buf + starts[k] + done, f.size - done, static_cast<off_t>(done));
         if (r < 0 && errno == EINTR) continue;
         if (r < 0) { rerr = true; break; }                        // Analyze's read error: no result
         if (r == 0) break;                                        // shrunk since the walk: what is there
         done += static_cast<uint64_t>(r);
       }
       ::close(fd);
-      (*got)[i] = rerr ? UINT64_MAX : done;
+      (*got)[k] = rerr ? UINT64_MAX : done;
     }
   };
   const int nt = std::max(1, std::min<int>(threads, static_cast<int>(std::max<uint32_t>(n, 1))));
@@ -303,7 +328,13 @@ bool read_fs_files(const FsWalk& walk, const std::vector<uint8_t>& want, const s
   for (int t = 1; t < nt; ++t) ts.emplace_back(run);
   run();
   for (auto& th : ts) th.join();
-  if (failed) { *err = first_err; return false; }
+  const uint32_t k = first_bad.load();
+  if (k != UINT32_MAX) {
+    const FsFile& f = walk.files[idx[k]];
+    *err = "walk dir error: unknown error with " + f.path + ": failed to analyze file: unable to open " + f.rel +
+           ": open " + f.path + ": " + go_errno(errs[k]);
+    return false;
+  }
   return true;
 }
 

@@ -368,6 +368,71 @@ def PrepareFsTree(scanner, root, skip_files=(), skip_dirs=(), file_patterns=(), 
         L.tsg_prepared_free(h)
 
 
+def _reader(fileobj):
+    """A tsg_read_fn over a Python binary file object (io.Reader)."""
+    def read(_user, buf, cap):
+        try:
+            b = fileobj.read(min(cap, 1 << 22))
+        except Exception:                      # noqa: BLE001 -- a reader error ends the walk
+            return -1
+        if not b:
+            return 0
+        ctypes.memmove(buf, b, len(b))
+        return len(b)
+    return _lib.READ_FN(read)
+
+
+def _stream_result(L, rc, res, as_result):
+    if rc != 0:
+        raise WalkError(L.tsg_last_error().decode("utf-8", "replace"))
+    walk = json.loads(L.tsg_result_walk_json(res).decode("utf-8", "surrogateescape"))
+    if as_result:
+        from .report import ScanResult
+        return ScanResult(res), walk
+    try:
+        secrets = _lib.result_json(res)
+    finally:
+        L.tsg_result_free(res)
+    for sec in secrets:
+        sec.pop("Error", None)
+    return secrets, walk
+
+
+def ScanLayerStream(scanner, fileobj, skip_files=(), skip_dirs=(), file_patterns=(), config_path="", threads=0,
+                    batch_bytes=0, as_result=False, model=False):
+    """One container layer read from a binary file object in order (an
+    io.Reader): walker.LayerTar.Walk -> AnalyzeFile's gate -> Analyze's prep ->
+    Scan, in bounded batches scanned while the next one is read
+    (tsg_scan_layer_stream).  Returns ([types.Secret] of every scanned file in
+    walk order, walk dict with "files", "opq_dirs", "wh_files", "stats");
+    as_result=True gives a report.ScanResult in place of the list.
+    model=True runs the CPU model of the GPU passes (tests)."""
+    L = _lib.lib()
+    o, keep = _lib.feed_opts(config_path, file_patterns, skip_files, skip_dirs, threads)
+    cb = _reader(fileobj)
+    res = ctypes.c_void_p()
+    if model:
+        rc = L.tsg_scan_layer_stream_model(scanner._rs, cb, None, ctypes.byref(o), batch_bytes, ctypes.byref(res))
+    else:
+        rc = L.tsg_scan_layer_stream(scanner.engine(), cb, None, ctypes.byref(o), batch_bytes, ctypes.byref(res))
+    return _stream_result(L, rc, res, as_result)
+
+
+def ScanFsTree(scanner, root, skip_files=(), skip_dirs=(), file_patterns=(), config_path="", threads=0,
+               batch_bytes=0, as_result=False, model=False):
+    """`trivy fs ROOT` streamed (tsg_scan_fs_tree): the walk and gate of
+    PrepareFsTree, the kept files read in walk order in bounded batches, each
+    scanned while the next is read.  Returns ([types.Secret], walk dict)."""
+    L = _lib.lib()
+    o, keep = _lib.feed_opts(config_path, file_patterns, skip_files, skip_dirs, threads)
+    res = ctypes.c_void_p()
+    if model:
+        rc = L.tsg_scan_fs_tree_model(scanner._rs, os.fsencode(root), ctypes.byref(o), batch_bytes, ctypes.byref(res))
+    else:
+        rc = L.tsg_scan_fs_tree(scanner.engine(), os.fsencode(root), ctypes.byref(o), batch_bytes, ctypes.byref(res))
+    return _stream_result(L, rc, res, as_result)
+
+
 # ---------------------------------------------------------------- test hooks
 def scan_host_reference(scanner, args_list, threads=1):
     """The C++ confirmer on every (file, rule) pair, no prefilter (tests only)."""
