@@ -167,9 +167,10 @@ class PinnedBatch:
             self.ptr = ctypes.c_void_p()
 
 
-def layer_tar_rate(L, sc, batch, target_bytes, threads):
+def layer_tar_rate(L, sc, batch, target_bytes, threads, stream_batch=256 << 20):
     """tsg_prepare_layer_tar over one PAX layer tar built from the batch's files
-    (rate in tar bytes per second, pinned output)."""
+    (rate in tar bytes per second, pinned output), and the same layer through
+    tsg_scan_layer_stream end to end (tar bytes -> findings)."""
     import io
     import tarfile
     from trivy_amd import _lib
@@ -185,7 +186,8 @@ def layer_tar_rate(L, sc, batch, target_bytes, threads):
             tot += len(c)
             if tot >= target_bytes:
                 break
-    tar = np.frombuffer(buf.getvalue(), dtype=np.uint8)
+    tar_bytes = buf.getvalue()
+    tar = np.frombuffer(tar_bytes, dtype=np.uint8)
     best, kept = None, 0
     for _ in range(3):
         h = ctypes.c_void_p()
@@ -200,7 +202,21 @@ def layer_tar_rate(L, sc, batch, target_bytes, threads):
         kept = nk.value
         L.tsg_prepared_free(h)
         best = dt if best is None else min(best, dt)
-    return len(tar) / best / 1e9, nfiles, kept, best
+    # the same layer streamed end to end (tsg_scan_layer_stream: walk + gate +
+    # prep of batch k+1 overlapping the GPU scan of batch k) -> findings
+    from trivy_amd import secret as S
+    sbest, swalk, nfind = None, None, 0
+    for _ in range(3):
+        t0 = time.perf_counter()
+        got, walk = S.ScanLayerStream(sc, io.BytesIO(tar_bytes), threads=threads, batch_bytes=stream_batch)
+        dt = time.perf_counter() - t0
+        if sbest is None or dt < sbest:
+            sbest, swalk, nfind = dt, walk, sum(len(g["Findings"]) for g in got)
+    stream = {"gbps": round(len(tar) / sbest / 1e9, 2), "s": round(sbest, 4), "findings": nfind,
+              "batches": swalk["stats"]["batches"], "feed_ms": round(swalk["stats"]["feed_ms"], 1),
+              "scan_ms": round(swalk["stats"]["scan_ms"], 1), "wait_ms": round(swalk["stats"]["wait_ms"], 1),
+              "batch_bytes": stream_batch, "of_walk_rate": round(best / sbest, 3)}
+    return len(tar) / best / 1e9, nfiles, kept, best, stream
 
 
 def _fs_type(path):
@@ -286,6 +302,18 @@ def tree_feed(L, sc, batch, threads, base_dir):
         warm, _ = run(False)
         drop_cache()
         cold, (tree_files, tree_res) = run(True)
+        # the same tree streamed (tsg_scan_fs_tree: reads + prep of batch k+1
+        # overlapping the scan of batch k), page cache dropped again
+        from trivy_amd import secret as S
+        drop_cache()
+        t1 = time.perf_counter()
+        sres, swalk = S.ScanFsTree(sc, root, threads=threads, batch_bytes=256 << 20)
+        sdt = time.perf_counter() - t1
+        streamed = {"s": round(sdt, 4), "end_to_end_gbps": round(swalk["stats"]["read_bytes"] / sdt / 1e9, 3),
+                    "batches": swalk["stats"]["batches"], "feed_ms": round(swalk["stats"]["feed_ms"], 1),
+                    "scan_ms": round(swalk["stats"]["scan_ms"], 1),
+                    "same_findings": {r["FilePath"]: r for r in sres if r["FilePath"]} ==
+                                     {k: v for k, v in tree_res.items() if v["FilePath"]}}
         # parity: the tree's prepared files == tsg_prepare_batch over the same files in memory
         o, _k = _lib.feed_opts(threads=threads)
         h = ctypes.c_void_p()
@@ -303,13 +331,74 @@ def tree_feed(L, sc, batch, threads, base_dir):
         L.tsg_prepared_free(h)
         same = mem == tree_files
         return {"files": batch.nfiles, "bytes": batch.nbytes, "dir_fs": _fs_type(os.path.realpath(root)),
-                "write_s": round(t_write, 2), "warm": warm, "cold": cold, "prepared_equal_in_memory": same,
+                "write_s": round(t_write, 2), "warm": warm, "cold": cold, "streamed_cold": streamed,
+                "prepared_equal_in_memory": same,
                 "findings": sum(len(r["Findings"]) for r in tree_res.values()),
                 "note": "tsg_prepare_fs_tree: walk + gate + %d reader threads + prep into pinned memory; cold = page "
                         "cache dropped per file (posix_fadvise DONTNEED after sync; no effect on tmpfs); the cold "
                         "batch then scanned by tsg_scan_batch (end_to_end = disk -> findings)" % threads}
     finally:
         shutil.rmtree(root, ignore_errors=True)
+
+
+def small_batches(L, eng, batch, counts=(1, 5, 64), reps=40):
+    """tsg_scan_batch latency on batches of 1 / 5 / 64 files of 8-32 KB (the
+    per-file drop-in's batch sizes: unchanged Trivy calls Scan per file from
+    --parallel goroutines, secret.go:137), pinned host memory, median of reps."""
+    from trivy_amd import _lib
+    sizes = np.diff(batch.offsets)
+    pick = [i for i in range(batch.nfiles) if (8 << 10) <= sizes[i] <= (32 << 10)][:max(counts)]
+    out = {}
+    if len(pick) < max(counts):
+        return {"note": "not enough 8-32 KB files in the batch"}
+    for n in counts:
+        files = [batch.file(i) for i in pick[:n]]
+        offs = np.zeros(n + 1, np.uint64)
+        offs[1:] = np.cumsum([len(f) for f in files])
+        ptr, view = _alloc_pinned(L, int(offs[-1]) + 64)
+        view[:int(offs[-1])] = np.frombuffer(b"".join(files), np.uint8)
+        view[int(offs[-1]):] = 0
+        paths, lens, _k = _lib.pack_paths([batch.paths[i] for i in pick[:n]])
+        ts = []
+        for r in range(reps + 3):
+            res = ctypes.c_void_p()
+            t0 = time.perf_counter()
+            _lib.check(L.tsg_scan_batch(eng, ptr, offs.ctypes.data, n, paths, lens, None, ctypes.byref(res)))
+            dt = time.perf_counter() - t0
+            L.tsg_result_free(res)
+            if r >= 3:
+                ts.append(dt)
+        L.tsg_free_pinned(ptr)
+        med = float(np.median(ts))
+        out[str(n)] = {"ms": round(med * 1e3, 3), "p90_ms": round(float(np.percentile(ts, 90)) * 1e3, 3),
+                       "bytes": int(offs[-1]), "gbps": round(int(offs[-1]) / med / 1e9, 4)}
+    return out
+
+
+def per_file_queue(sc, batch, callers_list, max_bytes=256 << 20, target_bytes=256e6):
+    """The per-file drop-in: `callers` threads (--parallel goroutines) each
+    calling Scan on one file at a time through the shared queue (tsg_queue_*),
+    over the batch's first files up to target_bytes."""
+    from trivy_amd import secret as S
+    n, tot = 0, 0
+    while n < batch.nfiles and tot < target_bytes:
+        tot += int(batch.offsets[n + 1] - batch.offsets[n])
+        n += 1
+    args = [S.ScanArgs(batch.paths[i], batch.file(i)) for i in range(n)]
+    out = {"files": n, "bytes": tot}
+    for c in callers_list:
+        q = S.ScanQueue(sc, max_bytes=max_bytes)
+        q.probe(args[:min(n, 200)], c)                       # warm (lanes, staging buffers)
+        q.close()
+        q = S.ScanQueue(sc, max_bytes=max_bytes)
+        sec, nf = q.probe(args, c)
+        st = q.stats()
+        q.close()
+        out["parallel_%d" % c] = {"gbps": round(tot / sec / 1e9, 4), "files_per_s": round(n / sec),
+                                  "s": round(sec, 3), "findings": nf, "batches": st["batches"],
+                                  "mean_batch_files": round(st["files"] / max(1, st["batches"]), 2),
+                                  "max_batch_files": st["max_batch"]}
+    return out
 
 
 def numa_bind(device):
@@ -404,6 +493,15 @@ def launch_ranks(n, argv, dry=False):
     return rc
 
 
+def gather_ranks(dist, world, mine):
+    """Every rank's record on every rank (gloo all_gather_object), rank order."""
+    if not dist:
+        return [mine]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    return got
+
+
 def _segment_bytes():
     v = os.environ.get("TSG_SEGMENT_BYTES")
     return int(v) if v and int(v) >= 4096 else 4 << 30
@@ -435,6 +533,9 @@ def main():
                     help="1: also measure the `trivy fs` feed over the batch written as a directory tree "
                          "(default: config 1 only)")
     ap.add_argument("--tree-dir", default=os.environ.get("TSG_TREE_DIR", "/tmp"))
+    ap.add_argument("--per-file", type=int, default=-1,
+                    help="1: also time the per-file drop-in (small batches, the Scan queue at --parallel 5 and at "
+                         "the rank's core count); default: config 1 only")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--dry-launch", action="store_true",
                     help="ranks only report their wiring (rank, device, device_mask) and exit: the launcher's "
@@ -455,16 +556,25 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
     if args.dry_launch:
+        # the wiring, and the per-rank gather the real run uses for its
+        # concurrent feed ceiling (a host memcpy probe stands in for the PCIe
+        # upload, every rank at once after a barrier)
         wiring = {"rank": rank, "world": world, "local_rank": local_rank, "device": local_rank,
                   "device_mask": 1 << local_rank}
-        got = [None] * world
         if dist:
-            dist.all_gather_object(got, wiring)
+            dist.barrier()
+        src = np.ones(64 << 20, np.uint8)
+        dst = np.empty_like(src)
+        t0 = time.perf_counter()
+        for _ in range(4):
+            np.copyto(dst, src)
+        wiring["ceiling_gbps"] = round(4 * src.nbytes / (time.perf_counter() - t0) / 1e9, 2)
+        got = gather_ranks(dist, world, wiring)
+        if dist:
             dist.destroy_process_group()
-        else:
-            got = [wiring]
         if rank == 0:
-            print(json.dumps({"dry_launch": got}), flush=True)
+            print(json.dumps({"dry_launch": got, "ceiling_gbps_all_ranks": round(sum(g["ceiling_gbps"] for g in got), 2)}),
+                  flush=True)
         return
 
     import torch
@@ -721,32 +831,64 @@ def main():
         "parity": None,
     }
 
-    # host-feed ceiling: the same segmented upload with no kernels
+    # host-feed ceiling: the same segmented upload with no kernels, every rank
+    # at once after a barrier (the ranks share host DRAM and the root
+    # complexes: the concurrent sum is the node's feed ceiling)
     fms = ctypes.c_double()
+    if dist:
+        dist.barrier()
     _lib.check(L.tsg_feed_probe(eng, batch.ptr, batch.nbytes, ctypes.byref(fms)))
-    out["host_feed"]["ceiling_gbps"] = round(batch.nbytes / (fms.value / 1e3) / 1e9, 2)
-    out["host_feed"]["note"] = ("ceiling_gbps: tsg_feed_probe, the step's segmented pinned upload with no kernels; "
+    my_ceiling = batch.nbytes / (fms.value / 1e3) / 1e9
+    mine = {"rank": rank, "device": device, "numa": numa, "ceiling_gbps": round(my_ceiling, 2),
+            "link_gbps": round(nbytes / (h2d_ms / 1e3) / 1e9, 2), "step_ms": round(elapsed / args.steps * 1e3, 3),
+            "k1_ms": round(k1_ms, 3), "k2_ms": round(k2_ms, 3), "h2d_ms": round(h2d_ms, 3),
+            "host_confirm_ms": round(host_ms, 3), "bytes": nbytes}
+    ranks = gather_ranks(dist, world, mine)
+    out["host_feed"]["ceiling_gbps"] = round(my_ceiling, 2)
+    out["host_feed"]["ceiling_gbps_all_ranks"] = round(sum(r["ceiling_gbps"] for r in ranks), 2)
+    out["per_rank"] = ranks
+    out["host_feed"]["note"] = ("ceiling_gbps: tsg_feed_probe on rank 0, the step's segmented pinned upload with no "
+                                "kernels; ceiling_gbps_all_ranks: the same probe on every rank at once after a "
+                                "barrier, summed (the node's concurrent host-feed ceiling to set `value` against); "
                                 "prepare_gbps: tsg_prepare_batch over the raw files")
-    log("host-feed ceiling (segmented pinned upload, no kernels): %.1f GB/s" % out["host_feed"]["ceiling_gbps"])
+    log("host-feed ceiling (segmented pinned upload, no kernels): %.1f GB/s on rank 0, %.1f GB/s over %d ranks at "
+        "once" % (my_ceiling, out["host_feed"]["ceiling_gbps_all_ranks"], world))
     if args.config == 3 and rank == 0:
         # the image path's host feed from a layer tar: walker.LayerTar.Walk +
         # Required + content prep into pinned memory (tsg_prepare_layer_tar)
-        tgb, tfiles, tkept, tdt = layer_tar_rate(L, sc, batch, 512e6, args.threads)
+        tgb, tfiles, tkept, tdt, tstream = layer_tar_rate(L, sc, batch, 2e9, args.threads)
         out["host_feed"]["layer_tar_gbps"] = round(tgb, 2)
         out["host_feed"]["layer_tar_sample"] = "%d files / %.0f MB of this batch written as one PAX layer tar, %d " \
                                                "kept, best of 3: %.1f ms" % (tfiles, tgb * tdt * 1e3, tkept, tdt * 1e3)
-        log("layer-tar feed (walk + Required + prep into pinned memory, %d threads): %.1f GB/s" % (args.threads, tgb))
+        out["host_feed"]["layer_tar_to_findings"] = tstream
+        log("layer-tar feed (walk + Required + prep into pinned memory, %d threads): %.1f GB/s; streamed end to end "
+            "(tar -> findings, tsg_scan_layer_stream): %.1f GB/s = %.2f of the walk rate" % (
+                args.threads, tgb, tstream["gbps"], tstream["of_walk_rate"]))
 
     if rank == 0 and (args.tree == 1 or (args.tree == -1 and args.config == 1)):
         tr = tree_feed(L, sc, batch, args.threads, args.tree_dir)
         out["host_feed"]["tree"] = tr
         out["host_feed"]["tree_read_gbps"] = {"warm": tr["warm"]["gbps"], "cold": tr["cold"]["gbps"]}
-        log("fs-tree feed (%d files on %s): warm %.2f GB/s, cold %.2f GB/s, disk -> findings %.2f GB/s; "
-            "prepared == in-memory: %s" % (tr["files"], tr["dir_fs"], tr["warm"]["gbps"], tr["cold"]["gbps"],
-                                           tr["cold"]["end_to_end_gbps"], tr["prepared_equal_in_memory"]))
+        out["host_feed"]["tree_to_findings_gbps"] = {"prepare_then_scan": tr["cold"]["end_to_end_gbps"],
+                                                      "streamed": tr["streamed_cold"]["end_to_end_gbps"]}
+        log("fs-tree feed (%d files on %s): warm %.2f GB/s, cold %.2f GB/s, disk -> findings %.2f GB/s (streamed "
+            "%.2f GB/s, same findings %s); prepared == in-memory: %s" % (
+                tr["files"], tr["dir_fs"], tr["warm"]["gbps"], tr["cold"]["gbps"], tr["cold"]["end_to_end_gbps"],
+                tr["streamed_cold"]["end_to_end_gbps"], tr["streamed_cold"]["same_findings"],
+                tr["prepared_equal_in_memory"]))
         if not tr["prepared_equal_in_memory"]:
             print("[bench] fs-tree feed differs from the in-memory preparation", file=sys.stderr, flush=True)
             sys.exit(1)
+
+    if rank == 0 and (args.per_file == 1 or (args.per_file == -1 and args.config == 1)):
+        out["small_batch"] = small_batches(L, eng, batch)
+        out["per_file"] = per_file_queue(sc, batch, (5, cores))
+        sb = out["small_batch"]
+        log("small batches (tsg_scan_batch, 8-32 KB files): %s" % ", ".join(
+            "%s files %.3f ms" % (k, v["ms"]) for k, v in sb.items() if isinstance(v, dict)))
+        log("per-file Scan through the queue: %s" % ", ".join(
+            "%s %.3f GB/s (%.1f files/batch)" % (k, v["gbps"], v["mean_batch_files"])
+            for k, v in out["per_file"].items() if isinstance(v, dict)))
 
     if not args.no_resident:
         # the same batch already resident in HBM (reported, never `value`)
@@ -839,6 +981,10 @@ def main():
                       "(tsg_scan_host_reference), %d threads, %.2f s; diff vs oracle: %d files"
                       % (len(idx), procs, cdt, cdiff),
         }
+        if "per_file" in out:
+            for k, v in out["per_file"].items():
+                if isinstance(v, dict):
+                    v["vs_cpu_baseline_cxx"] = round(v["gbps"] / (nb / cdt / 1e9), 2)
         out["parity"] = {"sample_files": len(idx), "sample_bytes": nb, "sample_findings": ofind,
                          "diff_files": len(diff), "diff_examples": diff[:5], "cxx_diff_files": cdiff}
         failed = bool(diff) or cdiff > 0

@@ -347,6 +347,30 @@ int tsg_scan_fs_tree_model(const tsg_ruleset* rs, const char* root, const tsg_fe
  * batches, files, peak_batch_bytes}}; NULL for other results.  Owned by r. */
 const char* tsg_result_walk_json(const tsg_result* r);
 
+/* ---- per-file Scan for unchanged callers ----
+ * SecretAnalyzer.Analyze calls Scanner.Scan once per file (pkg/fanal/analyzer/
+ * secret/secret.go:137) from --parallel goroutines (analyzer.go:434-451,
+ * default 5).  A queue gathers concurrent tsg_queue_scan calls into one engine
+ * batch: a caller that finds no batch forming leads one, waits until every
+ * caller not already in a running batch has joined (or max_files / max_bytes
+ * is reached, or max_wait_us has passed), scans it, and hands each caller its
+ * own result; up to max_inflight batches run at once.  Thread-safe. */
+typedef struct tsg_queue tsg_queue;
+int tsg_queue_create(tsg_engine* e, uint32_t max_files, uint64_t max_bytes, uint32_t max_wait_us,
+                     uint32_t max_inflight, tsg_queue** out);
+void tsg_queue_destroy(tsg_queue* q);
+/* Scanner.Scan(ScanArgs{path, content, binary}) -> a one-file result */
+int tsg_queue_scan(tsg_queue* q, const char* path, size_t path_len, const uint8_t* content, size_t len, int binary,
+                   tsg_result** out);
+int tsg_queue_stats(tsg_queue* q, uint64_t* calls, uint64_t* batches, uint64_t* files, uint32_t* max_batch);
+/* Measurement hook: `callers` threads, each calling tsg_queue_scan on the
+ * next not yet scanned file of the batch until all nfiles are done (the
+ * reference's goroutines calling Scan per file); *seconds = wall time,
+ * *findings = findings over all files.  Never used by tsg_scan_batch. */
+int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                    const char* const* paths, const uint32_t* path_lens, uint32_t callers, double* seconds,
+                    uint64_t* findings);
+
 /* Test hook: Regexp.MatchString(text) for `pattern` with the required-literal
  * gate the ruleset compiler sets on path / allow regexes (*gated) and without
  * it (*plain); *has_gate = 1 if a gate was found (2: bounded). */

@@ -42,6 +42,19 @@ def test_launcher_dry_run_four_ranks():
     assert [g["device_mask"] for g in got] == [1, 2, 4, 8]
 
 
+def test_launcher_dry_run_eight_ranks():
+    # the 8-GPU node's wiring: ranks 0-7 on devices 0-7, and the per-rank
+    # gather behind the N > 1 line's concurrent feed ceiling (every rank's
+    # probe after one barrier, summed on rank 0)
+    p = _run(["--gpus", "8", "--dry-launch"], timeout=300)
+    assert p.returncode == 0, p.stderr
+    doc = json.loads(p.stdout.strip().splitlines()[-1])
+    got = doc["dry_launch"]
+    assert [(g["rank"], g["device"], g["device_mask"]) for g in got] == [(r, r, 1 << r) for r in range(8)]
+    assert all(g["world"] == 8 and g["ceiling_gbps"] > 0 for g in got)
+    assert abs(doc["ceiling_gbps_all_ranks"] - sum(g["ceiling_gbps"] for g in got)) < 0.05
+
+
 def test_gpus_beyond_visible_devices_fails_loudly():
     import torch
     if torch.cuda.device_count() >= 2:

@@ -137,6 +137,17 @@ SIGNATURES += [
     ("tsg_scan_fs_tree_model", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(TsgFeedOpts),
                                               ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     ("tsg_result_walk_json", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("tsg_queue_create", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_queue_destroy", None, [ctypes.c_void_p]),
+    ("tsg_queue_scan", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_queue_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint32)]),
+    ("tsg_queue_probe", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                       c_char_pp, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_uint64)]),
 ]
 
 

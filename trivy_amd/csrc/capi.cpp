@@ -22,6 +22,7 @@
 #include "tar.h"
 #include "prefilter.h"
 #include "report.h"
+#include "queue.h"
 #include "stream.h"
 #include "scanner.h"
 #include "walkfs.h"
@@ -1263,6 +1264,90 @@ int tsg_scan_fs_tree_model(const tsg_ruleset* rs, const char* root, const tsg_fe
   StreamResult sr;
   if (!stream_fs_tree(*rs->rs, so, root, model_stage(*rs->rs, pf), &sr, &err)) return fail(TSG_ERR_INVALID, err);
   *out = stream_result(rs->rs, std::move(sr));
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+struct tsg_queue {
+  std::unique_ptr<ScanQueue> q;
+  std::shared_ptr<const Ruleset> rs;
+};
+
+int tsg_queue_create(tsg_engine* e, uint32_t max_files, uint64_t max_bytes, uint32_t max_wait_us,
+                     uint32_t max_inflight, tsg_queue** out) {
+  TSG_API_TRY
+  if (!e || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  auto* q = new tsg_queue();
+  q->q.reset(new ScanQueue(e->eng.get(), max_files ? max_files : 4096, max_bytes ? max_bytes : (256ull << 20),
+                           max_wait_us, max_inflight ? max_inflight : 4));
+  q->rs = e->eng->ruleset();
+  *out = q;
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+void tsg_queue_destroy(tsg_queue* q) { delete q; }
+
+int tsg_queue_scan(tsg_queue* q, const char* path, size_t path_len, const uint8_t* content, size_t len, int binary,
+                   tsg_result** out) {
+  TSG_API_TRY
+  if (!q || !out || (len && !content) || (path_len && !path)) return fail(TSG_ERR_INVALID, "NULL argument");
+  Secret sec;
+  std::string err;
+  if (!q->q->scan(path ? path : "", path_len, content, len, binary != 0, &sec, &err)) return fail(TSG_ERR_HIP, err);
+  auto* r = new tsg_result();
+  r->rs = q->rs;
+  r->files.push_back(std::move(sec));
+  *out = r;
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_queue_stats(tsg_queue* q, uint64_t* calls, uint64_t* batches, uint64_t* files, uint32_t* max_batch) {
+  TSG_API_TRY
+  if (!q || !calls || !batches || !files || !max_batch) return fail(TSG_ERR_INVALID, "NULL argument");
+  const QueueStats st = q->q->stats();
+  *calls = st.calls;
+  *batches = st.batches;
+  *files = st.files;
+  *max_batch = st.max_batch;
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                    const char* const* paths, const uint32_t* path_lens, uint32_t callers, double* seconds,
+                    uint64_t* findings) {
+  TSG_API_TRY
+  if (!q || !offsets || !seconds || !findings || (nfiles && (!data || !paths)) || callers == 0)
+    return fail(TSG_ERR_INVALID, "NULL argument");
+  std::atomic<uint32_t> next{0};
+  std::atomic<uint64_t> nf{0};
+  std::atomic<bool> bad{false};
+  std::string first_err;
+  std::mutex emu;
+  auto worker = [&]() {
+    for (;;) {
+      const uint32_t i = next.fetch_add(1);
+      if (i >= nfiles || bad.load()) break;
+      Secret sec;
+      std::string err;
+      const size_t pl = path_lens ? path_lens[i] : std::strlen(paths[i]);
+      if (!q->q->scan(paths[i], pl, data + offsets[i], offsets[i + 1] - offsets[i], false, &sec, &err)) {
+        std::lock_guard<std::mutex> lk(emu);
+        if (!bad.exchange(true)) first_err = err;
+        break;
+      }
+      nf += sec.findings.size();
+    }
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> ts;
+  for (uint32_t c = 0; c < callers; ++c) ts.emplace_back(worker);
+  for (auto& t : ts) t.join();
+  *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *findings = nf.load();
+  if (bad) return fail(TSG_ERR_HIP, first_err);
   return TSG_OK;
   TSG_API_CATCH
 }

@@ -1,0 +1,67 @@
+// Per-file Scan for unchanged callers: SecretAnalyzer.Analyze calls
+// Scanner.Scan once per file (pkg/fanal/analyzer/secret/secret.go:137) from
+// --parallel goroutines (analyzer.go:434-451, default 5, pkg/flag/
+// scan_flags.go:85).  Concurrent scan() calls are gathered into one engine
+// batch: the first caller that finds no batch forming leads one, waits until
+// every caller that is not already inside a running batch has joined (or the
+// batch is full, or max_wait has passed), packs the contents into a pinned
+// staging buffer and scans them; the others sleep until their result is set.
+// Several batches may run at once (the engine is reentrant).
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+namespace tsg {
+
+struct QueueStats {
+  uint64_t calls = 0, batches = 0, files = 0, bytes = 0;
+  uint32_t max_batch = 0;
+};
+
+class ScanQueue {
+ public:
+  ScanQueue(Engine* eng, uint32_t max_files, uint64_t max_bytes, uint32_t max_wait_us, uint32_t max_inflight);
+  ~ScanQueue();
+  // Scanner.Scan(ScanArgs{path, content, binary}) through a shared batch
+  bool scan(const char* path, size_t path_len, const uint8_t* content, size_t len, bool binary, Secret* out,
+            std::string* err);
+  QueueStats stats();
+
+ private:
+  struct Req {
+    const char* path;
+    size_t path_len;
+    const uint8_t* data;
+    size_t len;
+    bool binary;
+    Secret result;
+    std::string err;
+    bool done = false;
+  };
+  struct Staging { void* p = nullptr; size_t cap = 0; };
+  void run_batch(std::vector<Req*>& batch);
+  Staging take_staging(size_t bytes);
+  void give_staging(Staging s);
+
+  Engine* eng_;
+  uint32_t max_files_, max_wait_us_, max_inflight_;
+  uint64_t max_bytes_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Req*> pending_;
+  uint64_t pending_bytes_ = 0;
+  uint32_t callers_ = 0;       // callers inside scan()
+  uint32_t in_batches_ = 0;    // of them, in a running batch
+  uint32_t inflight_ = 0;      // running batches
+  bool forming_ = false;       // a leader is gathering a batch
+  std::vector<Staging> free_staging_;
+  QueueStats st_;
+};
+
+}  // namespace tsg

@@ -433,6 +433,58 @@ def ScanFsTree(scanner, root, skip_files=(), skip_dirs=(), file_patterns=(), con
     return _stream_result(L, rc, res, as_result)
 
 
+class ScanQueue:
+    """Per-file Scanner.Scan for unchanged callers (tsg_queue_*): concurrent
+    Scan calls (SecretAnalyzer.Analyze, secret.go:137, from --parallel
+    goroutines) share one engine batch."""
+
+    def __init__(self, scanner, max_files=0, max_bytes=0, max_wait_us=200, max_inflight=0):
+        self._sc = scanner
+        self._q = ctypes.c_void_p()
+        _lib.check(_lib.lib().tsg_queue_create(scanner.engine(), max_files, max_bytes, max_wait_us, max_inflight,
+                                               ctypes.byref(self._q)))
+
+    def Scan(self, args):
+        L = _lib.lib()
+        p = args.FilePath.encode("utf-8", "surrogateescape")
+        c = args.Content
+        buf = (ctypes.c_char * max(1, len(c))).from_buffer_copy(c) if c else None
+        res = ctypes.c_void_p()
+        _lib.check(L.tsg_queue_scan(self._q, p, len(p), buf, len(c), 1 if args.Binary else 0, ctypes.byref(res)))
+        try:
+            out = _lib.result_json(res)[0]
+        finally:
+            L.tsg_result_free(res)
+        out.pop("Error", None)
+        return out
+
+    def stats(self):
+        v = [ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()]
+        _lib.check(_lib.lib().tsg_queue_stats(self._q, *[ctypes.byref(x) for x in v]))
+        return {"calls": v[0].value, "batches": v[1].value, "files": v[2].value, "max_batch": v[3].value}
+
+    def probe(self, args_list, callers):
+        """callers threads scanning args_list file by file through the queue
+        (tsg_queue_probe); returns (seconds, findings)."""
+        data, offsets = pack(args_list)
+        paths, lens, _keep = _lib.pack_paths([a.FilePath for a in args_list])
+        sec, nf = ctypes.c_double(), ctypes.c_uint64()
+        _lib.check(_lib.lib().tsg_queue_probe(self._q, data.ctypes.data, offsets.ctypes.data, len(args_list), paths,
+                                              lens, callers, ctypes.byref(sec), ctypes.byref(nf)))
+        return sec.value, nf.value
+
+    def close(self):
+        if self._q:
+            _lib.lib().tsg_queue_destroy(self._q)
+            self._q = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ---------------------------------------------------------------- test hooks
 def scan_host_reference(scanner, args_list, threads=1):
     """The C++ confirmer on every (file, rule) pair, no prefilter (tests only)."""
