@@ -493,6 +493,14 @@ def launch_ranks(n, argv, dry=False):
     return rc
 
 
+def k1_build():
+    """Build hash of the scan kernels' source (trivy_amd/csrc/engine.hip): a
+    committed traffic measurement applies only to the build it was taken on."""
+    import hashlib
+    with open(os.path.join(ROOT, "trivy_amd", "csrc", "engine.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def gather_ranks(dist, world, mine):
     """Every rank's record on every rank (gloo all_gather_object), rank order."""
     if not dist:
@@ -749,17 +757,19 @@ def main():
             stats[-1]["hits"], stats[-1]["candidates"], findings, len(rules_hit)))
 
     # HBM traffic of K1 (PMC FETCH_SIZE + WRITE_SIZE, corrected as the microarch
-    # guide prescribes) from a rocprofv3 run of this same layout, if committed
+    # guide prescribes) from a rocprofv3 run of this same layout AND this same
+    # K1 build (profiles/traffic_c<config>.json carries the build hash of
+    # engine.hip it was measured on; a file from another build is refused)
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "traffic_c%d.json" % args.config)
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
         lay = tj.get("layout", {})
-        if (lay.get("config") == args.config and lay.get("segment_bytes") == _segment_bytes()
-                and lay.get("chunk_bytes") == stats[-1]["chunk_bytes"]):
+        if (tj.get("k1_build") == k1_build() and lay.get("config") == args.config
+                and lay.get("segment_bytes") == _segment_bytes() and lay.get("chunk_bytes") == stats[-1]["chunk_bytes"]):
             traffic = round(tj["traffic_over_algorithmic"] * nbytes / segments)
-            traffic_src = "%s: %.3f HBM bytes per content byte, K1 dispatches of this layout (%s)" % (
-                os.path.relpath(tpath, ROOT), tj["traffic_over_algorithmic"], tj.get("source", ""))
+            traffic_src = "%s: %.3f HBM bytes per content byte, K1 dispatches of this layout and build %s (%s)" % (
+                os.path.relpath(tpath, ROOT), tj["traffic_over_algorithmic"], tj["k1_build"], tj.get("source", ""))
 
     workload = {
         1: "config1: %.0f GB synthetic source tree (log-normal sizes, median 16 KB), builtin rules" % gb,
@@ -802,6 +812,7 @@ def main():
         "roofline": {
             "bound": "hbm",
             "kernel": "tsg_k1_scan",
+            "k1_build": k1_build(),
             "achieved": round(k1_gbps, 2),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",

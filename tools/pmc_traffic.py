@@ -8,7 +8,8 @@ chunks, 64-byte lines of temporal 16-byte loads, as K1 v3 reads):
 WRITE_SIZE is reported as read (exact for streaming stores per the guide;
 K1's writes are keyword bits, hit records and per-chunk counts).
 
-  python tools/pmc_traffic.py gpurun_out/<run> > profiles/<round>_traffic.json
+  python tools/pmc_traffic.py gpurun_out/<run> > profiles/traffic_c<config>.json
+(bench.py uses it only while engine.hip's build hash equals its k1_build)
 """
 import collections
 import csv
@@ -53,6 +54,7 @@ def main():
             bench = json.loads(line)
     out = {
         "kernel": "tsg_k1_scan",
+        "k1_build": bench["roofline"].get("k1_build") if bench else None,
         "layout": {"config": bench["config"].get("config_id") if bench else None,
                    "segment_bytes": bench["config"].get("segment_bytes") if bench else None,
                    "chunk_bytes": bench["breakdown_ms"].get("chunk_bytes") if bench else None},
