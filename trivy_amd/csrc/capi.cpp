@@ -534,12 +534,22 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
   if (prof) { g_scan_prof_on.store(true, std::memory_order_relaxed); for (auto& a : g_scan_prof) a.store(0); }
   uint64_t conf_ns = 0;
   for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += data[x] == '\n';
+  bool any_full = false;
+  for (size_t k = 0; k < rs->rs->rules.size(); ++k) any_full |= pf.rules[k].mode == 1;
   for (uint32_t f = 0; f < nfiles; ++f) {
     const uint8_t* c = data + offsets[f];
     const size_t len = offsets[f + 1] - offsets[f];
     std::vector<uint8_t> gate;
     const bool special = prefilter_reference_file(pf, c, len, &r->cands[f], &gate);
     if (special) prefilter_variant_file(pf, c, len, &r->cands[f], &gate);
+    if (!special && !any_full && std::all_of(r->cands[f].begin(), r->cands[f].end(),
+                                             [](const std::vector<uint64_t>& v) { return v.empty(); })) {
+      // as the engine's confirmer: no candidate, no host-evaluated rule -> only
+      // the global allow-path outcome (scanner.go:381-386)
+      const std::string p = path_of(paths, path_lens, f);
+      if (global_allow_path(*rs->rs, p)) r->files[f].file_path = p;
+      continue;
+    }
     std::vector<std::vector<uint64_t>> tmp = r->cands[f];
     FilePlan plan;
     plan_from_candidates(pf, &tmp, &plan);
