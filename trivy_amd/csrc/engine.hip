@@ -786,9 +786,14 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             for (int i = 0; i < kW; ++i) cur[i] = nxt[i];
           }
         } else {
-          // a line with a file boundary or the chunk end (rare): word by word
+          // a line with a file boundary or the range end (rare): word by
+          // word -- the words wholly inside the current file take the fast
+          // word step, only the word holding the boundary the byte loop
+          // (small files: a boundary every ~21 KB made every wave with one
+          // such lane run four byte loops per line)
           have = false;
           if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);     // parked outputs belong to file t.f
+#pragma unroll 1
           for (int i = 0; i < kW && t.p < k1_end(x, t); ++i) {
             if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
               if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
@@ -798,7 +803,15 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            k1_word_slow<kC>(x, t, w, S);
+            if ((kAbl & kAblDefer) && t.p + 16 <= t.lim) {
+              if (x.primary && ((v.x | v.y | v.z | v.w) & 0x80808080u) && t.p >= t.emit)
+                k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
+              if constexpr (kC) k1_word_c(x, t, ob, smem, v.x, v.y, v.z, v.w);
+              else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, v.x, v.y, v.z, v.w);
+            } else {
+              if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);   // before the word that may change the file
+              k1_word_slow<kC>(x, t, w, S);
+            }
           }
         }
       }
