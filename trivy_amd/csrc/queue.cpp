@@ -104,6 +104,7 @@ bool ScanQueue::scan(const char* path, size_t path_len, const uint8_t* content, 
   Req r{path, path_len, content, len, binary, Secret(), std::string()};
   std::unique_lock<std::mutex> lk(mu_);
   ++callers_;
+  peak_callers_ = std::max(peak_callers_, callers_);
   ++st_.calls;
   pending_.push_back(&r);
   pending_bytes_ += len;
@@ -116,9 +117,12 @@ bool ScanQueue::scan(const char* path, size_t path_len, const uint8_t* content, 
       // joined, the batch is full, or max_wait has passed
       forming_ = true;
       const auto deadline = Clock::now() + std::chrono::microseconds(max_wait_us_);
+      // every caller not busy in a running batch: the most callers ever seen
+      // at once (the --parallel goroutines come back one by one after their
+      // previous batch, so the callers inside scan() right now undercount)
       cv_.wait_until(lk, deadline, [&] {
         return pending_.size() >= max_files_ || pending_bytes_ >= max_bytes_ ||
-               pending_.size() >= callers_ - in_batches_;
+               pending_.size() + in_batches_ >= peak_callers_;
       });
       std::vector<Req*> batch;
       uint64_t bytes = 0;

@@ -3,9 +3,10 @@
 // --parallel goroutines (analyzer.go:434-451, default 5, pkg/flag/
 // scan_flags.go:85).  Concurrent scan() calls are gathered into one engine
 // batch: the first caller that finds no batch forming leads one, waits until
-// every caller that is not already inside a running batch has joined (or the
-// batch is full, or max_wait has passed), packs the contents into a pinned
-// staging buffer and scans them; the others sleep until their result is set.
+// as many callers as were ever seen at once (less those inside a running
+// batch) have joined -- or the batch is full, or max_wait has passed -- packs
+// the contents into a pinned staging buffer and scans them; the others sleep
+// until their result is set.
 // Several batches may run at once (the engine is reentrant).
 #pragma once
 #include <condition_variable>
@@ -57,6 +58,7 @@ class ScanQueue {
   std::vector<Req*> pending_;
   uint64_t pending_bytes_ = 0;
   uint32_t callers_ = 0;       // callers inside scan()
+  uint32_t peak_callers_ = 0;  // the most callers seen inside scan() at once
   uint32_t in_batches_ = 0;    // of them, in a running batch
   uint32_t inflight_ = 0;      // running batches
   bool forming_ = false;       // a leader is gathering a batch
