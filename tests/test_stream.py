@@ -212,7 +212,7 @@ def test_layer_stream_gpu_equals_oracle_concurrent():
     tars = [_make_layer(100 + i, fmt) for i, fmt in enumerate((tarfile.USTAR_FORMAT, tarfile.GNU_FORMAT,
                                                                tarfile.PAX_FORMAT))]
     with ThreadPoolExecutor(3) as ex:
-        outs = list(ex.map(lambda t: S.ScanLayerStream(sc, _Chunky(t, 5000), batch_bytes=16384), tars))
+        outs = list(ex.map(lambda t: S.ScanLayerStream(sc, _Chunky(t, 5000), batch_bytes=4096), tars))
     ref = so.Scanner(None)
     for t, (got, walk) in zip(tars, outs):
         files, _o, _w = wo.walk(t, (), ())
