@@ -480,6 +480,9 @@ constexpr int kAblPtrAddr = 1024;
 // issued together when the line starts (a 128-byte line is then fetched in one
 // burst instead of two halves microseconds apart)
 constexpr int kAblSingle = 2048;
+// measurement only (results valid): boundary lines word by word through the
+// byte loop, as before round 4 (no fast words inside them)
+constexpr int kAblNoBoundaryWords = 4096;
 // Deferred outputs (kAblDefer): a lane parks each output position of its
 // fast lines as (offset from the chunk start << 16 | state) in its own slots
 // of a global buffer (L2-resident) and handles them when its file or chunk
@@ -803,7 +806,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            if ((kAbl & kAblDefer) && t.p + 16 <= t.lim) {
+            if ((kAbl & kAblDefer) && !(kAbl & kAblNoBoundaryWords) && t.p + 16 <= t.lim) {
               if (x.primary && ((v.x | v.y | v.z | v.w) & 0x80808080u) && t.p >= t.emit)
                 k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
               if constexpr (kC) k1_word_c(x, t, ob, smem, v.x, v.y, v.z, v.w);
@@ -866,7 +869,7 @@ const void* k1_kernel(int abl, bool compressed) {
     TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(32) TSG_K1_V3(48)
     TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448)
     TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
-    TSG_K1_V3(2448) TSG_K1_V3(2512)
+    TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4560)
 #endif
 #undef TSG_K1_V3
     default: return nullptr;
