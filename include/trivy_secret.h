@@ -217,8 +217,11 @@ int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, ui
                       uint32_t* nstates, uint32_t* nclasses, uint32_t* first_out);
 /* Test hook for the host regexp engine: compiles `pattern` (Go syntax) and,
  * for each of the n positions, writes the end of the leftmost-first match
- * anchored there (-1: none) as computed by the lazy DFA (dfa_end) and by the
- * Pike VM (vm_end).  Never used by tsg_scan_batch. */
+ * anchored there (-1: none) as computed by the lazy DFA (dfa_end) and by
+ * match_at's anchored path (vm_end: the bit-state backtracker where Go would
+ * use it, else the Pike VM); fails with TSG_ERR_INTERNAL if the scanner's own
+ * match_end (span shape / backtracker / lazy DFA) differs from vm_end.  Never
+ * used by tsg_scan_batch. */
 int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
                     int64_t* dfa_end, int64_t* vm_end);
 /* Test hook for the Go sort.Slice restatement (gosort.h, pdqsort_func of

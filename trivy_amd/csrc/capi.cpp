@@ -680,8 +680,10 @@ int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const 
   std::vector<re::Cap> caps(2 * (rx->num_subexp() + 1));
   for (size_t i = 0; i < n; ++i) {
     if (pos[i] > len) return fail(TSG_ERR_INVALID, "position out of range");
-    dfa_end[i] = rx->match_end(text, len, pos[i]);
+    dfa_end[i] = rx->match_end_dfa(text, len, pos[i]);
     vm_end[i] = rx->match_at(text, len, pos[i], true, 0, caps.data()) ? caps[1] : -1;
+    // the product's dispatch (span shape / backtracker / lazy DFA) must agree
+    if (rx->match_end(text, len, pos[i]) != vm_end[i]) return fail(TSG_ERR_INTERNAL, "match_end differs from the VM");
   }
   return TSG_OK;
   TSG_API_CATCH

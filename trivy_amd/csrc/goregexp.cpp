@@ -1464,6 +1464,23 @@ bool Regexp::match_at(const uint8_t* text, size_t len, size_t pos, bool anchored
 
 long Regexp::match_end(const uint8_t* text, size_t len, size_t pos) const {
   if (prog_.start == 0) return -1;
+  // Bounded-width patterns take Go's bit-state backtracker (match_at's): a
+  // per-thread lazy DFA builds its states and transitions over the first
+  // hundreds of calls of each regexp (config 5: 7.7 us per call against ~1 us
+  // backtracking), which a batch's few candidates per rule and thread never
+  // amortise.  TSG_RE_MATCH_END_DFA=1 keeps the lazy DFA (A/B runs).
+  static const bool dfa_only = std::getenv("TSG_RE_MATCH_END_DFA") && std::atoi(std::getenv("TSG_RE_MATCH_END_DFA")) != 0;
+  if (!span_shape_ && !dfa_only && max_width_ >= 0 && pos <= len &&
+      prog_.inst.size() * (std::min<size_t>(static_cast<size_t>(max_width_), len - pos) + 1) <= 256 * 1024) {
+    thread_local std::vector<Cap> bcaps;
+    bcaps.resize(2 * (prog_.num_cap + 1));
+    return match_at(text, len, pos, true, 0, bcaps.data()) ? bcaps[1] : -1;
+  }
+  return match_end_dfa(text, len, pos);
+}
+
+long Regexp::match_end_dfa(const uint8_t* text, size_t len, size_t pos) const {
+  if (prog_.start == 0) return -1;
   if (span_shape_) {
     // L1 X* L2: X* takes any run of runes, and L2 (ASCII) starts on a rune
     // boundary wherever it occurs, so the match ends after the last (greedy)

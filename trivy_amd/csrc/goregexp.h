@@ -131,6 +131,9 @@ class Regexp {
   // End offset of the leftmost-first match anchored at `pos` (-1: none),
   // from a lazily built DFA (no captures); equals match_at(.., true, ..)'s caps[1].
   long match_end(const uint8_t* text, size_t len, size_t pos) const;
+  // match_end's lazy-DFA path alone (bounded-width patterns otherwise take
+  // the backtracker): the same result, for tests
+  long match_end_dfa(const uint8_t* text, size_t len, size_t pos) const;
   // Regexp.MatchString (with a gate set: false without running the VM when
   // no gate literal occurs in the text -- no match can exist then)
   bool match_string(const uint8_t* text, size_t len) const;
