@@ -480,9 +480,11 @@ constexpr int kAblPtrAddr = 1024;
 // issued together when the line starts (a 128-byte line is then fetched in one
 // burst instead of two halves microseconds apart)
 constexpr int kAblSingle = 2048;
-// measurement only (results valid): boundary lines word by word through the
-// byte loop, as before round 4 (no fast words inside them)
-constexpr int kAblNoBoundaryWords = 4096;
+// layout bits (results valid) for lines holding a file boundary: the words
+// wholly inside the current file take the fast word step (only the word with
+// the boundary runs the byte loop); and reloading such a line's words one by
+// one from memory, dropping the register prefetch (rounds 1-3)
+constexpr int kAblBoundaryFastWords = 4096, kAblBoundaryReload = 8192;
 // Deferred outputs (kAblDefer): a lane parks each output position of its
 // fast lines as (offset from the chunk start << 16 | state) in its own slots
 // of a global buffer (L2-resident) and handles them when its file or chunk
@@ -753,35 +755,70 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
           ++t.ci;
           t.cend = min(t.cend + chunk, t.end);
         }
-        if (t.p + kL <= t.lim) {
+        // a whole line inside the lane's range is loaded (and the next one
+        // prefetched) whatever file boundaries it holds; lines wholly inside
+        // the current file take the fast word steps
+        const bool reload = (kAbl & kAblBoundaryReload) != 0;
+        const bool in_file = t.p + kL <= t.lim;
+        if (reload ? in_file : t.p + kL <= k1_end(x, t)) {
           if (!have) {
 #pragma unroll
             for (int i = 0; i < kW; ++i) cur[i] = k1_load<kAbl>(data, t.p + 16 * i);
           }
-          have = !(kAbl & kAblSingle) && t.p + 2 * kL <= t.lim;
+          have = !(kAbl & kAblSingle) && t.p + 2 * kL <= (reload ? t.lim : k1_end(x, t));
           if (have) {
 #pragma unroll
             for (int i = 0; i < kW; ++i) nxt[i] = k1_load<kAbl>(data, t.p + kL + 16 * i);
           }
-          if (!(kAbl & (kAblNoSpecial | kAblLoadOnly)) && x.primary) {
-            uint32_t hb = 0;
+          if (in_file) {
+            if (!(kAbl & (kAblNoSpecial | kAblLoadOnly)) && x.primary) {
+              uint32_t hb = 0;
 #pragma unroll
-            for (int i = 0; i < kW; ++i) hb |= cur[i].x | cur[i].y | cur[i].z | cur[i].w;
-            if ((hb & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
-          }
-          if (kAbl & kAblRolled) {
-            // one copy of the word body: the uniform word index selects
-            // cur[i] by register indexing
+              for (int i = 0; i < kW; ++i) hb |= cur[i].x | cur[i].y | cur[i].z | cur[i].w;
+              if ((hb & 0x80808080u) && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
+            }
+            if (kAbl & kAblRolled) {
+              // one copy of the word body: the uniform word index selects
+              // cur[i] by register indexing
 #pragma unroll 1
-            for (int i = 0; i < kW; ++i) {
-              if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
-              else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+              for (int i = 0; i < kW; ++i) {
+                if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+                else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < kW; ++i) {
+                if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+                else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+              }
             }
           } else {
+            // a line holding a file boundary: its words (already in
+            // registers) through the byte loop, which switches files; parked
+            // outputs belong to file t.f, so they are handled first.  A
+            // boundary every ~21 KB (image layers) used to reload the line's
+            // words one by one and restart the prefetch: four exposed memory
+            // latencies per boundary for the whole wave.
+            if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
 #pragma unroll
             for (int i = 0; i < kW; ++i) {
-              if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
-              else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+              if (t.p >= k1_end(x, t)) break;
+              if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
+                if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
+                t.nl = 0;
+                ++t.ci;
+                t.cend = min(t.cend + chunk, t.end);
+              }
+              const uint32_t w[4] = {cur[i].x, cur[i].y, cur[i].z, cur[i].w};
+              if ((kAbl & kAblDefer) && (kAbl & kAblBoundaryFastWords) && t.p + 16 <= t.lim) {
+                if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit)
+                  k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
+                if constexpr (kC) k1_word_c(x, t, ob, smem, w[0], w[1], w[2], w[3]);
+                else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, w[0], w[1], w[2], w[3]);
+              } else {
+                if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
+                k1_word_slow<kC>(x, t, w, S);
+              }
             }
           }
           if (have) {
@@ -789,11 +826,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             for (int i = 0; i < kW; ++i) cur[i] = nxt[i];
           }
         } else {
-          // a line with a file boundary or the range end (rare): word by
-          // word -- the words wholly inside the current file take the fast
-          // word step, only the word holding the boundary the byte loop
-          // (small files: a boundary every ~21 KB made every wave with one
-          // such lane run four byte loops per line)
+          // the range's last, partial line (or, with kAblBoundaryReload, any
+          // line holding a file boundary): word by word from memory
           have = false;
           if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);     // parked outputs belong to file t.f
 #pragma unroll 1
@@ -806,7 +840,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            if ((kAbl & kAblDefer) && !(kAbl & kAblNoBoundaryWords) && t.p + 16 <= t.lim) {
+            if ((kAbl & kAblDefer) && (kAbl & kAblBoundaryFastWords) && t.p + 16 <= t.lim) {
               if (x.primary && ((v.x | v.y | v.z | v.w) & 0x80808080u) && t.p >= t.emit)
                 k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
               if constexpr (kC) k1_word_c(x, t, ob, smem, v.x, v.y, v.z, v.w);
@@ -869,7 +903,7 @@ const void* k1_kernel(int abl, bool compressed) {
     TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(32) TSG_K1_V3(48)
     TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448)
     TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
-    TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4560)
+    TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4560) TSG_K1_V3(8656) TSG_K1_V3(12752)
 #endif
 #undef TSG_K1_V3
     default: return nullptr;

@@ -672,7 +672,7 @@ StrRef put(std::string* arena, const std::string& v) {
 }
 
 // scanner.go:475-558 on the (virtual) censored buffer; appends to `out`.
-void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlines, Secret* out) {
+void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, Secret* out) {
   FindingRec f;
   f.rule = &rule;
   const size_t n = cv.size();
@@ -689,8 +689,10 @@ void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlin
   f.match = cv.put(&out->arena, line_start, line_end);
   const size_t end_line = start_line + cv.count_nl(start, end);
   const size_t code_start = start_line >= 2 ? start_line - 2 : 0;
-  const size_t code_end = std::min<size_t>(end_line + 2, nlines);
-  // bounds of lines code_start .. code_end-1 (bytes.Split of the censored buffer)
+  // lines code_start .. min(end_line + 2, len(lines)) - 1 of bytes.Split of
+  // the censored buffer: walking forward, a line ending at n (no '\n' after
+  // it) is the last one
+  size_t code_end = end_line + 2;
   std::pair<size_t, size_t> lines[8];
   size_t nl = 0;
   {
@@ -707,11 +709,13 @@ void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, uint64_t nlin
     while (nb > 0) lines[nl++] = before[--nb];
     size_t e = line0_e;
     lines[nl++] = {line0_b, line0_e};
-    for (size_t k = start_line + 1; k < code_end && nl < 8; ++k) {
+    size_t k = start_line + 1;
+    for (; k < code_end && nl < 8 && e < n; ++k) {
       const size_t bb = e + 1;
-      e = bb <= n ? cv.next_nl(bb) : n;
+      e = cv.next_nl(bb);
       lines[nl++] = {bb, e};
     }
+    code_end = k;
   }
   f.line_begin = static_cast<uint32_t>(out->lines.size());
   bool found_first = false;
@@ -893,11 +897,11 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
   std::vector<Loc> spans;
   for (const auto& m : matched) spans.push_back(m.loc);
   CensoredView cv(content, len, std::move(spans), nl);
-  const uint64_t nlines = cv.count_nl(0, len) + 1;
   out.findings.reserve(matched.size());
-  out.lines.reserve(matched.size() * 4);
+  out.lines.reserve(matched.size() * 5);
+  out.arena.reserve(matched.size() * 640);        // match line + up to 5 code lines of <= 100 bytes
   for (const auto& m : matched) {
-    to_finding(*m.rule, m.loc, cv, nlines, &out);
+    to_finding(*m.rule, m.loc, cv, &out);
     if (binary) {                                     // scanner.go:440-444
       FindingRec& f = out.findings.back();
       out.lines.resize(f.line_begin);
