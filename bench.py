@@ -494,11 +494,14 @@ def launch_ranks(n, argv, dry=False):
 
 
 def k1_build():
-    """Build hash of the scan kernels' source (trivy_amd/csrc/engine.hip): a
-    committed traffic measurement applies only to the build it was taken on."""
+    """Build hash of the scan kernels' source (the device part of
+    trivy_amd/csrc/engine.hip, up to its "==== host side" line): a committed
+    traffic measurement applies only to the kernel build it was taken on."""
     import hashlib
     with open(os.path.join(ROOT, "trivy_amd", "csrc", "engine.hip"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+        src = f.read()
+    cut = src.find(b"\n// ==== host side")
+    return hashlib.sha256(src[:cut] if cut >= 0 else src).hexdigest()[:16]
 
 
 def gather_ranks(dist, world, mine):

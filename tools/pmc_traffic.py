@@ -9,7 +9,7 @@ WRITE_SIZE is reported as read (exact for streaming stores per the guide;
 K1's writes are keyword bits, hit records and per-chunk counts).
 
   python tools/pmc_traffic.py gpurun_out/<run> > profiles/traffic_c<config>.json
-(bench.py uses it only while engine.hip's build hash equals its k1_build)
+(bench.py uses it only while the kernels' build hash -- engine.hip up to its "==== host side" line -- equals its k1_build)
 """
 import collections
 import csv
@@ -30,8 +30,8 @@ def per_kernel(root, counter):
             if m:
                 vals[(m.group(1), r["Dispatch_Id"])].append(float(r["Counter_Value"]))
     out = collections.defaultdict(list)
-    for (k, _), v in vals.items():
-        out[k].append(sum(v))          # sum over XCD/instance rows of one dispatch
+    for (k, d), v in sorted(vals.items(), key=lambda kv: int(kv[0][1])):
+        out[k].append(sum(v))          # sum over XCD/instance rows of one dispatch, in dispatch order
     return out
 
 
@@ -61,16 +61,20 @@ def main():
         "source": run,
         "bytes_per_launch": bench["roofline"]["bytes_per_launch"] if bench else None,
         "workload": bench["config"]["workload"] if bench else None,
-        "k1_fetch_size_kb_per_launch": sorted(k1["tsg_k1_scan"]),
-        "k1_write_size_kb_per_launch": sorted(k1w.get("tsg_k1_scan", [])),
-        "k2_fetch_size_kb_per_launch": sorted(k1.get("tsg_k2_verify", [])),
+        "k1_fetch_size_kb_per_launch": k1["tsg_k1_scan"],
+        "k1_write_size_kb_per_launch": k1w.get("tsg_k1_scan", []),
+        "k2_fetch_size_kb_per_launch": k1.get("tsg_k2_verify", []),
         "calib_k1v3": {"bytes": calib_bytes, "fetch_size_kb": cal, "scale": scale},
         "calib_coalesced_fetch_size_kb": coal,
     }
-    # mean over the K1 launches (a pipelined step launches K1 once per piece,
-    # pieces of unequal size; bytes_per_launch is the mean too)
-    kf = k1["tsg_k1_scan"]
-    kw = k1w.get("tsg_k1_scan", [0.0])
+    # the timed step's launches only: with --steps 1 --warmup 0 they are the
+    # process's first launches_per_step K1 dispatches (the resident leg, the
+    # parity sample and the other legs come after it with other sizes); the
+    # step's bytes are bytes_per_launch x launches_per_step
+    n = bench["roofline"]["launches_per_step"] if bench else len(k1["tsg_k1_scan"])
+    kf = k1["tsg_k1_scan"][:n]
+    kw = (k1w.get("tsg_k1_scan") or [0.0] * n)[:n]
+    out["step_launches"] = n
     f = sum(kf) / len(kf) * 1024.0 * scale
     w = sum(kw) / len(kw) * 1024.0
     out["traffic_bytes_per_launch"] = f + w

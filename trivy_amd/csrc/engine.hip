@@ -929,6 +929,9 @@ const void* k1_kernel(int abl, bool compressed) {
   }
 }
 
+// ==== host side: everything above this line is the kernels' build hash
+// (bench.py k1_build: a committed traffic measurement applies to that code)
+
 template <typename T>
 bool dev_upload(const std::vector<T>& v, T** out, std::string* err) {
   size_t n = std::max<size_t>(v.size(), 1) * sizeof(T);
