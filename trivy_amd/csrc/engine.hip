@@ -1087,6 +1087,14 @@ struct Engine::Segment {
   std::vector<uint64_t> off;
   uint32_t f0 = 0;
   uint64_t b0 = 0, bytes = 0;
+  // resident pieces: file 0 of `in` is a lead of the bytes between the
+  // 256-byte boundary below the piece's first file and that file (the tail of
+  // the previous piece), so K1's lines are aligned as on the pinned path; its
+  // results are dropped.  lead_* hold the shifted path / length / binary arrays.
+  uint32_t lead = 0;
+  std::vector<const char*> lead_paths;
+  std::vector<uint32_t> lead_lens;
+  std::vector<uint8_t> lead_bin;
 };
 
 DeviceTables::~DeviceTables() {
@@ -1839,7 +1847,8 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
   // in blocks after them (image layers: hundreds of thousands of such files)
   std::vector<uint32_t> work, light;
   work.reserve(in.nfiles / 4 + 16);
-  for (uint32_t f = 0; f < in.nfiles; ++f) {
+  results -= sg.lead;                      // results[f] for the piece's files f >= lead
+  for (uint32_t f = sg.lead; f < in.nfiles; ++f) {
     if (any_full || g.ff[f] || per_file[f] != per_file[f + 1]) work.push_back(f);
     else light.push_back(f);
   }
@@ -2004,8 +2013,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
         // piece 0 takes first_piece_ of the bytes, the others share the rest
         const double share = first_piece_ + (1.0 - first_piece_) * (p - 1) / (want - 1);
         const uint64_t target = static_cast<uint64_t>(share * static_cast<double>(total));
-        uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
-        while (f < in.nfiles && (in.offsets[f] & 15) != 0) ++f;   // resident data: aligned piece starts
+        const uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
         if (f > cut.back() && f < in.nfiles) cut.push_back(f);
       }
     } else {
@@ -2069,6 +2077,34 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       q.paths = in.paths ? in.paths + a : nullptr;
       q.path_lens = in.path_lens ? in.path_lens + a : nullptr;
       q.binary = in.binary ? in.binary + a : nullptr;
+      // a resident piece after the first starts at an arbitrary file offset:
+      // K1 reads 64-byte lines from the piece's base, and a base off the
+      // 128-byte L2 line grid made it fetch 2.4 HBM bytes per content byte
+      // (aligned pieces 1.5, profiles/rd4k traffic runs).  Start it at the
+      // 256-byte boundary below, the bytes in between a lead file.
+      const uint64_t delta = resident && p > 0 ? (reinterpret_cast<uintptr_t>(in.d_data) + sg.b0) & 255u : 0;
+      if (delta && in.h_data && in.paths) {
+        sg.lead = 1;
+        sg.off.insert(sg.off.begin(), 0);
+        for (size_t k = 1; k < sg.off.size(); ++k) sg.off[k] += delta;
+        q.offsets = sg.off.data();
+        q.nfiles = b - a + 1;
+        q.h_data -= delta;
+        q.d_data = static_cast<const uint8_t*>(q.d_data) - delta;
+        sg.lead_paths.assign(1, "");
+        sg.lead_paths.insert(sg.lead_paths.end(), in.paths + a, in.paths + b);
+        q.paths = sg.lead_paths.data();
+        if (in.path_lens) {
+          sg.lead_lens.assign(1, 0);
+          sg.lead_lens.insert(sg.lead_lens.end(), in.path_lens + a, in.path_lens + b);
+          q.path_lens = sg.lead_lens.data();
+        }
+        if (in.binary) {
+          sg.lead_bin.assign(1, 0);
+          sg.lead_bin.insert(sg.lead_bin.end(), in.binary + a, in.binary + b);
+          q.binary = sg.lead_bin.data();
+        }
+      }
     }
   }
   uint64_t max_seg = 0;
