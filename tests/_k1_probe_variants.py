@@ -15,8 +15,12 @@ from workload import synth  # noqa: E402
 
 def main():
     assert os.environ.get("TSG_LIB") == "libtrivysecret_probe.so"
+    # large files plus ~21 KB files (a file boundary in most K1 lines' ranges:
+    # the boundary-line builds) with non-ASCII text (the fold-special check)
     c = synth.generate(24_000_000, seed=31, sizes="loguniform", plant_rate=3e-3)
+    d = synth.generate(8_000_000, seed=32, sizes="small", layout="image", plant_rate=3e-3)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    args += [S.ScanArgs(d.paths[i], d.file(i)) for i in range(len(d.paths))]
     want = S.scan_host_reference(S.Scanner(None), args, threads=16)
     assert sum(len(w["Findings"]) for w in want) > 20
     for v in sys.argv[1].split(","):
