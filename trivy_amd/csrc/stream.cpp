@@ -99,7 +99,9 @@ class Pipeline {
     fo_ = o.feed;
     fo_.assume_required = true;                 // the producer gates each file before reading it
     limit_ = std::max<uint64_t>(o.batch_bytes, 1);
-    raw_cap_ = std::min<uint64_t>(limit_, 64ull << 20);      // grown as batches fill (up to the limit, or a larger file)
+    // the whole batch limit at once: its pages are only backed as a batch
+    // fills (no growth copies); a file larger than a batch grows it
+    raw_cap_ = limit_;
     raw_.reset(new uint8_t[raw_cap_]);
     consumer_ = std::thread([this] { consume(); });
   }
@@ -245,16 +247,43 @@ class Pipeline {
 };
 
 // a layer from a reader callback
+// The reader callback behind a buffer: the walk asks for a 512-byte header,
+// a file's data and its padding per entry, and one callback per request cost
+// more than the walk itself on layers of small files (a ctypes / cgo call
+// each: 2.4 GB/s end to end against 10.5 GB/s for the in-memory walk,
+// profiles/rd4l_bench_c3.json).  Requests of at least a buffer go straight to
+// the caller's memory.  A read error is reported once the bytes read before
+// it have been consumed, where the unbuffered walk would have met it.
 class ReaderTarInput : public TarInput {
  public:
-  ReaderTarInput(StreamReadFn fn, void* user) : fn_(fn), user_(user) {}
+  static constexpr size_t kBuf = 4u << 20;
+  ReaderTarInput(StreamReadFn fn, void* user) : fn_(fn), user_(user), buf_(kBuf) {}
   bool read(uint8_t* dst, size_t n, size_t* got, std::string* err) override {
     *got = 0;
-    if (n == 0 || eof_) return true;
-    const int64_t r = fn_(user_, dst, n);
-    if (r < 0) { *err = "failed to extract the archive: read error"; return false; }
-    if (r == 0) { eof_ = true; return true; }
-    *got = static_cast<size_t>(std::min<int64_t>(r, static_cast<int64_t>(n)));
+    while (*got < n) {
+      if (bpos_ < blen_) {
+        const size_t take = std::min(n - *got, blen_ - bpos_);
+        std::memcpy(dst + *got, buf_.data() + bpos_, take);
+        bpos_ += take;
+        *got += take;
+        continue;
+      }
+      if (failed_) {
+        if (*got) break;                 // deliver what was read first
+        *err = "failed to extract the archive: read error";
+        return false;
+      }
+      if (eof_) break;
+      const bool direct = n - *got >= kBuf;
+      uint8_t* to = direct ? dst + *got : buf_.data();
+      const size_t want = direct ? n - *got : kBuf;
+      const int64_t r = fn_(user_, to, want);
+      if (r < 0) { failed_ = true; continue; }
+      if (r == 0) { eof_ = true; continue; }
+      const size_t k = static_cast<size_t>(std::min<int64_t>(r, static_cast<int64_t>(want)));
+      if (direct) *got += k;
+      else { blen_ = k; bpos_ = 0; }
+    }
     pos += *got;
     return true;
   }
@@ -262,7 +291,9 @@ class ReaderTarInput : public TarInput {
  private:
   StreamReadFn fn_;
   void* user_;
-  bool eof_ = false;
+  std::vector<uint8_t> buf_;
+  size_t bpos_ = 0, blen_ = 0;
+  bool eof_ = false, failed_ = false;
 };
 
 }  // namespace

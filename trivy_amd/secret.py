@@ -369,10 +369,20 @@ def PrepareFsTree(scanner, root, skip_files=(), skip_dirs=(), file_patterns=(), 
 
 
 def _reader(fileobj):
-    """A tsg_read_fn over a Python binary file object (io.Reader)."""
+    """A tsg_read_fn over a Python binary file object (io.Reader): readinto()
+    straight into the engine's buffer where the object has it (one copy),
+    else read() + memmove."""
+    into = [getattr(fileobj, "readinto", None)]
+
     def read(_user, buf, cap):
         try:
-            b = fileobj.read(min(cap, 1 << 22))
+            if into[0] is not None:
+                try:
+                    n = into[0](memoryview((ctypes.c_char * cap).from_address(buf)).cast("B"))
+                    return n or 0
+                except NotImplementedError:    # io.RawIOBase subclasses with read() only
+                    into[0] = None
+            b = fileobj.read(cap)
         except Exception:                      # noqa: BLE001 -- a reader error ends the walk
             return -1
         if not b:
