@@ -29,12 +29,54 @@ double ms_between(Clock::time_point a, Clock::time_point b) {
   return std::chrono::duration<double, std::milli>(b - a).count();
 }
 
+// Pinned buffers outlive one stream: hipHostMalloc of a stream's two batch
+// buffers took ~45 ms per call (profiles/rd4l_bench_c1.json, tree
+// pinned_alloc_ms), paid again by every layer of an image and every call.
+// Streams return theirs here (up to 4 GiB) and take the smallest that fits.
+// Never freed at exit (the HIP runtime may be gone by then).
+class PinnedCache {
+ public:
+  static PinnedCache& get() {
+    static PinnedCache* c = new PinnedCache();
+    return *c;
+  }
+  uint8_t* take(size_t want, size_t* cap) {
+    std::lock_guard<std::mutex> lk(mu_);
+    size_t best = free_.size();
+    for (size_t i = 0; i < free_.size(); ++i)
+      if (free_[i].second >= want && (best == free_.size() || free_[i].second < free_[best].second)) best = i;
+    if (best == free_.size()) return nullptr;
+    uint8_t* p = free_[best].first;
+    *cap = free_[best].second;
+    bytes_ -= *cap;
+    free_.erase(free_.begin() + static_cast<long>(best));
+    return p;
+  }
+  void give(uint8_t* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (bytes_ + cap <= kMax) {
+        free_.push_back({p, cap});
+        bytes_ += cap;
+        return;
+      }
+    }
+    tsg_free_pinned(p);
+  }
+
+ private:
+  static constexpr size_t kMax = 4ull << 30;
+  std::mutex mu_;
+  std::vector<std::pair<uint8_t*, size_t>> free_;
+  size_t bytes_ = 0;
+};
+
 // The prepared-batch buffers: `n` of them in circulation, grown on demand.
 class BufPool {
  public:
   BufPool(bool pinned, size_t n) : pinned_(pinned), n_(n) {}
   ~BufPool() {
-    for (auto& b : bufs_) release(b.p);
+    for (auto& b : bufs_) release(b.p, b.cap);
   }
   // a buffer of >= bytes (blocks while all are in use); nullptr if allocation failed
   uint8_t* get(size_t bytes, double* wait_ms) {
@@ -45,18 +87,16 @@ class BufPool {
     for (auto& b : bufs_) {
       if (b.used) continue;
       if (b.cap < bytes) {
-        release(b.p);
-        b.p = alloc(bytes);
-        b.cap = b.p ? bytes : 0;
+        release(b.p, b.cap);
+        b.p = alloc(bytes, &b.cap);
       }
       if (!b.p) return nullptr;
       b.used = true;
       return b.p;
     }
     B b;
-    b.p = alloc(bytes);
+    b.p = alloc(bytes, &b.cap);
     if (!b.p) return nullptr;
-    b.cap = bytes;
     b.used = true;
     bufs_.push_back(b);
     return b.p;
@@ -69,14 +109,22 @@ class BufPool {
 
  private:
   struct B { uint8_t* p = nullptr; size_t cap = 0; bool used = false; };
-  uint8_t* alloc(size_t bytes) {
-    if (!pinned_) return static_cast<uint8_t*>(std::malloc(bytes));
+  uint8_t* alloc(size_t bytes, size_t* cap) {
+    *cap = 0;
+    if (!pinned_) {
+      uint8_t* p = static_cast<uint8_t*>(std::malloc(bytes));
+      if (p) *cap = bytes;
+      return p;
+    }
+    if (uint8_t* p = PinnedCache::get().take(bytes, cap)) return p;
     void* p = nullptr;
-    return tsg_alloc_pinned(bytes, &p) == 0 ? static_cast<uint8_t*>(p) : nullptr;
+    if (tsg_alloc_pinned(bytes, &p) != 0) return nullptr;
+    *cap = bytes;
+    return static_cast<uint8_t*>(p);
   }
-  void release(uint8_t* p) {
+  void release(uint8_t* p, size_t cap) {
     if (!p) return;
-    if (pinned_) tsg_free_pinned(p);
+    if (pinned_) PinnedCache::get().give(p, cap);
     else std::free(p);
   }
   bool pinned_;
