@@ -112,7 +112,7 @@ def test_k1_probe_variants_agree_gpu():
     assert r.stdout.count("agree") == 7, r.stdout
 
 
-@pytest.mark.parametrize("abl,chunk", [("464", "2048"), ("464", "1024"), ("464", "4096")])
+@pytest.mark.parametrize("abl,chunk", [("464", "2048"), ("464", "1024"), ("464", "4096"), ("464", "256")])
 def test_k1_variants_agree_gpu(monkeypatch, abl, chunk):
     # the product K1 build over every chunk size gives the host confirmer's
     # result (the measurement builds: test_k1_probe_variants_agree_gpu)

@@ -955,8 +955,12 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // Default K1 chunk for a launch of `bytes`.  K1 walks ranges of 1-4 chunks
 // per lane (guided schedule): its chunk is the '\n'-count granularity and the
 // last round's range: 2 KiB for launches of 2 GiB and more (measured r2r:
-// 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB.
-uint32_t k1_chunk_for(uint64_t bytes) { return bytes >= (2ull << 30) ? 2048 : 1024; }
+// 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB; batches under 8 MB (per-file Scan
+// batches of a few files) 256 B, so a one-workgroup launch spreads its bytes
+// over four times the lanes (a lane walks ~12 MB/s: a 1 KiB range is ~85 us).
+uint32_t k1_chunk_for(uint64_t bytes) {
+  return bytes >= (2ull << 30) ? 2048 : bytes >= (8ull << 20) ? 1024 : 256;
+}
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
