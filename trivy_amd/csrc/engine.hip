@@ -2167,7 +2167,7 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     };
     size_t cur = ok ? next_seg.fetch_add(1) : segs.size();
     int slot = 0;
-    if (ok && host_profile_) hipEventRecord(ln->anchor, ln->copy);
+    if (ok && host_profile_) hipEventRecord(ln->anchor, resident ? ln->compute : ln->copy);
     if (ok && cur < segs.size() && !resident) ok = upload(cur, slot);
     while (ok && cur < segs.size() && !q.aborted()) {
       const size_t nxt = next_seg.fetch_add(1);
@@ -2190,11 +2190,13 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
       const double h_start = ms_since(t_feed0);
       ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e);
       if (!ok) break;
-      if (host_profile_ && !resident) {
+      if (host_profile_) {
         // GPU timeline of this segment from the scan's anchor event
         float ub = 0, ud = 0, k1a = 0, k1b = 0, k2b = 0;
-        hipEventElapsedTime(&ub, ln->anchor, ln->up_begin[slot]);
-        hipEventElapsedTime(&ud, ln->anchor, ln->up_done[slot]);
+        if (!resident) {
+          hipEventElapsedTime(&ub, ln->anchor, ln->up_begin[slot]);
+          hipEventElapsedTime(&ud, ln->anchor, ln->up_done[slot]);
+        }
         hipEventElapsedTime(&k1a, ln->anchor, ln->ev[0]);
         hipEventElapsedTime(&k1b, ln->anchor, ln->ev[1]);
         hipEventElapsedTime(&k2b, ln->anchor, ln->ev[3]);
@@ -2241,8 +2243,10 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
     if (!job) break;
     auto th = std::chrono::steady_clock::now();
     const Segment& sg = segs[job->seg];
+    const double c_start = host_profile_ ? ms_since(t_feed0) : 0.0;
     confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0);
     host_ms += ms_since(th);
+    if (host_profile_) std::fprintf(stderr, "[tsg tl] seg %zu confirm %.3f-%.3f ms\n", job->seg, c_start, ms_since(t_feed0));
   }
   for (auto& t : threads) t.join();
   release_call(cc);
