@@ -1845,6 +1845,15 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
   }
   bool any_full = false;
   for (size_t r = 0; r < nr; ++r) if (pf_.rules[r].mode == 1) any_full = true;
+  // the plan every confirmed file starts from, and its mode-1 rules
+  std::vector<uint8_t> kind0(nplan, kPlanNoMatch);
+  std::vector<uint32_t> full_rules;
+  for (size_t r = 0; r < nplan; ++r) {
+    if (pf_.rules[r].mode == 1) {            // (mode 3: only with a presence candidate)
+      kind0[r] = kPlanFull;
+      full_rules.push_back(static_cast<uint32_t>(r));
+    }
+  }
   // files to confirm (candidates, fold-special content, or host-evaluated
   // rules), largest first (LPT: the per-file confirm cost grows with size);
   // every other file only needs the global allow-path outcome and is handled
@@ -1904,12 +1913,8 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
         continue;
       }
       nconf.fetch_add(1);
-      plan.kind.assign(nplan, kPlanNoMatch);
+      plan.kind = kind0;                       // mode-1 rules kPlanFull, the rest kPlanNoMatch
       plan.cands.clear();
-      for (size_t r = 0; r < nplan; ++r) {
-        const RuleGpuInfo& gi = pf_.rules[r];
-        if (gi.mode == 1) plan.kind[r] = kPlanFull;   // (mode 3: only with a presence candidate, below)
-      }
       std::sort(sorted.begin() + cb, sorted.begin() + ce, [](const CandDev& a, const CandDev& b) {
         return a.rule != b.rule ? a.rule < b.rule : a.start < b.start;
       });
@@ -1926,6 +1931,18 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
         plan.kind[r] = pf_.rules[r].mode == 3 || rc.starts.back() == kFullScanStart ? kPlanFull
                      : pf_.rules[r].gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
         plan.cands.push_back(std::move(rc));
+      }
+      // the rules scan_file visits: mode-1 rules and those with candidates, ascending
+      plan.active.clear();
+      plan.active_set = true;
+      {
+        size_t a = 0, b = 0;
+        while (a < full_rules.size() || b < plan.cands.size()) {
+          const uint32_t x = a < full_rules.size() ? full_rules[a] : UINT32_MAX;
+          const uint32_t y = b < plan.cands.size() ? plan.cands[b].rule : UINT32_MAX;
+          if (x <= y) { plan.active.push_back(x); ++a; if (x == y) ++b; }
+          else { plan.active.push_back(y); ++b; }
+        }
       }
       NlSource nls;
       nls.chunk_nl = g.nl.data();

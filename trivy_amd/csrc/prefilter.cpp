@@ -1502,14 +1502,18 @@ void plan_from_candidates(const Prefilter& pf, std::vector<std::vector<uint64_t>
   const size_t nr = pf.rules.size();
   plan->kind.assign(nr, kPlanNoMatch);
   plan->cands.clear();
+  plan->active.clear();
+  plan->active_set = true;
   for (size_t k = 0; k < nr; ++k) {
     const RuleGpuInfo& gi = pf.rules[k];
     if (gi.mode == 1 || (gi.mode == 3 && !(*cands)[k].empty()) ||
         (gi.mode == 4 && !(*cands)[k].empty() && (*cands)[k].back() == kFullScanStart)) {
       plan->kind[k] = kPlanFull;
+      plan->active.push_back(static_cast<uint32_t>(k));
     } else if ((gi.mode == 0 || gi.mode == 4) && !(*cands)[k].empty()) {
       plan->kind[k] = gi.gate_on_gpu ? kPlanCandidates : kPlanCandHostGate;
       plan->cands.push_back({static_cast<uint32_t>(k), std::move((*cands)[k])});
+      plan->active.push_back(static_cast<uint32_t>(k));
     }
   }
 }

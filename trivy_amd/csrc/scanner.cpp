@@ -871,7 +871,11 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
   std::vector<M> matched;
   size_t cand_i = 0;
   std::vector<Loc> locs;
-  for (size_t ri = 0; ri < rs.rules.size(); ++ri) {
+  const bool listed = plan && plan->active_set;
+  const size_t niter = listed ? plan->active.size() : rs.rules.size();
+  for (size_t it = 0; it < niter; ++it) {
+    const size_t ri = listed ? plan->active[it] : it;
+    if (ri >= rs.rules.size()) break;                // exclude-regex pseudo-rules (listed last)
     const Rule& rule = rs.rules[ri];
     const uint8_t kind = plan ? plan->kind[ri] : static_cast<uint8_t>(kPlanFull);
     const std::vector<uint64_t>* starts = nullptr;

@@ -117,6 +117,11 @@ struct RuleCandidates {
 struct FilePlan {
   std::vector<uint8_t> kind;             // one PlanKind per rule, then one per exclude regex
   std::vector<RuleCandidates> cands;     // sorted by rule (exclude regexes after the rules)
+  // with active_set: every index whose kind is kPlanFull / kPlanCandidates /
+  // kPlanCandHostGate, ascending -- scan_file visits only these rules (config
+  // 5: 1-3 of 587 per file) instead of testing every rule's kind
+  std::vector<uint32_t> active;
+  bool active_set = false;
 };
 
 // Newline counts for findLocation without rescanning a file: K1's per-chunk
