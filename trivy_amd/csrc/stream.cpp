@@ -176,6 +176,28 @@ class Pipeline {
     used_ += n;
     out_->st.read_bytes += n;
   }
+  // Window mode (stream_layer): the tar reader fills raw_ itself and the
+  // kept files are committed where they lie, so file data is copied once
+  // (reader -> window) on its way to the prepared batch.
+  uint8_t* window() { return raw_.get(); }
+  uint64_t window_cap() const { return raw_cap_; }
+  bool has_files() const { return !paths_.empty(); }
+  double flush_wall_ms() const { return flush_wall_ms_; }   // wall time inside flush() so far
+  void commit_at(const std::string& path, uint64_t off, uint64_t n) {
+    starts_.push_back(off);
+    sizes_.push_back(n);
+    paths_.push_back(path);
+    used_ += n;
+    out_->st.read_bytes += n;
+  }
+  // a larger window holding the unconsumed bytes [from, to) at its start
+  // (only between batches: no file is committed)
+  void grow_window(uint64_t cap, uint64_t from, uint64_t to) {
+    std::unique_ptr<uint8_t[]> nb(new uint8_t[cap]);
+    std::memcpy(nb.get(), raw_.get() + from, to - from);
+    raw_ = std::move(nb);
+    raw_cap_ = cap;
+  }
   // prepare the current batch and hand it to the scan stage
   bool flush() {
     if (paths_.empty()) return ok();
@@ -203,6 +225,7 @@ class Pipeline {
     paths_.clear();
     used_ = 0;
     out_->st.feed_ms += ms_between(t0, Clock::now());
+    flush_wall_ms_ += ms_between(t0, Clock::now());
     {
       std::unique_lock<std::mutex> lk(mu_);
       q_.push_back(std::move(job));
@@ -285,6 +308,7 @@ class Pipeline {
   std::unique_ptr<uint8_t[]> raw_;
   uint64_t limit_ = 0, raw_cap_ = 0, used_ = 0;
   std::vector<uint64_t> starts_, sizes_;
+  double flush_wall_ms_ = 0;
   std::vector<std::string> paths_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -295,52 +319,96 @@ class Pipeline {
 };
 
 // a layer from a reader callback
-// The reader callback behind a buffer: the walk asks for a 512-byte header,
-// a file's data and its padding per entry, and one callback per request cost
-// more than the walk itself on layers of small files (a ctypes / cgo call
-// each: 2.4 GB/s end to end against 10.5 GB/s for the in-memory walk,
-// profiles/rd4l_bench_c3.json).  Requests of at least a buffer go straight to
-// the caller's memory.  A read error is reported once the bytes read before
-// it have been consumed, where the unbuffered walk would have met it.
-class ReaderTarInput : public TarInput {
+// The tar pulled from the reader callback straight into the pipeline's raw
+// batch (the window): one callback per window fill instead of one per header
+// and per file (a ctypes / cgo call each: 2.4 GB/s end to end against 10.5
+// GB/s for the in-memory walk, profiles/rd4l_bench_c3.json), and a kept
+// file's data is committed in place (`view`) instead of being copied out of a
+// read buffer.  Headers, padding and skipped files pass through the window
+// too.  The window is compacted -- its unconsumed tail moved to the start --
+// only after the files committed in it have been prepared (flush).  A read
+// error is reported once the bytes read before it have been consumed, where
+// the unbuffered walk would have met it.
+class WindowTarInput : public TarInput {
  public:
-  static constexpr size_t kBuf = 4u << 20;
-  ReaderTarInput(StreamReadFn fn, void* user) : fn_(fn), user_(user), buf_(kBuf) {}
+  WindowTarInput(StreamReadFn fn, void* user, Pipeline* pl) : fn_(fn), user_(user), pl_(pl) {}
   bool read(uint8_t* dst, size_t n, size_t* got, std::string* err) override {
     *got = 0;
     while (*got < n) {
-      if (bpos_ < blen_) {
-        const size_t take = std::min(n - *got, blen_ - bpos_);
-        std::memcpy(dst + *got, buf_.data() + bpos_, take);
-        bpos_ += take;
+      if (rpos_ < wlen_) {
+        const size_t take = std::min<size_t>(n - *got, wlen_ - rpos_);
+        std::memcpy(dst + *got, pl_->window() + rpos_, take);
+        rpos_ += take;
         *got += take;
         continue;
       }
-      if (failed_) {
-        if (*got) break;                 // deliver what was read first
-        *err = "failed to extract the archive: read error";
-        return false;
-      }
-      if (eof_) break;
-      const bool direct = n - *got >= kBuf;
-      uint8_t* to = direct ? dst + *got : buf_.data();
-      const size_t want = direct ? n - *got : kBuf;
-      const int64_t r = fn_(user_, to, want);
-      if (r < 0) { failed_ = true; continue; }
-      if (r == 0) { eof_ = true; continue; }
-      const size_t k = static_cast<size_t>(std::min<int64_t>(r, static_cast<int64_t>(want)));
-      if (direct) *got += k;
-      else { blen_ = k; bpos_ = 0; }
+      if (!fill(1, err)) return false;
+      if (rpos_ >= wlen_) break;                 // end of the data
     }
+    pos += *got;
+    return true;
+  }
+  bool skip(uint64_t n, uint64_t* got, std::string* err) override {
+    *got = 0;
+    while (*got < n) {
+      if (rpos_ < wlen_) {
+        const uint64_t take = std::min<uint64_t>(n - *got, wlen_ - rpos_);
+        rpos_ += take;
+        *got += take;
+        continue;
+      }
+      if (!fill(1, err)) return false;
+      if (rpos_ >= wlen_) break;
+    }
+    pos += *got;
+    return true;
+  }
+  // the next n bytes in place, consumed: their window offset in *off, *got < n
+  // only at the end of the data
+  bool view(uint64_t n, uint64_t* off, uint64_t* got, std::string* err) {
+    if (!fill(n, err)) return false;
+    *got = std::min<uint64_t>(n, wlen_ - rpos_);
+    *off = rpos_;
+    rpos_ += *got;
     pos += *got;
     return true;
   }
 
  private:
+  // at least `need` unconsumed bytes contiguous in the window (fewer only at
+  // the end of the data); false: a read error before them, or a failed flush
+  bool fill(uint64_t need, std::string* err) {
+    while (wlen_ - rpos_ < need && !eof_ && !failed_) {
+      if (rpos_ + need > pl_->window_cap() || wlen_ == pl_->window_cap()) {
+        // make room: prepare the files committed in the window, then move the
+        // unconsumed tail to the start (a larger window for a file larger
+        // than a batch)
+        if (pl_->has_files() && !pl_->flush()) { *err = pl_->error(); return false; }
+        const uint64_t keep = wlen_ - rpos_;
+        if (need > pl_->window_cap()) {
+          pl_->grow_window(need, rpos_, wlen_);
+        } else if (rpos_) {
+          std::memmove(pl_->window(), pl_->window() + rpos_, keep);
+        }
+        rpos_ = 0;
+        wlen_ = keep;
+      }
+      const int64_t r = fn_(user_, pl_->window() + wlen_, pl_->window_cap() - wlen_);
+      if (r < 0) failed_ = true;
+      else if (r == 0) eof_ = true;
+      else wlen_ += static_cast<uint64_t>(std::min<int64_t>(r, static_cast<int64_t>(pl_->window_cap() - wlen_)));
+    }
+    if (failed_ && wlen_ - rpos_ < need) {
+      *err = "failed to extract the archive: read error";
+      return false;
+    }
+    return true;
+  }
+
   StreamReadFn fn_;
   void* user_;
-  std::vector<uint8_t> buf_;
-  size_t bpos_ = 0, blen_ = 0;
+  Pipeline* pl_;
+  uint64_t rpos_ = 0, wlen_ = 0;
   bool eof_ = false, failed_ = false;
 };
 
@@ -350,39 +418,37 @@ bool stream_layer(const Ruleset& rs, const StreamOpts& o, StreamReadFn read, voi
                   StreamResult* out, std::string* err) {
   *out = StreamResult();
   const auto t0 = Clock::now();
-  ReaderTarInput in(read, user);
   LayerWalk walk;
   const std::string cfg_base = o.feed.config_path;
   Pipeline pl(rs, o, scan, "/", out);
+  WindowTarInput in(read, user, &pl);
   auto t_feed = Clock::now();
   // processFile (tar.go:94-105) -> AnalyzeFile's gate -> read the content
   auto on_file = [&](const std::string& path, uint64_t size, TarInput& tin, std::string* e) {
     out->walked.push_back(path);
     out->st.walked_bytes += size;
     if (!secret_analyzer_wants(rs, o.feed, path, size)) return true;     // the walker skips the data
-    uint8_t* dst = pl.reserve(size);
-    if (!dst) { *e = pl.error(); return false; }
-    size_t got = 0;
-    if (!read_full(tin, dst, static_cast<size_t>(size), &got, e)) return false;
+    (void)tin;                                                          // (tin is `in`)
+    uint64_t off = 0, got = 0;
+    if (!in.view(size, &off, &got, e)) return false;
     if (got < size) {
       *e = "failed to process the file: failed to analyze file: failed to open: unable to read the file: unexpected EOF";
       return false;
     }
-    pl.commit(path, size);
+    pl.commit_at(path, off, size);
     return true;
   };
   std::string werr;
   const bool wok = walk_layer(in, o.skip_files, o.skip_dirs, &walk, on_file, &werr);
-  out->st.feed_ms += ms_between(t_feed, Clock::now());
+  // the walk's own time: the batches it flushed (window full) count themselves
+  out->st.feed_ms += ms_between(t_feed, Clock::now()) - pl.flush_wall_ms();
   if (!wok) {
     pl.set_error(werr);
     pl.finish();
     *err = werr;
     return false;
   }
-  t_feed = Clock::now();
   pl.flush();
-  out->st.feed_ms += ms_between(t_feed, Clock::now());
   if (!pl.finish()) { *err = pl.error(); return false; }
   out->opq_dirs = std::move(walk.opq_dirs);
   out->wh_files = std::move(walk.wh_files);
