@@ -1003,6 +1003,11 @@ def main():
             "sample": "same %d files, C++ Go-regexp restatement of scanner.go on every (file, rule) pair "
                       "(tsg_scan_host_reference), %d threads, %.2f s; diff vs oracle: %d files"
                       % (len(idx), procs, cdt, cdiff),
+            "note": "the one that approximates the reference's own speed: the same algorithm as Go's scanner.go "
+                    "(per rule: keyword gate, then regexp find-all over the whole file) on Go's regexp engines "
+                    "(Pike VM; bit-state backtracker only for small inputs, as Go), compiled; cpu_baseline "
+                    "(the oracle) runs the third-party `regex` module's backtracking engine with Go-semantics "
+                    "rewrites, faster on these patterns than a Pike VM but not Go's algorithm",
         }
         if "per_file" in out:
             for k, v in out["per_file"].items():
