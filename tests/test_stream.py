@@ -254,3 +254,14 @@ def test_layer_stream_bounded_memory_gpu():
     hits = [g for g in got if g["Findings"]]
     assert len(hits) == (n + 6) // 7
     assert all(g["Findings"][0]["RuleID"] == "aws-access-key-id" for g in hits)
+
+
+def test_huge_size_field_is_unexpected_eof_not_allocation():
+    # a kept file whose (valid) PAX size claims ~9 EB: the window grows only
+    # with the bytes actually read, so the walk ends in the analyzer's
+    # "unexpected EOF" rather than an allocation of the claimed size
+    from test_layer_tar import _pax_layer
+    tar = _pax_layer(b"9223372036854775000", b"ghp_" + b"x" * 600)
+    for batch in (0, 4096):
+        with pytest.raises(S.WalkError, match="unexpected EOF"):
+            S.ScanLayerStream(S.Scanner(None), io.BytesIO(tar), batch_bytes=batch, model=True)

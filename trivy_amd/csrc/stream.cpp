@@ -381,17 +381,15 @@ class WindowTarInput : public TarInput {
     while (wlen_ - rpos_ < need && !eof_ && !failed_) {
       if (rpos_ + need > pl_->window_cap() || wlen_ == pl_->window_cap()) {
         // make room: prepare the files committed in the window, then move the
-        // unconsumed tail to the start (a larger window for a file larger
-        // than a batch)
+        // unconsumed tail to the start; a window still full holds part of a
+        // file larger than a batch: double it (by the bytes actually read, so
+        // a hostile size field ends in "unexpected EOF", not an allocation)
         if (pl_->has_files() && !pl_->flush()) { *err = pl_->error(); return false; }
         const uint64_t keep = wlen_ - rpos_;
-        if (need > pl_->window_cap()) {
-          pl_->grow_window(need, rpos_, wlen_);
-        } else if (rpos_) {
-          std::memmove(pl_->window(), pl_->window() + rpos_, keep);
-        }
+        if (rpos_) std::memmove(pl_->window(), pl_->window() + rpos_, keep);
         rpos_ = 0;
         wlen_ = keep;
+        if (wlen_ == pl_->window_cap()) pl_->grow_window(2 * pl_->window_cap(), 0, wlen_);
       }
       const int64_t r = fn_(user_, pl_->window() + wlen_, pl_->window_cap() - wlen_);
       if (r < 0) failed_ = true;
