@@ -70,7 +70,7 @@ struct tsg_prepared {
 struct tsg_result {
   std::shared_ptr<const Ruleset> rs;     // findings point at its rules
   std::shared_ptr<std::deque<Rule>> own_rules;   // or at these (tsg_result_from_json)
-  std::vector<Secret> files;
+  SecretVec files;
   ScanStats stats;
   std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
   std::vector<std::vector<LayerRef>> layers;               // optional [file][finding] (tsg_result_from_proto)
@@ -818,7 +818,7 @@ int tsg_report_json(const tsg_result* const* layers, const tsg_layer* layer_refs
                     const tsg_result* image_config, const tsg_report_opts* opts, char** out, size_t* len) {
   TSG_API_TRY
   if ((nlayers && !layers) || !out) return fail(TSG_ERR_INVALID, "NULL argument");
-  std::vector<const std::vector<Secret>*> ls;
+  std::vector<const SecretVec*> ls;
   std::vector<LayerRef> refs;
   for (uint32_t i = 0; i < nlayers; ++i) {
     if (!layers[i]) return fail(TSG_ERR_INVALID, "NULL layer result");
@@ -1143,12 +1143,13 @@ int tsg_prepare_fs_tree(const tsg_ruleset* rs, const char* root, const tsg_feed_
 namespace {
 // CPU model of the engine's scan stage for one batch (tsg_scan_table_model's
 // per-file work): tests of the stream pipelines without a GPU.
-bool model_scan_batch(const Ruleset& rs, const Prefilter& pf, const BatchInput& in, std::vector<Secret>* res) {
+bool model_scan_batch(const Ruleset& rs, const Prefilter& pf, const BatchInput& in, SecretVec* res) {
   const uint32_t ch = 2048;
   const uint64_t total = in.nfiles ? in.offsets[in.nfiles] : 0;
   std::vector<uint16_t> chunk_nl((total + ch - 1) / ch, 0);
   for (uint64_t x = 0; x < total; ++x) chunk_nl[x / ch] += in.h_data[x] == '\n';
-  res->assign(in.nfiles, Secret());
+  res->clear();
+  res->resize(in.nfiles);
   for (uint32_t f = 0; f < in.nfiles; ++f) {
     const uint8_t* c = in.h_data + in.offsets[f];
     const size_t len = in.offsets[f + 1] - in.offsets[f];
@@ -1207,14 +1208,14 @@ tsg_result* stream_result(std::shared_ptr<const Ruleset> rs, StreamResult&& sr) 
 }
 
 BatchScanFn engine_stage(tsg_engine* e) {
-  return [e](const BatchInput& in, std::vector<Secret>* res, std::string* err) {
+  return [e](const BatchInput& in, SecretVec* res, std::string* err) {
     ScanStats st;
     return e->eng->scan(in, res, &st, err);
   };
 }
 
 BatchScanFn model_stage(const Ruleset& rs, const Prefilter& pf) {
-  return [&rs, &pf](const BatchInput& in, std::vector<Secret>* res, std::string*) {
+  return [&rs, &pf](const BatchInput& in, SecretVec* res, std::string*) {
     return model_scan_batch(rs, pf, in, res);
   };
 }

@@ -55,7 +55,7 @@ class Engine {
   ~Engine();
 
   // results[i] is Scanner.Scan(ScanArgs{paths[i], data[off[i]:off[i+1]], binary[i]}).
-  bool scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* stats, std::string* err);
+  bool scan(const BatchInput& in, SecretVec* results, ScanStats* stats, std::string* err);
 
   // Only the two GPU passes (no host confirmation): used by tests to compare
   // raw candidates.  Resident data on the engine's first device.

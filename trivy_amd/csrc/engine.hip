@@ -1995,7 +1995,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
 // Every segment is a self-contained batch (offsets rebased to 0, data a
 // 16-byte aligned sub-range), so the kernels are unchanged and the result is
 // the one-segment result.
-bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats* st, std::string* err) {
+bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::string* err) {
   ScanStats local;
   if (!st) st = &local;
   *st = ScanStats();
@@ -2011,7 +2011,8 @@ bool Engine::scan(const BatchInput& in, std::vector<Secret>* results, ScanStats*
   if (in.nfiles == 0 || total == 0) {
     // nothing for the GPU: every file is empty, so only the global
     // allow-path outcome (scanner.go:381-386) can make a Secret non-empty
-    results->assign(in.nfiles, Secret());
+    results->clear();
+    results->resize(in.nfiles);
     for (uint32_t f = 0; f < in.nfiles; ++f)
       (*results)[f] = scan_file(*rs_, in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]),
                                 in.h_data, 0, in.binary ? in.binary[f] != 0 : false, nullptr);

@@ -79,7 +79,7 @@ void ScanQueue::run_batch(std::vector<Req*>& batch) {
   in.paths = paths.data();
   in.path_lens = lens.data();
   in.binary = bin.data();
-  std::vector<Secret> res;
+  SecretVec res;
   ScanStats st;
   std::string err;
   const bool ok = eng_->scan(in, &res, &st, &err);

@@ -545,7 +545,7 @@ bool guess_base_layers(const std::string& config_json, const std::vector<std::st
   return true;
 }
 
-bool report_json(const std::vector<const std::vector<Secret>*>& layers, const std::vector<LayerRef>& refs,
+bool report_json(const std::vector<const SecretVec*>& layers, const std::vector<LayerRef>& refs,
                  const Secret* image_config, const ReportOptions& opt, std::string* out, std::string* err) {
   // --- per layer: the analyzer keeps Secrets with findings (secret.go:139-141),
   // AnalysisResult.Sort orders them by FilePath and each one's findings by

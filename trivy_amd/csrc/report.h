@@ -40,7 +40,7 @@ struct ReportOptions {
 // The JSON report for the secret results of one artifact: layers[i] are the
 // secrets analysed in layer i (lowest first; an fs scan is one layer with an
 // empty LayerRef), image_config the image-config analyzer's result (or null).
-bool report_json(const std::vector<const std::vector<Secret>*>& layers, const std::vector<LayerRef>& refs,
+bool report_json(const std::vector<const SecretVec*>& layers, const std::vector<LayerRef>& refs,
                  const Secret* image_config, const ReportOptions& opt, std::string* out, std::string* err);
 
 // json.Indent(dst, compact, prefix, indent) (encoding/json/indent.go).

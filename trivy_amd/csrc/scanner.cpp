@@ -11,6 +11,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <thread>
 
 namespace tsg {
 
@@ -935,6 +936,59 @@ Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* cont
   out.file_path = path;
   pc.lap(4);
   return out;
+}
+
+}  // namespace tsg
+
+namespace tsg {
+
+void SecretVec::reserve(size_t c) {
+  if (c <= cap_) return;
+  Secret* q = static_cast<Secret*>(::operator new(c * sizeof(Secret)));
+  for (size_t i = 0; i < n_; ++i) {
+    new (q + i) Secret(std::move(p_[i]));
+    p_[i].~Secret();
+  }
+  ::operator delete(p_);
+  p_ = q;
+  cap_ = c;
+}
+
+void SecretVec::clear() {
+  for (size_t i = 0; i < n_; ++i) p_[i].~Secret();
+  n_ = 0;
+}
+
+void SecretVec::destroy() {
+  clear();
+  ::operator delete(p_);
+  p_ = nullptr;
+  cap_ = 0;
+}
+
+void SecretVec::resize(size_t n) {
+  if (n <= n_) {
+    for (size_t i = n; i < n_; ++i) p_[i].~Secret();
+    n_ = n;
+    return;
+  }
+  reserve(n);
+  const size_t add = n - n_;
+  constexpr size_t kPerThread = 32768;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = std::min<size_t>({add / kPerThread, 8, hw});
+  if (nt <= 1) {
+    for (size_t i = n_; i < n; ++i) new (p_ + i) Secret();
+  } else {
+    std::vector<std::thread> ts;
+    const size_t per = (add + nt - 1) / nt;
+    for (size_t t = 0; t < nt; ++t) {
+      const size_t a = n_ + t * per, b = std::min(n, a + per);
+      ts.emplace_back([this, a, b] { for (size_t i = a; i < b; ++i) new (p_ + i) Secret(); });
+    }
+    for (auto& t : ts) t.join();
+  }
+  n_ = n;
 }
 
 }  // namespace tsg

@@ -286,7 +286,7 @@ class Pipeline {
       in.paths = pp.data();
       in.path_lens = pl.data();
       in.binary = job->b.binary.data();
-      std::vector<Secret> res;
+      SecretVec res;
       std::string err;
       if (!scan_(in, &res, &err)) { set_error(err); return; }
       out_->st.scanned_bytes += job->b.offsets[nk];

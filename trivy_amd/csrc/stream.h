@@ -21,7 +21,7 @@
 namespace tsg {
 
 // The scan stage: results[i] = Scan(ScanArgs{paths[i], data[off[i]:off[i+1]], binary[i]}).
-using BatchScanFn = std::function<bool(const BatchInput& in, std::vector<Secret>* results, std::string* err)>;
+using BatchScanFn = std::function<bool(const BatchInput& in, SecretVec* results, std::string* err)>;
 
 // A reader (io.Reader): > 0 bytes read into buf, 0 at the end, < 0 on an error.
 using StreamReadFn = int64_t (*)(void* user, uint8_t* buf, size_t cap);
@@ -46,7 +46,7 @@ struct StreamStats {
 };
 
 struct StreamResult {
-  std::vector<Secret> files;              // every scanned file, walk order
+  SecretVec files;              // every scanned file, walk order
   std::vector<std::string> walked;        // every regular file handed to the analyzers, walk order
   std::vector<std::string> opq_dirs, wh_files;
   StreamStats st;
