@@ -129,3 +129,15 @@ def test_multi_driver_queue_equals_single(monkeypatch):
     assert stats["devices"] == 3
     assert stats["pieces"] >= 20
     assert got == want
+
+
+def test_many_files_result_vector_cpu():
+    # > 64k files: the per-file result vector is constructed on several
+    # threads (SecretVec::resize); every file keeps its own result
+    n = 70_000
+    args = [S.ScanArgs("/f/%d.txt" % i, b"plain text %d\n" % i) for i in range(n)]
+    args[12345] = S.ScanArgs("/f/key.txt", b"token = ghp_" + b"a1B2" * 9 + b"\n")
+    got = S.scan_table_model(S.Scanner(None), args)
+    assert len(got) == n
+    hits = [i for i, g in enumerate(got) if g.get("Findings")]
+    assert hits == [12345] and got[12345]["FilePath"] == "/f/key.txt"
