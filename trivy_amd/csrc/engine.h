@@ -83,7 +83,8 @@ class Engine {
   struct Segment;
   bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, const uint64_t* d_off_up,
                    ScanStats* st, GpuOut* out, std::string* err);
-  void confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Secret* results, uint64_t* nconf,
+  void plan_confirm(const Segment& sg, GpuOut* g) const;
+  void confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* results, uint64_t* nconf,
                        uint64_t* nfind, bool gpu_in_flight);
   Lane* acquire_lane(DeviceTables& dt, std::string* err);
   void release_lane(DeviceTables& dt, Lane* ln);
@@ -113,7 +114,7 @@ class Engine {
   uint32_t pieces_ = 4;                 // resident data: pipeline pieces (TSG_PIECES; r3za config 2: 4 pieces, first 10%: 1286 GB/s, 2 at 70/30: 919)
   double first_piece_ = 0.1;            // resident data: share of the first piece (TSG_FIRST_PIECE)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
-  uint64_t segment_min_ = 128ull << 20;  // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1)
+  uint64_t segment_min_ = 64ull << 20;   // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1; r4p: 64 MB 53.2 vs 128 MB 52.5)
   uint64_t segment_tail_ = 0;           // uploaded data: a short last segment (TSG_SEGMENT_TAIL; 0 = none: the
                                         // rest after the full segments is one launch, K1 keeps its large-launch rate)
   uint64_t segment_ = 4ull << 30;       // uploaded data: bytes per pipeline segment (TSG_SEGMENT_BYTES);

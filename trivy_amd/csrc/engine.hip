@@ -611,6 +611,24 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
 // K1c's 16-byte word: two halves of 8 bytes (8 class reads, then the 8
 // dependent steps, then their outputs), so the two-read step's registers fit
 // the 128-VGPR budget of 1024-thread workgroups without spilling.
+// measurement only (invalid results): K1c's step with the row read alone
+// (no record), or with both reads but no exception test (their values
+// folded by two VALU): prices the record read and the select chain
+constexpr int kAblCRowOnly = 16384, kAblCNoSelect = 32768;
+template <int kAbl>
+__device__ __forceinline__ uint32_t k1c_step_abl(uint32_t s, uint32_t c4) {
+  if constexpr ((kAbl & kAblCRowOnly) != 0) {
+    return k1_lds32(((s >> 16) << 2) + c4);
+  } else if constexpr ((kAbl & kAblCNoSelect) != 0) {
+    const uint32_t f = k1_lds32(((s >> 16) << 2) + c4);
+    const v4u d = k1_lds128(s & 0xfff0u);
+    return f ^ (d.y & 0x10u);
+  } else {
+    return k1c_next(s, c4, __builtin_amdgcn_perm(0u, c4, 0u));   // c4 in every byte
+  }
+}
+
+template <int kAbl>
 __device__ __forceinline__ void k1_word_c(const K1Ctx& x, K1Stream& t, OutBuf& ob, const uint8_t* smem,
                                           uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   const bool emit = t.p >= t.emit;
@@ -624,7 +642,7 @@ __device__ __forceinline__ void k1_word_c(const K1Ctx& x, K1Stream& t, OutBuf& o
     uint32_t st[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      s = k1c_next(s, c4[k], __builtin_amdgcn_perm(0u, c4[k], 0u));   // c4 in every byte
+      s = k1c_step_abl<kAbl>(s, c4[k]);
       st[k] = s;
     }
     if (emit) {
@@ -801,13 +819,13 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
               // cur[i] by register indexing
 #pragma unroll 1
               for (int i = 0; i < kW; ++i) {
-                if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+                if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
                 else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
               }
             } else {
 #pragma unroll
               for (int i = 0; i < kW; ++i) {
-                if constexpr (kC) k1_word_c(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
+                if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
                 else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cur[i].x, cur[i].y, cur[i].z, cur[i].w);
               }
             }
@@ -832,7 +850,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
               if ((kAbl & kAblDefer) && (kAbl & kAblBoundaryFastWords) && t.p + 16 <= t.lim) {
                 if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit)
                   k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
-                if constexpr (kC) k1_word_c(x, t, ob, smem, w[0], w[1], w[2], w[3]);
+                if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, w[0], w[1], w[2], w[3]);
                 else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, w[0], w[1], w[2], w[3]);
               } else {
                 if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
@@ -862,7 +880,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             if ((kAbl & kAblDefer) && (kAbl & kAblBoundaryFastWords) && t.p + 16 <= t.lim) {
               if (x.primary && ((v.x | v.y | v.z | v.w) & 0x80808080u) && t.p >= t.emit)
                 k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
-              if constexpr (kC) k1_word_c(x, t, ob, smem, v.x, v.y, v.z, v.w);
+              if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, v.x, v.y, v.z, v.w);
               else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, v.x, v.y, v.z, v.w);
             } else {
               if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);   // before the word that may change the file
@@ -914,7 +932,14 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
 // (python -m trivy_amd.build --probe -> libtrivysecret_probe.so, -DTSG_K1_PROBE).
 constexpr int kK1Default = 464;
 const void* k1_kernel(int abl, bool compressed) {
-  if (compressed) return abl == kK1Default ? reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, kK1Default, true>) : nullptr;
+  if (compressed) {
+    if (abl == kK1Default) return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, kK1Default, true>);
+#ifdef TSG_K1_PROBE
+    if (abl == (kK1Default | kAblCRowOnly)) return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, kK1Default | kAblCRowOnly, true>);
+    if (abl == (kK1Default | kAblCNoSelect)) return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, kK1Default | kAblCNoSelect, true>);
+#endif
+    return nullptr;
+  }
   switch (abl) {
 #define TSG_K1_V3(A) case (A): return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, (A), false>);
     TSG_K1_V3(kK1Default)
@@ -1077,6 +1102,12 @@ struct GpuOut {
   std::vector<uint16_t> nl;     // '\n' count per K1 chunk
   std::vector<uint32_t> ff;     // per-file flags (fold-special content)
   uint32_t chunk = 0;           // K1 chunk bytes of this segment (nl[] granularity)
+  // the confirmation's plan (plan_confirm), built by the segment's driver
+  // thread while the host confirms the previous segment: candidates grouped
+  // per file, the files to confirm (largest first) and the rest
+  bool planned = false;
+  std::vector<uint32_t> per_file, work, light;
+  std::vector<CandDev> sorted;
 };
 
 // One call's host confirm resources.
@@ -1827,24 +1858,50 @@ bool Engine::strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles,
 
 // Host confirmation of one segment (files [0, in.nfiles) of sg.in, results
 // into results[0..nfiles)) from that segment's GPU output `g`.
-void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Secret* results, uint64_t* nconf_out,
-                             uint64_t* nfind_out, bool gpu_in_flight) {
+void Engine::plan_confirm(const Segment& sg, GpuOut* gp) const {
+  GpuOut& g = *gp;
   const BatchInput& in = sg.in;
-  const Ruleset& rs = *rs_;
-  const size_t nr = rs.rules.size();
-  const size_t nplan = pf_.rules.size();   // rules + exclude-block pseudo-rules
-  const auto t_begin = std::chrono::steady_clock::now();
+  const size_t nr = rs_->rules.size();
   // group candidates per file (counting sort by file, then sort each file's list)
-  std::vector<uint32_t> per_file(in.nfiles + 1, 0);
-  for (const CandDev& c : g.cands) per_file[c.file + 1]++;
-  for (uint32_t f = 0; f < in.nfiles; ++f) per_file[f + 1] += per_file[f];
-  std::vector<CandDev> sorted(g.cands.size());
+  g.per_file.assign(in.nfiles + 1, 0);
+  for (const CandDev& c : g.cands) g.per_file[c.file + 1]++;
+  for (uint32_t f = 0; f < in.nfiles; ++f) g.per_file[f + 1] += g.per_file[f];
+  g.sorted.resize(g.cands.size());
   {
-    std::vector<uint32_t> pos(per_file.begin(), per_file.end() - 1);
-    for (const CandDev& c : g.cands) sorted[pos[c.file]++] = c;
+    std::vector<uint32_t> pos(g.per_file.begin(), g.per_file.end() - 1);
+    for (const CandDev& c : g.cands) g.sorted[pos[c.file]++] = c;
   }
   bool any_full = false;
   for (size_t r = 0; r < nr; ++r) if (pf_.rules[r].mode == 1) any_full = true;
+  // files to confirm (candidates, fold-special content, or host-evaluated
+  // rules), largest first (LPT: the per-file confirm cost grows with size);
+  // every other file only needs the global allow-path outcome and is handled
+  // in blocks after them (image layers: hundreds of thousands of such files)
+  g.work.clear();
+  g.light.clear();
+  g.work.reserve(in.nfiles / 4 + 16);
+  for (uint32_t f = sg.lead; f < in.nfiles; ++f) {
+    if (any_full || g.ff[f] || g.per_file[f] != g.per_file[f + 1]) g.work.push_back(f);
+    else g.light.push_back(f);
+  }
+  std::sort(g.work.begin(), g.work.end(), [&](uint32_t a, uint32_t b) {
+    const uint64_t sa = in.offsets[a + 1] - in.offsets[a], sb = in.offsets[b + 1] - in.offsets[b];
+    return sa != sb ? sa > sb : a < b;
+  });
+  g.planned = true;
+}
+
+void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* results, uint64_t* nconf_out,
+                             uint64_t* nfind_out, bool gpu_in_flight) {
+  const BatchInput& in = sg.in;
+  const Ruleset& rs = *rs_;
+  const size_t nplan = pf_.rules.size();   // rules + exclude-block pseudo-rules
+  const auto t_begin = std::chrono::steady_clock::now();
+  if (!g.planned) plan_confirm(sg, &g);
+  const std::vector<uint32_t>& per_file = g.per_file;
+  std::vector<CandDev>& sorted = g.sorted;
+  const std::vector<uint32_t>& work = g.work;
+  const std::vector<uint32_t>& light = g.light;
   // the plan every confirmed file starts from, and its mode-1 rules
   std::vector<uint8_t> kind0(nplan, kPlanNoMatch);
   std::vector<uint32_t> full_rules;
@@ -1854,21 +1911,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, const GpuOut& g, Se
       full_rules.push_back(static_cast<uint32_t>(r));
     }
   }
-  // files to confirm (candidates, fold-special content, or host-evaluated
-  // rules), largest first (LPT: the per-file confirm cost grows with size);
-  // every other file only needs the global allow-path outcome and is handled
-  // in blocks after them (image layers: hundreds of thousands of such files)
-  std::vector<uint32_t> work, light;
-  work.reserve(in.nfiles / 4 + 16);
   results -= sg.lead;                      // results[f] for the piece's files f >= lead
-  for (uint32_t f = sg.lead; f < in.nfiles; ++f) {
-    if (any_full || g.ff[f] || per_file[f] != per_file[f + 1]) work.push_back(f);
-    else light.push_back(f);
-  }
-  std::sort(work.begin(), work.end(), [&](uint32_t a, uint32_t b) {
-    const uint64_t sa = in.offsets[a + 1] - in.offsets[a], sb = in.offsets[b + 1] - in.offsets[b];
-    return sa != sb ? sa > sb : a < b;
-  });
   constexpr uint32_t kLightBlock = 512;
   const uint32_t nlight_blocks = static_cast<uint32_t>((light.size() + kLightBlock - 1) / kLightBlock);
   std::atomic<uint32_t> next_light{0};
@@ -2208,6 +2251,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       const double h_start = ms_since(t_feed0);
       ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e);
       if (!ok) break;
+      plan_confirm(segs[cur], &job->out);      // off the confirming thread (it is busy with the previous segment)
       if (host_profile_) {
         // GPU timeline of this segment from the scan's anchor event
         float ub = 0, ud = 0, k1a = 0, k1b = 0, k2b = 0;
