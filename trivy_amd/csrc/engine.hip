@@ -1102,9 +1102,10 @@ struct GpuOut {
   std::vector<uint16_t> nl;     // '\n' count per K1 chunk
   std::vector<uint32_t> ff;     // per-file flags (fold-special content)
   uint32_t chunk = 0;           // K1 chunk bytes of this segment (nl[] granularity)
-  // the confirmation's plan (plan_confirm), built by the segment's driver
-  // thread while the host confirms the previous segment: candidates grouped
-  // per file, the files to confirm (largest first) and the rest
+  // the confirmation's plan (plan_confirm): candidates grouped per file, the
+  // files to confirm (largest first) and the rest.  (Built on the driver
+  // thread it delayed the next piece's launch by as much as it saved the
+  // confirming thread: profiles/rd4q_bench_c3prof.log.)
   bool planned = false;
   std::vector<uint32_t> per_file, work, light;
   std::vector<CandDev> sorted;
@@ -2251,7 +2252,6 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       const double h_start = ms_since(t_feed0);
       ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e);
       if (!ok) break;
-      plan_confirm(segs[cur], &job->out);      // off the confirming thread (it is busy with the previous segment)
       if (host_profile_) {
         // GPU timeline of this segment from the scan's anchor event
         float ub = 0, ud = 0, k1a = 0, k1b = 0, k2b = 0;
