@@ -140,6 +140,11 @@ struct Job {
   std::vector<std::string> scan_paths;
 };
 
+// Producer -> prepare -> scan.  The producer (walk + reads) fills one of two
+// raw batch buffers while a prepare thread turns the other (filled) one into
+// a prepared pinned batch and the consumer thread scans the batch before it:
+// the prepare of batch k overlaps the reads of batch k+1 (round 4: a
+// synchronous prepare stopped the walk for ~9 ms per 256 MiB batch).
 class Pipeline {
  public:
   Pipeline(const Ruleset& rs, const StreamOpts& o, const BatchScanFn& scan, const char* prefix, StreamResult* out)
@@ -149,8 +154,9 @@ class Pipeline {
     limit_ = std::max<uint64_t>(o.batch_bytes, 1);
     // the whole batch limit at once: its pages are only backed as a batch
     // fills (no growth copies); a file larger than a batch grows it
-    raw_cap_ = limit_;
-    raw_.reset(new uint8_t[raw_cap_]);
+    raw_cap_[0] = limit_;
+    raw_[0].reset(new uint8_t[raw_cap_[0]]);
+    prep_ = std::thread([this] { prepare_loop(); });
     consumer_ = std::thread([this] { consume(); });
   }
   ~Pipeline() { finish(); }
@@ -159,14 +165,11 @@ class Pipeline {
   // if it does not fit); returns where to put it, nullptr on failure
   uint8_t* reserve(uint64_t n) {
     if (!paths_.empty() && used_ + n > limit_ && !flush()) return nullptr;
-    if (used_ + n > raw_cap_) {                 // grow (a file larger than a batch: a buffer of its size)
-      const uint64_t cap = std::max<uint64_t>(used_ + n, std::min<uint64_t>(limit_, 2 * raw_cap_));
-      std::unique_ptr<uint8_t[]> nb(new uint8_t[cap]);
-      std::memcpy(nb.get(), raw_.get(), used_);
-      raw_ = std::move(nb);
-      raw_cap_ = cap;
+    if (used_ + n > raw_cap_[cur_]) {           // grow (a file larger than a batch: a buffer of its size)
+      const uint64_t cap = std::max<uint64_t>(used_ + n, std::min<uint64_t>(limit_, 2 * raw_cap_[cur_]));
+      grow_window(cap, 0, used_);
     }
-    return raw_.get() + used_;
+    return raw_[cur_].get() + used_;
   }
   // the file just written at reserve()'s pointer: n bytes
   void commit(const std::string& path, uint64_t n) {
@@ -176,13 +179,13 @@ class Pipeline {
     used_ += n;
     out_->st.read_bytes += n;
   }
-  // Window mode (stream_layer): the tar reader fills raw_ itself and the
-  // kept files are committed where they lie, so file data is copied once
-  // (reader -> window) on its way to the prepared batch.
-  uint8_t* window() { return raw_.get(); }
-  uint64_t window_cap() const { return raw_cap_; }
+  // Window mode (stream_layer): the tar reader fills the raw buffer itself
+  // and the kept files are committed where they lie, so file data is copied
+  // once (reader -> window) on its way to the prepared batch.
+  uint8_t* window() { return raw_[cur_].get(); }
+  uint64_t window_cap() const { return raw_cap_[cur_]; }
   bool has_files() const { return !paths_.empty(); }
-  double flush_wall_ms() const { return flush_wall_ms_; }   // wall time inside flush() so far
+  double flush_wall_ms() const { return flush_wall_ms_; }   // producer wall time inside flush() so far
   void commit_at(const std::string& path, uint64_t off, uint64_t n) {
     starts_.push_back(off);
     sizes_.push_back(n);
@@ -190,60 +193,72 @@ class Pipeline {
     used_ += n;
     out_->st.read_bytes += n;
   }
-  // a larger window holding the unconsumed bytes [from, to) at its start
-  // (only between batches: no file is committed)
+  // a larger current buffer holding its bytes [from, to) at its start
+  // (no file committed in it)
   void grow_window(uint64_t cap, uint64_t from, uint64_t to) {
     std::unique_ptr<uint8_t[]> nb(new uint8_t[cap]);
-    std::memcpy(nb.get(), raw_.get() + from, to - from);
-    raw_ = std::move(nb);
-    raw_cap_ = cap;
+    if (to > from) std::memcpy(nb.get(), raw_[cur_].get() + from, to - from);
+    raw_[cur_] = std::move(nb);
+    raw_cap_[cur_] = cap;
   }
-  // prepare the current batch and hand it to the scan stage
+  // the window is full: hand its committed files to the prepare thread and
+  // continue in the other buffer with the unconsumed bytes [from, to) of
+  // this one at its start (or, with no file committed, move them down in place)
+  bool next_window(uint64_t from, uint64_t to) {
+    const uint64_t keep = to - from;
+    if (paths_.empty()) {
+      if (from) std::memmove(raw_[cur_].get(), raw_[cur_].get() + from, keep);
+      return ok();
+    }
+    const int old = cur_;
+    if (!flush()) return false;                 // switches cur_ (the prepare reads [0, from) of `old`)
+    if (raw_cap_[cur_] < keep) { raw_[cur_].reset(new uint8_t[keep]); raw_cap_[cur_] = keep; }
+    if (keep) std::memcpy(raw_[cur_].get(), raw_[old].get() + from, keep);
+    return ok();
+  }
+  // hand the current batch to the prepare thread and switch buffers
   bool flush() {
     if (paths_.empty()) return ok();
     const auto t0 = Clock::now();
-    auto job = std::make_unique<Job>();
-    std::string err;
-    double wait = 0;
-    BufPool* pool = &pool_;
-    FeedAlloc alloc = [pool, &wait](size_t bytes, FeedFree* free_fn) -> uint8_t* {
-      uint8_t* p = pool->get(bytes, &wait);
-      if (p) *free_fn = [pool](uint8_t* q) { pool->put(q); };
-      return p;
-    };
-    if (!prepare_files(rs_, fo_, raw_.get(), starts_.data(), sizes_.data(), paths_, o_.threads, &job->b, &err, alloc)) {
-      set_error(err);
-      return false;
-    }
-    if (!job->b.data) { set_error("out of memory for a prepared batch"); return false; }
-    for (uint32_t i : job->b.index) job->scan_paths.push_back(prefix_ + paths_[i]);
-    out_->st.peak_batch_bytes = std::max<uint64_t>(out_->st.peak_batch_bytes, used_);
-    out_->st.wait_ms += wait;
-    out_->st.feed_ms -= wait;                   // blocked on a buffer: not feed work
-    starts_.clear();
-    sizes_.clear();
-    paths_.clear();
+    auto task = std::make_unique<PrepTask>();
+    task->buf = cur_;
+    task->used = used_;
+    task->starts.swap(starts_);
+    task->sizes.swap(sizes_);
+    task->paths.swap(paths_);
     used_ = 0;
-    out_->st.feed_ms += ms_between(t0, Clock::now());
-    flush_wall_ms_ += ms_between(t0, Clock::now());
     {
       std::unique_lock<std::mutex> lk(mu_);
-      q_.push_back(std::move(job));
+      busy_[cur_] = true;
+      prep_q_.push_back(std::move(task));
+      cv_.notify_all();
+      cur_ ^= 1;
+      // the other buffer is free once its previous batch has been prepared
+      cv_.wait(lk, [&] { return !busy_[cur_] || !err_.empty(); });
     }
-    cv_.notify_all();
+    if (!raw_[cur_]) { raw_cap_[cur_] = limit_; raw_[cur_].reset(new uint8_t[limit_]); }
+    flush_wall_ms_ += ms_between(t0, Clock::now());
     return ok();
   }
-  // drain: the last batch, then wait for the scan stage; true if no error
+  // drain: the last batch, then wait for the prepare and scan stages; true if no error
   bool finish() {
     if (finished_) return ok();
     finished_ = true;
     if (ok()) flush();
     {
       std::lock_guard<std::mutex> lk(mu_);
+      prep_done_ = true;
+    }
+    cv_.notify_all();
+    if (prep_.joinable()) prep_.join();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
       done_ = true;
     }
     cv_.notify_all();
     if (consumer_.joinable()) consumer_.join();
+    out_->st.feed_ms += prep_ms_;
+    out_->st.wait_ms += prep_wait_ms_;
     return ok();
   }
   bool ok() {
@@ -261,6 +276,50 @@ class Pipeline {
   }
 
  private:
+  struct PrepTask {
+    int buf = 0;
+    uint64_t used = 0;
+    std::vector<uint64_t> starts, sizes;
+    std::vector<std::string> paths;
+  };
+  void prepare_loop() {
+    for (;;) {
+      std::unique_ptr<PrepTask> task;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !prep_q_.empty() || prep_done_; });
+        if (prep_q_.empty()) return;
+        task = std::move(prep_q_.front());
+        prep_q_.pop_front();
+      }
+      const auto t0 = Clock::now();
+      auto job = std::make_unique<Job>();
+      std::string err;
+      double wait = 0;
+      BufPool* pool = &pool_;
+      FeedAlloc alloc = [pool, &wait](size_t bytes, FeedFree* free_fn) -> uint8_t* {
+        uint8_t* p = pool->get(bytes, &wait);
+        if (p) *free_fn = [pool](uint8_t* q) { pool->put(q); };
+        return p;
+      };
+      bool good = ok() && prepare_files(rs_, fo_, raw_[task->buf].get(), task->starts.data(), task->sizes.data(),
+                                        task->paths, o_.threads, &job->b, &err, alloc);
+      if (good && !job->b.data) { good = false; err = "out of memory for a prepared batch"; }
+      if (good) for (uint32_t i : job->b.index) job->scan_paths.push_back(prefix_ + task->paths[i]);
+      std::lock_guard<std::mutex> lk(mu_);
+      busy_[task->buf] = false;
+      if (!good) {
+        if (err_.empty()) err_ = err.empty() ? std::string("prepare failed") : err;
+      } else {
+        peak_batch_ = std::max<uint64_t>(peak_batch_, task->used);
+        out_->st.peak_batch_bytes = peak_batch_;
+        prep_ms_ += ms_between(t0, Clock::now()) - wait;   // blocked on a buffer: not feed work
+        prep_wait_ms_ += wait;
+        q_.push_back(std::move(job));
+      }
+      cv_.notify_all();
+    }
+  }
   void consume() {
     for (;;) {
       std::unique_ptr<Job> job;
@@ -305,17 +364,21 @@ class Pipeline {
   StreamResult* out_;
   FeedOpts fo_;
   BufPool pool_;
-  std::unique_ptr<uint8_t[]> raw_;
-  uint64_t limit_ = 0, raw_cap_ = 0, used_ = 0;
+  std::unique_ptr<uint8_t[]> raw_[2];
+  uint64_t raw_cap_[2] = {0, 0};
+  int cur_ = 0;
+  bool busy_[2] = {false, false};
+  uint64_t limit_ = 0, used_ = 0, peak_batch_ = 0;
   std::vector<uint64_t> starts_, sizes_;
-  double flush_wall_ms_ = 0;
   std::vector<std::string> paths_;
+  double flush_wall_ms_ = 0, prep_ms_ = 0, prep_wait_ms_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;
+  std::deque<std::unique_ptr<PrepTask>> prep_q_;
   std::deque<std::unique_ptr<Job>> q_;
-  bool done_ = false, finished_ = false;
+  bool prep_done_ = false, done_ = false, finished_ = false;
   std::string err_;
-  std::thread consumer_;
+  std::thread prep_, consumer_;
 };
 
 // a layer from a reader callback
@@ -380,13 +443,13 @@ class WindowTarInput : public TarInput {
   bool fill(uint64_t need, std::string* err) {
     while (wlen_ - rpos_ < need && !eof_ && !failed_) {
       if (rpos_ + need > pl_->window_cap() || wlen_ == pl_->window_cap()) {
-        // make room: prepare the files committed in the window, then move the
-        // unconsumed tail to the start; a window still full holds part of a
-        // file larger than a batch: double it (by the bytes actually read, so
-        // a hostile size field ends in "unexpected EOF", not an allocation)
-        if (pl_->has_files() && !pl_->flush()) { *err = pl_->error(); return false; }
+        // make room: hand the files committed in the window to the prepare
+        // stage and continue in the other buffer with the unconsumed tail at
+        // its start; a window still full holds part of a file larger than a
+        // batch: double it (by the bytes actually read, so a hostile size
+        // field ends in "unexpected EOF", not an allocation)
         const uint64_t keep = wlen_ - rpos_;
-        if (rpos_) std::memmove(pl_->window(), pl_->window() + rpos_, keep);
+        if (!pl_->next_window(rpos_, wlen_)) { *err = pl_->error(); return false; }
         rpos_ = 0;
         wlen_ = keep;
         if (wlen_ == pl_->window_cap()) pl_->grow_window(2 * pl_->window_cap(), 0, wlen_);
