@@ -113,6 +113,7 @@ class Engine {
   std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
   uint32_t pieces_ = 4;                 // resident data: pipeline pieces (TSG_PIECES; r3za config 2: 4 pieces, first 10%: 1286 GB/s, 2 at 70/30: 919)
   double first_piece_ = 0.1;            // resident data: share of the first piece (TSG_FIRST_PIECE)
+  double last_piece_ = 0.0;             // resident data: share of a short last piece (TSG_LAST_PIECE; 0: none)
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
   uint64_t segment_min_ = 64ull << 20;   // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1; r4p: 64 MB 53.2 vs 128 MB 52.5)
   uint64_t segment_tail_ = 0;           // uploaded data: a short last segment (TSG_SEGMENT_TAIL; 0 = none: the

@@ -1422,6 +1422,10 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const double v = std::atof(c);
     if (v > 0.0 && v < 1.0) e->first_piece_ = v;
   }
+  if (const char* c = std::getenv("TSG_LAST_PIECE")) {
+    const double v = std::atof(c);
+    if (v >= 0.0 && v < 0.5) e->last_piece_ = v;
+  }
   if (const char* c = std::getenv("TSG_MIN_PIECE_BYTES")) {
     const long long v = std::atoll(c);
     if (v >= 1) e->min_piece_ = static_cast<uint64_t>(v);
@@ -2075,9 +2079,14 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       for (auto& d : dev_) if (d->device == dev) { drivers.push_back(d.get()); break; }
       if (drivers.empty()) { *err = "d_data is not device memory of one of the engine's devices"; return false; }
       const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(pieces_, std::max<uint64_t>(1, total / min_piece_)));
+      // piece 0 takes first_piece_ of the bytes; with last_piece_ a short
+      // last piece of that share follows the others (its confirmation is the
+      // tail left after the GPU's last pass); the rest share what remains
+      const bool short_last = last_piece_ > 0.0 && want >= 3;
+      const double mid = 1.0 - first_piece_ - (short_last ? last_piece_ : 0.0);
+      const uint32_t nmid = want - 1 - (short_last ? 1 : 0);
       for (uint32_t p = 1; p < want; ++p) {
-        // piece 0 takes first_piece_ of the bytes, the others share the rest
-        const double share = first_piece_ + (1.0 - first_piece_) * (p - 1) / (want - 1);
+        const double share = p <= nmid ? first_piece_ + mid * (p - 1) / nmid : 1.0 - last_piece_;
         const uint64_t target = static_cast<uint64_t>(share * static_cast<double>(total));
         const uint32_t f = static_cast<uint32_t>(std::lower_bound(in.offsets, in.offsets + in.nfiles, target) - in.offsets);
         if (f > cut.back() && f < in.nfiles) cut.push_back(f);
