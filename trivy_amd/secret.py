@@ -16,6 +16,7 @@ types.Secret is returned as a dict with the Go field names
 Go byte strings are decoded with 'surrogateescape'.  Scan runs on the GPU; a
 machine without a HIP device raises instead of silently scanning on the CPU.
 """
+import collections.abc
 import ctypes
 import json
 import os
@@ -392,10 +393,34 @@ def _reader(fileobj):
     return _lib.READ_FN(read)
 
 
+class _Walk(collections.abc.Mapping):
+    """Walk's outcome ("files", "opq_dirs", "wh_files", "stats"), decoded from
+    the engine's JSON on first use (a layer's walked-path list runs to
+    megabytes; most callers only want the findings)."""
+
+    def __init__(self, raw):
+        self._raw, self._d = raw, None
+
+    def _get(self):
+        if self._d is None:
+            self._d = json.loads(self._raw.decode("utf-8", "surrogateescape")) if self._raw else {}
+            self._raw = None
+        return self._d
+
+    def __getitem__(self, k):
+        return self._get()[k]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
+
+
 def _stream_result(L, rc, res, as_result):
     if rc != 0:
         raise WalkError(L.tsg_last_error().decode("utf-8", "replace"))
-    walk = json.loads(L.tsg_result_walk_json(res).decode("utf-8", "surrogateescape"))
+    walk = _Walk(L.tsg_result_walk_json(res))
     if as_result:
         from .report import ScanResult
         return ScanResult(res), walk
