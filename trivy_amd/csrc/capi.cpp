@@ -74,7 +74,11 @@ struct tsg_result {
   ScanStats stats;
   std::vector<std::vector<std::vector<uint64_t>>> cands;   // optional [file][rule]
   std::vector<std::vector<LayerRef>> layers;               // optional [file][finding] (tsg_result_from_proto)
-  std::string walk_json;                                   // streamed results (tsg_result_walk_json)
+  // streamed results: the walk outcome, turned into JSON on the first
+  // tsg_result_walk_json call (a layer's walked-path list runs to megabytes)
+  std::unique_ptr<StreamResult> walk;
+  mutable std::mutex walk_mu;
+  mutable std::string walk_json;
 };
 
 extern "C" {
@@ -1179,11 +1183,8 @@ bool stream_opts(const tsg_feed_opts* opts, uint64_t batch_bytes, bool pinned, S
   return true;
 }
 
-tsg_result* stream_result(std::shared_ptr<const Ruleset> rs, StreamResult&& sr) {
-  auto* r = new tsg_result();
-  r->rs = std::move(rs);
-  r->files = std::move(sr.files);
-  std::string& js = r->walk_json;
+void build_walk_json(const StreamResult& sr, std::string* out) {
+  std::string& js = *out;
   js = "{\"files\": ";
   json_str_array(&js, sr.walked);
   js += ", \"opq_dirs\": ";
@@ -1201,9 +1202,16 @@ tsg_result* stream_result(std::shared_ptr<const Ruleset> rs, StreamResult&& sr) 
                 static_cast<unsigned long long>(st.batches), static_cast<unsigned long long>(st.files),
                 static_cast<unsigned long long>(st.peak_batch_bytes));
   js += buf;
-  r->stats.bytes = st.scanned_bytes;
-  r->stats.files = st.files;
-  r->stats.total_ms = st.wall_ms;
+}
+
+tsg_result* stream_result(std::shared_ptr<const Ruleset> rs, StreamResult&& sr) {
+  auto* r = new tsg_result();
+  r->rs = std::move(rs);
+  r->files = std::move(sr.files);
+  r->stats.bytes = sr.st.scanned_bytes;
+  r->stats.files = sr.st.files;
+  r->stats.total_ms = sr.st.wall_ms;
+  r->walk.reset(new StreamResult(std::move(sr)));
   return r;
 }
 
@@ -1365,7 +1373,12 @@ int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, 
   TSG_API_CATCH
 }
 
-const char* tsg_result_walk_json(const tsg_result* r) { return r && !r->walk_json.empty() ? r->walk_json.c_str() : nullptr; }
+const char* tsg_result_walk_json(const tsg_result* r) {
+  if (!r || !r->walk) return nullptr;
+  std::lock_guard<std::mutex> lk(r->walk_mu);
+  if (r->walk_json.empty()) build_walk_json(*r->walk, &r->walk_json);
+  return r->walk_json.c_str();
+}
 
 int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens) {
   TSG_API_TRY
