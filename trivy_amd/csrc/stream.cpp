@@ -82,8 +82,11 @@ class BufPool {
   uint8_t* get(size_t bytes, double* wait_ms) {
     std::unique_lock<std::mutex> lk(mu_);
     const auto t0 = Clock::now();
-    cv_.wait(lk, [&] { return bufs_.size() < n_ || std::any_of(bufs_.begin(), bufs_.end(), [](const B& b) { return !b.used; }); });
+    cv_.wait(lk, [&] {
+      return cancelled_ || bufs_.size() < n_ || std::any_of(bufs_.begin(), bufs_.end(), [](const B& b) { return !b.used; });
+    });
     *wait_ms += ms_between(t0, Clock::now());
+    if (cancelled_) return nullptr;
     for (auto& b : bufs_) {
       if (b.used) continue;
       if (b.cap < bytes) {
@@ -104,6 +107,13 @@ class BufPool {
   void put(uint8_t* p) {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& b : bufs_) if (b.p == p) b.used = false;
+    cv_.notify_all();
+  }
+  // the pipeline failed: waiters give up (the scan stage may have stopped
+  // returning buffers)
+  void cancel() {
+    std::lock_guard<std::mutex> lk(mu_);
+    cancelled_ = true;
     cv_.notify_all();
   }
 
@@ -129,6 +139,7 @@ class BufPool {
   }
   bool pinned_;
   size_t n_;
+  bool cancelled_ = false;
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<B> bufs_;
@@ -270,9 +281,12 @@ class Pipeline {
     return err_;
   }
   void set_error(const std::string& e) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (err_.empty()) err_ = e;
-    cv_.notify_all();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (err_.empty()) err_ = e;
+      cv_.notify_all();
+    }
+    pool_.cancel();
   }
 
  private:
@@ -310,6 +324,7 @@ class Pipeline {
       busy_[task->buf] = false;
       if (!good) {
         if (err_.empty()) err_ = err.empty() ? std::string("prepare failed") : err;
+        pool_.cancel();
       } else {
         peak_batch_ = std::max<uint64_t>(peak_batch_, task->used);
         out_->st.peak_batch_bytes = peak_batch_;
