@@ -326,7 +326,7 @@ typedef int64_t (*tsg_read_fn)(void* user, uint8_t* buf, size_t cap);
  * io.Reader (pkg/fanal/walker/tar.go:35-103) -> AnalyzeFile's gate
  * (analyzer.go:403-419) before a file's content is read -> SecretAnalyzer
  * .Analyze's preparation (secret.go:103-150) -> Scan, the kept files packed
- * into batches of about batch_bytes raw bytes (0: 512 MiB; a larger file is a
+ * into batches of about batch_bytes raw bytes (0: 256 MiB; a larger file is a
  * batch of its own), each scanned on the engine while the next is read.  The
  * result holds every scanned file in walk order, ScanArgs.FilePath = "/" +
  * path; tsg_result_walk_json gives Walk's return values and the feed timing.

@@ -71,6 +71,48 @@ class PinnedCache {
   size_t bytes_ = 0;
 };
 
+// Raw batch buffers (the windows) likewise outlive one stream: a fresh
+// 256 MiB window is backed page by page as the reader first fills it, on
+// every call and every layer.  Up to 2 GiB are kept.
+class RawCache {
+ public:
+  static RawCache& get() {
+    static RawCache* c = new RawCache();
+    return *c;
+  }
+  // a buffer of at least `want` bytes; *cap = its real size
+  std::unique_ptr<uint8_t[]> take(uint64_t want, uint64_t* cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      size_t best = free_.size();
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].second >= want && (best == free_.size() || free_[i].second < free_[best].second)) best = i;
+      if (best != free_.size()) {
+        uint8_t* p = free_[best].first;
+        *cap = free_[best].second;
+        bytes_ -= *cap;
+        free_.erase(free_.begin() + static_cast<long>(best));
+        return std::unique_ptr<uint8_t[]>(p);
+      }
+    }
+    *cap = want;
+    return std::unique_ptr<uint8_t[]>(new uint8_t[want]);
+  }
+  void give(std::unique_ptr<uint8_t[]> p, uint64_t cap) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (bytes_ + cap > kMax) return;            // freed by the unique_ptr
+    free_.push_back({p.release(), cap});
+    bytes_ += cap;
+  }
+
+ private:
+  static constexpr uint64_t kMax = 2ull << 30;
+  std::mutex mu_;
+  std::vector<std::pair<uint8_t*, uint64_t>> free_;
+  uint64_t bytes_ = 0;
+};
+
 // The prepared-batch buffers: `n` of them in circulation, grown on demand.
 class BufPool {
  public:
@@ -166,11 +208,14 @@ class Pipeline {
     // the whole batch limit at once: its pages are only backed as a batch
     // fills (no growth copies); a file larger than a batch grows it
     raw_cap_[0] = limit_;
-    raw_[0].reset(new uint8_t[raw_cap_[0]]);
+    raw_[0] = RawCache::get().take(limit_, &raw_real_[0]);
     prep_ = std::thread([this] { prepare_loop(); });
     consumer_ = std::thread([this] { consume(); });
   }
-  ~Pipeline() { finish(); }
+  ~Pipeline() {
+    finish();
+    for (int i = 0; i < 2; ++i) RawCache::get().give(std::move(raw_[i]), raw_real_[i]);
+  }
 
   // room for a file of n raw bytes in the current batch (flushing it first
   // if it does not fit); returns where to put it, nullptr on failure
@@ -207,10 +252,13 @@ class Pipeline {
   // a larger current buffer holding its bytes [from, to) at its start
   // (no file committed in it)
   void grow_window(uint64_t cap, uint64_t from, uint64_t to) {
-    std::unique_ptr<uint8_t[]> nb(new uint8_t[cap]);
+    uint64_t real = 0;
+    std::unique_ptr<uint8_t[]> nb = RawCache::get().take(cap, &real);
     if (to > from) std::memcpy(nb.get(), raw_[cur_].get() + from, to - from);
+    RawCache::get().give(std::move(raw_[cur_]), raw_real_[cur_]);
     raw_[cur_] = std::move(nb);
     raw_cap_[cur_] = cap;
+    raw_real_[cur_] = real;
   }
   // the window is full: hand its committed files to the prepare thread and
   // continue in the other buffer with the unconsumed bytes [from, to) of
@@ -223,7 +271,11 @@ class Pipeline {
     }
     const int old = cur_;
     if (!flush()) return false;                 // switches cur_ (the prepare reads [0, from) of `old`)
-    if (raw_cap_[cur_] < keep) { raw_[cur_].reset(new uint8_t[keep]); raw_cap_[cur_] = keep; }
+    if (raw_cap_[cur_] < keep) {
+      RawCache::get().give(std::move(raw_[cur_]), raw_real_[cur_]);
+      raw_[cur_] = RawCache::get().take(keep, &raw_real_[cur_]);
+      raw_cap_[cur_] = keep;
+    }
     if (keep) std::memcpy(raw_[cur_].get(), raw_[old].get() + from, keep);
     return ok();
   }
@@ -247,7 +299,7 @@ class Pipeline {
       // the other buffer is free once its previous batch has been prepared
       cv_.wait(lk, [&] { return !busy_[cur_] || !err_.empty(); });
     }
-    if (!raw_[cur_]) { raw_cap_[cur_] = limit_; raw_[cur_].reset(new uint8_t[limit_]); }
+    if (!raw_[cur_]) { raw_cap_[cur_] = limit_; raw_[cur_] = RawCache::get().take(limit_, &raw_real_[cur_]); }
     flush_wall_ms_ += ms_between(t0, Clock::now());
     return ok();
   }
@@ -380,7 +432,8 @@ class Pipeline {
   FeedOpts fo_;
   BufPool pool_;
   std::unique_ptr<uint8_t[]> raw_[2];
-  uint64_t raw_cap_[2] = {0, 0};
+  uint64_t raw_cap_[2] = {0, 0};           // the size a window / batch may use
+  uint64_t raw_real_[2] = {0, 0};          // the buffer's real size (a cached one may be larger)
   int cur_ = 0;
   bool busy_[2] = {false, false};
   uint64_t limit_ = 0, used_ = 0, peak_batch_ = 0;

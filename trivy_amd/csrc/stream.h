@@ -29,7 +29,7 @@ using StreamReadFn = int64_t (*)(void* user, uint8_t* buf, size_t cap);
 struct StreamOpts {
   FeedOpts feed;
   std::vector<std::string> skip_files, skip_dirs;
-  uint64_t batch_bytes = 512ull << 20;   // raw bytes per batch (a larger file is a batch of its own)
+  uint64_t batch_bytes = 256ull << 20;   // raw bytes per batch (a larger file is a batch of its own); host memory ~4 batches
   int threads = 16;                      // prepare / read threads of the producer
   bool pinned = true;                    // prepared batches in pinned host memory (the GPU engine)
 };
