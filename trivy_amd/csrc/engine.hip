@@ -1938,10 +1938,18 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
   };
   auto worker = [&]() {
     FilePlan plan;
+    // per-thread counts and work taken a few files at a time: 15 threads
+    // hitting shared counters once per file serialised on their cache lines
+    uint64_t my_conf = 0, my_find = 0;
+    constexpr uint32_t kTake = 4;
+    uint32_t wi = 0, wend = 0;
     for (;;) {
-      uint32_t wi = next.fetch_add(1);
-      if (wi >= work.size()) break;
-      uint32_t f = work[wi];
+      if (wi == wend) {
+        wi = next.fetch_add(kTake);
+        if (wi >= work.size()) break;
+        wend = std::min<uint32_t>(wi + kTake, static_cast<uint32_t>(work.size()));
+      }
+      uint32_t f = work[wi++];
       std::string path = in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]);
       const uint8_t* content = in.h_data + in.offsets[f];
       const size_t len = in.offsets[f + 1] - in.offsets[f];
@@ -1950,17 +1958,17 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       if (g.ff[f]) {
         // fold-special file (U+0130/U+212A/U+017F present): the two passes run
         // on the host with the variant scan DFA, then the exact confirmer
-        nconf.fetch_add(1);
+        ++my_conf;
         std::vector<std::vector<uint64_t>> vc;
         std::vector<uint8_t> vg;
         prefilter_variant_file(pf_, content, len, &vc, &vg);
         plan_from_candidates(pf_, &vc, &plan);
         Secret s = scan_file(rs, path, content, len, binary, &plan);
-        nfind.fetch_add(s.findings.size());
+        my_find += s.findings.size();
         results[f] = std::move(s);
         continue;
       }
-      nconf.fetch_add(1);
+      ++my_conf;
       plan.kind = kind0;                       // mode-1 rules kPlanFull, the rest kPlanNoMatch
       plan.cands.clear();
       std::sort(sorted.begin() + cb, sorted.begin() + ce, [](const CandDev& a, const CandDev& b) {
@@ -1998,9 +2006,11 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       nls.file_off = in.offsets[f];
       nls.chunk = g.chunk;
       Secret s = scan_file(rs, path, content, len, binary, &plan, &nls);
-      nfind.fetch_add(s.findings.size());
+      my_find += s.findings.size();
       results[f] = std::move(s);
     }
+    nconf.fetch_add(my_conf);
+    nfind.fetch_add(my_find);
   };
   const int nt = cc.pool->size();
   // while GPU passes are in flight one core stays with each thread driving

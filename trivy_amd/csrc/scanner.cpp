@@ -400,7 +400,8 @@ void find_all_from_candidates(const re::Regexp& re, const uint8_t* text, size_t 
                               const std::vector<uint64_t>& starts, bool submatch,
                               std::vector<re::Cap>* out) {
   const int ncap = 2 * (re.num_subexp() + 1);
-  std::vector<re::Cap> caps(ncap);
+  thread_local std::vector<re::Cap> caps;        // per-thread scratch (no allocation per call)
+  caps.resize(ncap);
   size_t pos = 0;
   long prev_end = -1;
   size_t idx = 0;
@@ -515,7 +516,8 @@ void find_locations(const Ruleset& rs, const Rule& rule, const uint8_t* c, size_
                     const std::vector<uint64_t>* starts, std::vector<Loc>* locs, int* error) {
   if (!rule.regex) return;
   const bool sub = !rule.secret_group_name.empty();
-  std::vector<re::Cap> m;
+  thread_local std::vector<re::Cap> m;           // per-thread scratch
+  m.clear();
   if (starts) find_all_from_candidates(*rule.regex, c, n, *starts, sub, &m);
   else rule.regex->find_all(c, n, sub, &m);
   const size_t stride = sub ? 2 * (rule.regex->num_subexp() + 1) : 2;
