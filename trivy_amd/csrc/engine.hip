@@ -2316,6 +2316,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
   // while the first segment's upload and GPU passes run
   results->clear();
   results->resize(in.nfiles);
+  if (host_profile_) std::fprintf(stderr, "[tsg tl] %u result slots ready at %.3f ms\n", in.nfiles, ms_since(t_feed0));
   uint64_t nconf = 0, nfind = 0;
   double host_ms = 0;
   for (;;) {
