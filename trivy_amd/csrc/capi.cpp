@@ -423,6 +423,12 @@ struct Reaper {
   std::thread th;
   bool stop = false;
   void loop() {
+    // idle priority: the frees of one batch's result overlap the next batch,
+    // whose host confirmation keeps every core of the quota busy (on the
+    // resident path a normal-priority reaper took a core from it)
+    sched_param sp{};
+    sp.sched_priority = 0;
+    pthread_setschedparam(pthread_self(), SCHED_IDLE, &sp);
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
       cv.wait(lk, [&] { return stop || !q.empty(); });
@@ -463,6 +469,7 @@ struct ReaperOwner {
   }
 } g_reaper_owner;
 constexpr size_t kReapInlineFiles = 4096;
+constexpr size_t kReapMaxQueued = 4;
 }  // namespace
 
 void tsg_result_free(tsg_result* r) {
@@ -479,9 +486,19 @@ void tsg_result_free(tsg_result* r) {
   }
   {
     std::lock_guard<std::mutex> lq(g_reaper->mu);
-    g_reaper->q.push_back(r);
+    // backpressure: an idle-priority reaper that never gets a core (a
+    // saturated host) must not let freed results pile up
+    if (g_reaper->q.size() >= kReapMaxQueued) {
+      g_reaper->q.push_back(r);
+      r = g_reaper->q.front();
+      g_reaper->q.pop_front();
+    } else {
+      g_reaper->q.push_back(r);
+      r = nullptr;
+    }
   }
   g_reaper->cv.notify_one();       // under g_reaper_mu: the owner cannot delete the reaper meanwhile
+  delete r;                        // the oldest queued result, inline (nullptr: nothing)
 }
 void tsg_free(void* p) { free(p); }
 
