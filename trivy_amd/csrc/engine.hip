@@ -1963,7 +1963,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         std::vector<uint8_t> vg;
         prefilter_variant_file(pf_, content, len, &vc, &vg);
         plan_from_candidates(pf_, &vc, &plan);
-        Secret s = scan_file(rs, path, content, len, binary, &plan);
+        Secret s = scan_file(rs, std::move(path), content, len, binary, &plan);
         my_find += s.findings.size();
         results[f] = std::move(s);
         continue;
@@ -2005,7 +2005,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       nls.data = in.h_data;
       nls.file_off = in.offsets[f];
       nls.chunk = g.chunk;
-      Secret s = scan_file(rs, path, content, len, binary, &plan, &nls);
+      Secret s = scan_file(rs, std::move(path), content, len, binary, &plan, &nls);
       my_find += s.findings.size();
       results[f] = std::move(s);
     }

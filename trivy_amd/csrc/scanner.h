@@ -194,7 +194,7 @@ std::string go_quote(const std::string& s);
 // 0 keyword gate, 1 find_locations, 2 exclude blocks, 3 censor + findings, 4 sort
 extern std::atomic<bool> g_scan_prof_on;
 extern std::atomic<uint64_t> g_scan_prof[5];
-Secret scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t len,
+Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl = nullptr);
 
 // Exact Go FindAll(Submatch)Index restricted to candidate start offsets.
