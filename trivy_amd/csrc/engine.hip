@@ -1889,10 +1889,21 @@ void Engine::plan_confirm(const Segment& sg, GpuOut* gp) const {
     if (any_full || g.ff[f] || g.per_file[f] != g.per_file[f + 1]) g.work.push_back(f);
     else g.light.push_back(f);
   }
-  std::sort(g.work.begin(), g.work.end(), [&](uint32_t a, uint32_t b) {
-    const uint64_t sa = in.offsets[a + 1] - in.offsets[a], sb = in.offsets[b + 1] - in.offsets[b];
-    return sa != sb ? sa > sb : a < b;
-  });
+  // largest first, by power-of-two size class (a counting sort: a full sort
+  // of config 5's 13k files per piece cost ~1 ms on the confirming thread;
+  // LPT within a factor of two balances the pool as well)
+  {
+    uint32_t cnt[65] = {};
+    auto cls = [&](uint32_t f) {
+      const uint64_t n = in.offsets[f + 1] - in.offsets[f];
+      return 63 - __builtin_clzll(n + 1);           // 0..63
+    };
+    for (uint32_t f : g.work) ++cnt[63 - cls(f) + 1];
+    for (int k = 1; k <= 64; ++k) cnt[k] += cnt[k - 1];
+    std::vector<uint32_t> by(g.work.size());
+    for (uint32_t f : g.work) by[cnt[63 - cls(f)]++] = f;
+    g.work.swap(by);
+  }
   g.planned = true;
 }
 
