@@ -1024,6 +1024,9 @@ def main():
 
     for b in shard_batches:
         b.free()
+    if os.environ.get("TSG_K2_STATS") and sc._engine:
+        L.tsg_engine_destroy(sc._engine)      # prints the per-rule K2 counters
+        sc._engine = None
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

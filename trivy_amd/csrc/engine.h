@@ -5,6 +5,7 @@
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -81,8 +82,10 @@ class Engine {
  private:
   Engine() = default;
   struct Segment;
+  // while_gpu (optional) runs once on the calling thread after the segment's
+  // kernels are queued, before it waits for them
   bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, const uint64_t* d_off_up,
-                   ScanStats* st, GpuOut* out, std::string* err);
+                   ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu = nullptr);
   void plan_confirm(const Segment& sg, GpuOut* g) const;
   void confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* results, uint64_t* nconf,
                        uint64_t* nfind, bool gpu_in_flight);

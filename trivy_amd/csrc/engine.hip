@@ -347,6 +347,10 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
   t.lim = min(end, x.offsets[t.f + 1]);
 }
 
+// TSG_K2_STATS counters per rule: hits, gated hits, verify starts, verify
+// bytes, the most verify bytes of one hit
+constexpr uint32_t kK2Stat = 5;
+
 template <bool kStats>
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     const AnchorDev an = anchors[h & 0xffffffu];
     const RuleDev r = rules[an.rule];
     const uint32_t f = file_of(offsets, nfiles, q);
-    if (kStats) atomicAdd(&k2s[4 * an.rule], 1ull);
+    if (kStats) atomicAdd(&k2s[kK2Stat * an.rule], 1ull);
     if (r.mode == 3) {
       // presence anchor of a rule evaluated in full on the host: the hit is
       // the candidate (any one per file suffices)
@@ -388,9 +392,10 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
       }
       if (!g) continue;
     }
-    if (kStats) atomicAdd(&k2s[4 * an.rule + 1], 1ull);
+    if (kStats) atomicAdd(&k2s[kK2Stat * an.rule + 1], 1ull);
     const long long fstart = static_cast<long long>(offsets[f]);
     const long long fend = static_cast<long long>(offsets[f + 1]);
+    unsigned long long hit_bytes = 0;
     const VDfaDev d = vd[r.verify_dfa];
     const uint16_t* nx = v_next + d.next_off;
     const uint8_t* acc = v_acc + d.acc_off;
@@ -405,19 +410,30 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     };
     // anchored verify DFA from s: does a prefix of the text from s lie in the
     // rule's relaxed language?
+    // the text is read 16 aligned bytes at a time (the batch is 16-byte
+    // aligned with 64 readable bytes past its end): one memory round trip per
+    // 16 steps instead of one per byte next to the table's
     auto verify = [&](long long s) {
       uint32_t st = 0;
       bool ok = acc[0] != 0;
       long long p = s;
       const long long lim = min(fend, s + static_cast<long long>(r.verify_limit));
+      long long wb = -1;
+      v4u win{0, 0, 0, 0};
       for (; !ok && p < lim; ++p) {
-        st = nx[st * d.nclasses + cl[data[p]]];
+        if ((p & ~15ll) != wb) {
+          wb = p & ~15ll;
+          win = *reinterpret_cast<const v4u*>(data + wb);
+        }
+        const uint32_t wd = (p & 8) ? ((p & 4) ? win.w : win.z) : ((p & 4) ? win.y : win.x);
+        st = nx[st * d.nclasses + cl[(wd >> ((p & 3) * 8)) & 0xffu]];
         if (acc[st]) ok = true;
         else if (st == d.dead) break;
       }
       if (kStats) {
-        atomicAdd(&k2s[4 * an.rule + 2], 1ull);
-        atomicAdd(&k2s[4 * an.rule + 3], static_cast<unsigned long long>(p - s + 1));
+        atomicAdd(&k2s[kK2Stat * an.rule + 2], 1ull);
+        atomicAdd(&k2s[kK2Stat * an.rule + 3], static_cast<unsigned long long>(p - s + 1));
+        hit_bytes += static_cast<unsigned long long>(p - s + 1);
       }
       if (!ok && st != d.dead && p < fend && p >= lim) ok = true;   // gave up: conservative
       return ok;
@@ -435,9 +451,11 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
       for (long long p = static_cast<long long>(q); p >= fstart; --p) {
         if (static_cast<long long>(q) - p >= static_cast<long long>(kRevLimit)) { emit(kFullScanStart); break; }
         st = rnx[st * rd.nclasses + rcl[data[p]]];
+        if (kStats) ++hit_bytes;
         if (st == rd.dead) break;
         if (racc[st] && verify(p)) emit(static_cast<unsigned long long>(p - fstart));
       }
+      if (kStats) atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
       continue;
     }
     long long hi = static_cast<long long>(q) + 1 - an.min_len - an.dmin;
@@ -446,6 +464,7 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     for (long long s = lo; s <= hi; ++s) {
       if (verify(s)) emit(static_cast<unsigned long long>(s - fstart));
     }
+    if (kStats) atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
   }
 }
 
@@ -1473,17 +1492,18 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
 Engine::~Engine() {
   if (k2_stats_ && !k2s_.empty()) {
     // TSG_K2_STATS: per-rule K2 work of every scan of this engine, busiest first
-    std::vector<size_t> order(k2s_.size() / 4);
+    std::vector<size_t> order(k2s_.size() / kK2Stat);
     for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return k2s_[4 * a + 3] > k2s_[4 * b + 3]; });
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return k2s_[kK2Stat * a + 3] > k2s_[kK2Stat * b + 3]; });
     std::string js = "{\"k2_stats\": [";
     bool first = true;
     for (size_t i : order) {
-      if (k2s_[4 * i] == 0) continue;
+      if (k2s_[kK2Stat * i] == 0) continue;
       const std::string id = i < rs_->rules.size() ? rs_->rules[i].id : "exclude-" + std::to_string(i - rs_->rules.size());
-      js += std::string(first ? "" : ", ") + "{\"rule\": \"" + id + "\", \"hits\": " + std::to_string(k2s_[4 * i]) +
-            ", \"gated\": " + std::to_string(k2s_[4 * i + 1]) + ", \"starts\": " + std::to_string(k2s_[4 * i + 2]) +
-            ", \"bytes\": " + std::to_string(k2s_[4 * i + 3]) + "}";
+      js += std::string(first ? "" : ", ") + "{\"rule\": \"" + id + "\", \"hits\": " + std::to_string(k2s_[kK2Stat * i]) +
+            ", \"gated\": " + std::to_string(k2s_[kK2Stat * i + 1]) + ", \"starts\": " + std::to_string(k2s_[kK2Stat * i + 2]) +
+            ", \"bytes\": " + std::to_string(k2s_[kK2Stat * i + 3]) + ", \"max_hit_bytes\": " +
+            std::to_string(k2s_[kK2Stat * i + 4]) + "}";
       first = false;
     }
     js += "]}";
@@ -1511,7 +1531,7 @@ Lane* Engine::acquire_lane(DeviceTables& dt, std::string* err) {
   }
   for (auto& ev : l->ev) if (hipEventCreate(&ev) != hipSuccess) { *err = "hipEventCreate failed"; return nullptr; }
   if (k2_stats_) {
-    const size_t n = 4 * std::max<size_t>(pf_.rules.size(), 1) * sizeof(unsigned long long);
+    const size_t n = kK2Stat * std::max<size_t>(pf_.rules.size(), 1) * sizeof(unsigned long long);
     if (hipMalloc(&l->d_k2s, n) != hipSuccess || hipMemset(l->d_k2s, 0, n) != hipSuccess) {
       *err = "K2 stats buffer";
       return nullptr;
@@ -1558,7 +1578,7 @@ void Engine::release_call(CallCtx* cc) {
 // lane's device (resident, or landed by the lane's upload), on the lane's
 // compute stream.  Returns when the segment's results are on the host.
 bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, const uint64_t* d_off_up,
-                         ScanStats* st, GpuOut* out, std::string* err) {
+                         ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu) {
   const BatchInput& in = sg.in;
   HIP_OK(hipSetDevice(dt.device));
   const uint64_t total = in.offsets[in.nfiles];
@@ -1712,6 +1732,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
           !readback(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2, nullptr, 0, s, err) ||
           !readback(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4,
                     s, err)) return false;
+      if (while_gpu && *while_gpu) {
+        (*while_gpu)();
+        while_gpu = nullptr;
+      }
       HIP_OK(hipStreamSynchronize(s));
       const double t_k1_sync = ms_since(t_seg0);
       const uint32_t* h_bh = ln.rb_bh.as<const uint32_t>();
@@ -1751,12 +1775,13 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
                      osub, ms_since(t_d2h), ms_since(t_seg0));
       st->candidates += c2;
       if (ln.d_k2s) {
-        std::vector<unsigned long long> h(4 * pf_.rules.size());
+        std::vector<unsigned long long> h(kK2Stat * pf_.rules.size());
         HIP_OK(hipMemcpy(h.data(), ln.d_k2s, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         HIP_OK(hipMemset(ln.d_k2s, 0, h.size() * sizeof(unsigned long long)));
         std::lock_guard<std::mutex> lk(k2s_mu_);
         if (k2s_.size() < h.size()) k2s_.resize(h.size(), 0);
-        for (size_t i = 0; i < h.size(); ++i) k2s_[i] += h[i];
+        for (size_t i = 0; i < h.size(); ++i)
+          k2s_[i] = i % kK2Stat == 4 ? std::max(k2s_[i], h[i]) : k2s_[i] + h[i];
       }
       return true;
     }
@@ -1949,6 +1974,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
   };
   auto worker = [&]() {
     FilePlan plan;
+    std::vector<std::vector<uint64_t>> spare;
     // per-thread counts and work taken a few files at a time: 15 threads
     // hitting shared counters once per file serialised on their cache lines
     uint64_t my_conf = 0, my_find = 0;
@@ -1981,6 +2007,10 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       }
       ++my_conf;
       plan.kind = kind0;                       // mode-1 rules kPlanFull, the rest kPlanNoMatch
+      for (RuleCandidates& c : plan.cands) {   // start lists are reused from file to file
+        c.starts.clear();
+        spare.push_back(std::move(c.starts));
+      }
       plan.cands.clear();
       std::sort(sorted.begin() + cb, sorted.begin() + ce, [](const CandDev& a, const CandDev& b) {
         return a.rule != b.rule ? a.rule < b.rule : a.start < b.start;
@@ -1989,6 +2019,10 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         uint32_t r = sorted[k].rule;
         RuleCandidates rc;
         rc.rule = r;
+        if (!spare.empty()) {
+          rc.starts = std::move(spare.back());
+          spare.pop_back();
+        }
         while (k < ce && sorted[k].rule == r) {
           if (rc.starts.empty() || rc.starts.back() != sorted[k].start) rc.starts.push_back(sorted[k].start);
           ++k;
@@ -2221,6 +2255,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
   double gpu_busy = 0;
   auto t_feed0 = std::chrono::steady_clock::now();
   std::atomic<int64_t> feed_end_ns{0};
+  std::atomic<bool> confirmer_idle{true};
   auto driver = [&](DeviceTables* dt) {
     std::string e;
     ScanStats dst;
@@ -2257,6 +2292,17 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       HIP_OK(hipEventRecord(ln->up_done[slot], ln->copy));
       return true;
     };
+    // a finished segment is handed to the confirmer once this thread has
+    // queued the next segment's kernels and planned its confirmation
+    // (plan_confirm) while they run: the confirming pool never waits on the
+    // plan of a segment whose successor is on the GPU
+    // (an idle confirmer gets the segment at once and plans it itself)
+    std::unique_ptr<Job> pending;
+    const std::function<void()> plan_pending = [&]() {
+      if (!pending) return;
+      if (!confirmer_idle.load(std::memory_order_acquire)) plan_confirm(segs[pending->seg], &pending->out);
+      q.push(std::move(pending));
+    };
     size_t cur = ok ? next_seg.fetch_add(1) : segs.size();
     int slot = 0;
     if (ok && host_profile_) hipEventRecord(ln->anchor, resident ? ln->compute : ln->copy);
@@ -2280,8 +2326,10 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       job->seg = cur;
       ScanStats sst;
       const double h_start = ms_since(t_feed0);
-      ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e);
+      ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e,
+                       &plan_pending);
       if (!ok) break;
+      plan_pending();                    // (a rerun path may not have called it)
       if (host_profile_) {
         // GPU timeline of this segment from the scan's anchor event
         float ub = 0, ud = 0, k1a = 0, k1b = 0, k2b = 0;
@@ -2303,10 +2351,11 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
         while (ns > prev && !feed_end_ns.compare_exchange_weak(prev, ns)) {}
       }
       add_stats(&dst, sst);
-      q.push(std::move(job));
+      pending = std::move(job);
       cur = nxt;
       slot ^= 1;
     }
+    if (ok) plan_pending();
     if (ln) {
       if (!ok) { hipStreamSynchronize(ln->copy); hipStreamSynchronize(ln->compute); }
       release_lane(*dt, ln);
@@ -2332,7 +2381,9 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
   double host_ms = 0;
   for (;;) {
     int left = 0;
+    confirmer_idle.store(true, std::memory_order_release);
     std::unique_ptr<Job> job = q.pop(&left);
+    confirmer_idle.store(false, std::memory_order_release);
     if (!job) break;
     auto th = std::chrono::steady_clock::now();
     const Segment& sg = segs[job->seg];

@@ -24,7 +24,11 @@ constexpr int kMaxUnits = 6;             // literal length cap (units): longer a
 constexpr uint32_t kMaxPrefixBytes = 96; // dmax cap for a usable anchor
 constexpr uint32_t kVerifyStateCap = 3000;
 constexpr uint32_t kScanStateCap = 60000;
-constexpr uint32_t kVerifyLimitCap = 8192;
+// K2 gives up on a verify walk after this many bytes and passes the start on
+// (the host decides it exactly): one thread walking an exclude block's
+// `.*?END NOSCAN` over 8 KiB held a 3 GB config-5 piece's K2 for 2.4 ms
+// (profiles/rd4z_bench_c5k2.log, max_hit_bytes 8193)
+constexpr uint32_t kVerifyLimitCap = 1024;
 constexpr double kWeakAnchor = 3.0;
 constexpr size_t kHostKeywordLen = 3;     // keywords this short gate on the host      // literal anchors scoring below this get class extensions
 

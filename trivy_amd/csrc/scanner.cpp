@@ -560,13 +560,20 @@ uint64_t count_newlines(const uint8_t* p, size_t n) {
 // overwritten by '*'), represented virtually: original bytes + merged spans.
 class CensoredView {
  public:
-  CensoredView(const uint8_t* c, size_t n, std::vector<Loc> spans, const NlSource* nl) : c_(c), n_(n) {
+  // `spans` is merged in place and kept as the view's span list; `scratch`
+  // holds the newline prefix (both the caller's per-thread buffers: no
+  // allocation per confirmed file)
+  CensoredView(const uint8_t* c, size_t n, std::vector<Loc>& spans, std::vector<uint64_t>& scratch, const NlSource* nl)
+      : c_(c), n_(n), iv_(spans), local_(scratch) {
     std::sort(spans.begin(), spans.end(), [](const Loc& a, const Loc& b) { return a.start < b.start; });
-    for (const Loc& l : spans) {
+    size_t m = 0;
+    for (size_t i = 0; i < spans.size(); ++i) {
+      const Loc l = spans[i];
       if (l.end <= l.start) continue;
-      if (!iv_.empty() && l.start <= iv_.back().end) iv_.back().end = std::max(iv_.back().end, l.end);
-      else iv_.push_back(l);
+      if (m > 0 && l.start <= spans[m - 1].end) spans[m - 1].end = std::max(spans[m - 1].end, l.end);
+      else spans[m++] = l;
     }
+    spans.resize(m);
     if (nl && nl->chunk_nl) {
       // local prefix over the batch chunks this file touches
       ch_ = nl->chunk;
@@ -655,8 +662,8 @@ class CensoredView {
  private:
   const uint8_t* c_;
   size_t n_;
-  std::vector<Loc> iv_;
-  mutable std::vector<uint64_t> local_;   // local_[k] = '\n' in data_[first_*ch_, (first_+k)*ch_)
+  const std::vector<Loc>& iv_;
+  std::vector<uint64_t>& local_;          // local_[k] = '\n' in data_[first_*ch_, (first_+k)*ch_)
   const uint16_t* chunk_nl_ = nullptr;      // per-chunk counts (K1's), summed into local_ on demand
   const uint8_t* data_ = nullptr;
   uint64_t off_ = 0, first_ = 0;
@@ -841,6 +848,10 @@ bool keywords_match_raw(const Rule& r, const uint8_t* content, size_t len, Lower
 }  // namespace
 
 std::atomic<bool> g_scan_prof_on{false};
+
+namespace {
+struct Matched { const Rule* rule; Loc loc; };
+}  // namespace
 std::atomic<uint64_t> g_scan_prof[5];
 
 namespace {
@@ -872,10 +883,14 @@ Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, si
     return lower;
   };
   Blocks gblocks(content, len, rs.exclude_block, plan, rs.rules.size());
-  struct M { const Rule* rule; Loc loc; };
-  std::vector<M> matched;
+  // per-thread working vectors (kept across files: no allocation per file)
+  thread_local std::vector<Matched> matched_tl;
+  thread_local std::vector<Loc> locs_tl, spans_tl;
+  thread_local std::vector<uint64_t> nl_tl;
+  std::vector<Matched>& matched = matched_tl;
+  std::vector<Loc>& locs = locs_tl;
+  matched.clear();
   size_t cand_i = 0;
-  std::vector<Loc> locs;
   const bool listed = plan && plan->active_set;
   const size_t niter = listed ? plan->active.size() : rs.rules.size();
   for (size_t it = 0; it < niter; ++it) {
@@ -915,9 +930,10 @@ Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, si
     pc.lap(2);
   }
   if (matched.empty()) return out;                    // types.Secret{}
-  std::vector<Loc> spans;
+  std::vector<Loc>& spans = spans_tl;
+  spans.clear();
   for (const auto& m : matched) spans.push_back(m.loc);
-  CensoredView cv(content, len, std::move(spans), nl);
+  CensoredView cv(content, len, spans, nl_tl, nl);
   out.findings.reserve(matched.size());
   out.lines.reserve(matched.size() * 5);
   out.arena.reserve(matched.size() * 640);        // match line + up to 5 code lines of <= 100 bytes
