@@ -41,6 +41,7 @@ struct DeviceTables;
 struct Lane;
 struct GpuOut;
 struct CallCtx;
+struct K1Chain;
 
 // One engine = the compiled ruleset's device tables on every selected device.
 // scan() is reentrant: each call takes its own lane (HIP streams + scratch
@@ -83,9 +84,11 @@ class Engine {
   Engine() = default;
   struct Segment;
   // while_gpu (optional) runs once on the calling thread after the segment's
-  // kernels are queued, before it waits for them
+  // kernels are queued, before it waits for them; chain (optional) orders
+  // the K1 launches of several drivers of one device (K1Chain)
   bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, const uint64_t* d_off_up,
-                   ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu = nullptr);
+                   ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu = nullptr,
+                   K1Chain* chain = nullptr);
   void plan_confirm(const Segment& sg, GpuOut* g) const;
   void confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* results, uint64_t* nconf,
                        uint64_t* nfind, bool gpu_in_flight);
@@ -109,6 +112,10 @@ class Engine {
   // valid); the other bits are measurement builds whose results are invalid.
   int k1_abl_ = 464;
   uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
+  // drivers per device for resident batches (TSG_RESIDENT_DRIVERS; 2 =
+  // K1Chain: measured no gain, config 2 1530 vs 1528 GB/s, config 3 766 vs
+  // 803 -- the second driver's launch lands behind the first's next segment)
+  int resident_drivers_ = 1;
   uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
   bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
   bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr

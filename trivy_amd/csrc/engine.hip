@@ -1078,10 +1078,24 @@ bool readback(const void* src, const PinnedBuf& b, size_t nwords, const uint32_t
   return true;
 }
 
+// Two drivers of one device (resident batches): each queues its segment's
+// K1 + K2 behind the other's last K2 (the event below), so the device runs
+// the segments' passes back to back -- a K1 takes every CU's LDS, a K2
+// launched beside it would wait for it -- while the other driver's readback,
+// copy-out and launch overhead overlap them instead of leaving the device
+// idle between segments (0.17-0.21 ms per piece, profiles/rd5c_bench_c2prof.log).
+// Drivers in this mode poll their event between short sleeps (no spinning
+// core taken from the confirm pool).
+struct K1Chain {
+  std::mutex mu;
+  hipEvent_t last = nullptr;                    // end of the last K2 queued on the device
+};
+
 struct Lane {
   int device = 0;
   hipStream_t compute = nullptr, copy = nullptr;
   hipEvent_t ev[4] = {};                        // K1 start/end, K2 start/end (compute stream)
+  hipEvent_t ev_sync = nullptr;                 // blocking-sync event (K1Chain drivers)
   hipEvent_t up_begin[2] = {}, up_done[2] = {}; // upload ring slot: H2D start / done (copy stream)
   hipEvent_t anchor = nullptr;                   // TSG_HOST_PROFILE: start of a scan() on the copy stream
   uint8_t* ring[2] = {nullptr, nullptr};
@@ -1172,6 +1186,7 @@ Lane::~Lane() {
   void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s, d_cr};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
+  if (ev_sync) hipEventDestroy(ev_sync);
   if (anchor) hipEventDestroy(anchor);
   for (int i = 0; i < 2; ++i) {
     if (up_begin[i]) hipEventDestroy(up_begin[i]);
@@ -1463,6 +1478,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   }
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // K1 measurement builds (kAbl bits)
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
   if (e->host_profile_) g_scan_prof_on.store(true, std::memory_order_relaxed);
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
@@ -1578,7 +1594,8 @@ void Engine::release_call(CallCtx* cc) {
 // lane's device (resident, or landed by the lane's upload), on the lane's
 // compute stream.  Returns when the segment's results are on the host.
 bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, const uint64_t* d_off_up,
-                         ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu) {
+                         ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu,
+                         K1Chain* chain) {
   const BatchInput& in = sg.in;
   HIP_OK(hipSetDevice(dt.device));
   const uint64_t total = in.offsets[in.nfiles];
@@ -1651,6 +1668,11 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       if (!g.in_lds || lds_of(g) > kLdsBytes) { *err = "K1 LDS budget exceeded"; return false; }
       HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_of(g))));
     }
+    std::unique_lock<std::mutex> chain_lk;
+    if (chain && attempt == 0) {
+      chain_lk = std::unique_lock<std::mutex>(chain->mu);
+      if (chain->last) HIP_OK(hipStreamWaitEvent(s, chain->last, 0));
+    }
     HIP_OK(hipEventRecord(ln.ev[0], s));
     uint32_t launches = 0;
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
@@ -1719,6 +1741,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       }
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));
+      if (chain_lk.owns_lock()) {            // the other driver's next K1 follows this K2
+        chain->last = ln.ev[3];
+        chain_lk.unlock();
+      }
       // everything to the host in one round trip: per-region hit counts, the
       // counters (candidates, overflow hits, LDS check), file flags, newline
       // counts and the candidates (as many as fit)
@@ -1736,7 +1762,20 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
         (*while_gpu)();
         while_gpu = nullptr;
       }
-      HIP_OK(hipStreamSynchronize(s));
+      if (chain) {
+        // polled with short sleeps: a blocking-sync event woke its driver
+        // 0.3-1.2 ms after the passes ended (profiles/rd5e_bench_c2prof.log)
+        if (!ln.ev_sync) HIP_OK(hipEventCreateWithFlags(&ln.ev_sync, hipEventDisableTiming));
+        HIP_OK(hipEventRecord(ln.ev_sync, s));
+        for (;;) {
+          const hipError_t q = hipEventQuery(ln.ev_sync);
+          if (q == hipSuccess) break;
+          if (q != hipErrorNotReady) HIP_OK(q);
+          std::this_thread::sleep_for(std::chrono::microseconds(10));
+        }
+      } else {
+        HIP_OK(hipStreamSynchronize(s));
+      }
       const double t_k1_sync = ms_since(t_seg0);
       const uint32_t* h_bh = ln.rb_bh.as<const uint32_t>();
       const uint32_t* h_cnt = ln.rb_c2.as<const uint32_t>();
@@ -2237,6 +2276,11 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       }
     }
   }
+  // resident batches of several pieces: two drivers on the device (K1Chain)
+  const bool dual = resident && segs.size() >= 2 && resident_drivers_ >= 2;
+  K1Chain chain;
+  K1Chain* chain_p = dual ? &chain : nullptr;
+  if (dual) drivers.push_back(drivers[0]);
   uint64_t max_seg = 0;
   size_t max_seg_files = 0;
   for (const Segment& sg : segs) {
@@ -2308,7 +2352,9 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     if (ok && host_profile_) hipEventRecord(ln->anchor, resident ? ln->compute : ln->copy);
     if (ok && cur < segs.size() && !resident) ok = upload(cur, slot);
     while (ok && cur < segs.size() && !q.aborted()) {
-      const size_t nxt = next_seg.fetch_add(1);
+      // (resident data: the next segment is taken when this one is done, so
+      // two drivers take them in order)
+      const size_t nxt = resident ? segs.size() : next_seg.fetch_add(1);
       // the next segment's upload goes behind this one's on the copy stream;
       // its ring slot was last read by the segment before this one, whose
       // kernels have completed (run_segment returns after its D2H)
@@ -2327,7 +2373,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       ScanStats sst;
       const double h_start = ms_since(t_feed0);
       ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e,
-                       &plan_pending);
+                       &plan_pending, chain_p);
       if (!ok) break;
       plan_pending();                    // (a rerun path may not have called it)
       if (host_profile_) {
@@ -2352,7 +2398,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       }
       add_stats(&dst, sst);
       pending = std::move(job);
-      cur = nxt;
+      cur = resident ? next_seg.fetch_add(1) : nxt;
       slot ^= 1;
     }
     if (ok) plan_pending();
@@ -2363,7 +2409,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     {
       std::lock_guard<std::mutex> lk(st_mu);
       add_stats(st, dst);
-      gpu_busy += ms_since(tb);
+      gpu_busy = dual ? std::max(gpu_busy, ms_since(tb)) : gpu_busy + ms_since(tb);
       if (!ok && drv_err.empty()) drv_err = e.empty() ? "device driver failed" : e;
     }
     if (!ok) q.abort();
@@ -2388,7 +2434,8 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     auto th = std::chrono::steady_clock::now();
     const Segment& sg = segs[job->seg];
     const double c_start = host_profile_ ? ms_since(t_feed0) : 0.0;
-    confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0);
+    // (drivers that block on an event leave every core to the pool)
+    confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0 && !dual);
     host_ms += ms_since(th);
     if (host_profile_) std::fprintf(stderr, "[tsg tl] seg %zu confirm %.3f-%.3f ms\n", job->seg, c_start, ms_since(t_feed0));
   }
