@@ -84,11 +84,12 @@ class Engine {
   Engine() = default;
   struct Segment;
   // while_gpu (optional) runs once on the calling thread after the segment's
-  // kernels are queued, before it waits for them; chain (optional) orders
-  // the K1 launches of several drivers of one device (K1Chain)
+  // kernels are queued, before their readbacks are; chain (optional) orders
+  // the K1 launches of several drivers of one device (K1Chain); defer_copy
+  // leaves the readback in the lane's pinned buffers (GpuOut::finish_copy)
   bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, const uint64_t* d_off_up,
                    ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu = nullptr,
-                   K1Chain* chain = nullptr);
+                   K1Chain* chain = nullptr, bool defer_copy = false);
   void plan_confirm(const Segment& sg, GpuOut* g) const;
   void confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* results, uint64_t* nconf,
                        uint64_t* nfind, bool gpu_in_flight);

@@ -1135,10 +1135,26 @@ struct GpuOut {
   std::vector<uint16_t> nl;     // '\n' count per K1 chunk
   std::vector<uint32_t> ff;     // per-file flags (fold-special content)
   uint32_t chunk = 0;           // K1 chunk bytes of this segment (nl[] granularity)
+  // deferred copy-out (run_segment with defer_copy): the three arrays are
+  // still in the lane's pinned readback buffers; finish_copy() moves them
+  // here before the lane's next readback is queued
+  const CandDev* rb_cands = nullptr;
+  const uint32_t* rb_ff = nullptr;
+  const uint16_t* rb_nl = nullptr;
+  size_t n_cands = 0, n_ff = 0, n_nl = 0;
+  bool deferred = false;
+  void finish_copy() {
+    if (!deferred) return;
+    cands.assign(rb_cands, rb_cands + n_cands);
+    ff.assign(rb_ff, rb_ff + n_ff);
+    nl.assign(rb_nl, rb_nl + n_nl);
+    deferred = false;
+  }
   // the confirmation's plan (plan_confirm): candidates grouped per file, the
   // files to confirm (largest first) and the rest.  (Built on the driver
   // thread it delayed the next piece's launch by as much as it saved the
-  // confirming thread: profiles/rd4q_bench_c3prof.log.)
+  // confirming thread: profiles/rd4q_bench_c3prof.log; it is now built while
+  // the next piece's passes run.)
   bool planned = false;
   std::vector<uint32_t> per_file, work, light;
   std::vector<CandDev> sorted;
@@ -1595,7 +1611,7 @@ void Engine::release_call(CallCtx* cc) {
 // compute stream.  Returns when the segment's results are on the host.
 bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, const uint64_t* d_off_up,
                          ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu,
-                         K1Chain* chain) {
+                         K1Chain* chain, bool defer_copy) {
   const BatchInput& in = sg.in;
   HIP_OK(hipSetDevice(dt.device));
   const uint64_t total = in.offsets[in.nfiles];
@@ -1745,6 +1761,12 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
         chain->last = ln.ev[3];
         chain_lk.unlock();
       }
+      // (before this segment's readbacks are queued: the callback may copy
+      // the lane's previous segment out of the readback buffers)
+      if (while_gpu && *while_gpu) {
+        (*while_gpu)();
+        while_gpu = nullptr;
+      }
       // everything to the host in one round trip: per-region hit counts, the
       // counters (candidates, overflow hits, LDS check), file flags, newline
       // counts and the candidates (as many as fit)
@@ -1758,10 +1780,6 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
           !readback(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2, nullptr, 0, s, err) ||
           !readback(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4,
                     s, err)) return false;
-      if (while_gpu && *while_gpu) {
-        (*while_gpu)();
-        while_gpu = nullptr;
-      }
       if (chain) {
         // polled with short sleeps: a blocking-sync event woke its driver
         // 0.3-1.2 ms after the passes ended (profiles/rd5e_bench_c2prof.log)
@@ -1804,9 +1822,14 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       ln.k2_over_est = nover;
       st->hits += nhits;
       auto t_d2h = std::chrono::steady_clock::now();
-      out->cands.assign(ln.rb_cands.as<CandDev>(), ln.rb_cands.as<CandDev>() + c2);
-      out->ff.assign(ln.rb_ff.as<uint32_t>(), ln.rb_ff.as<uint32_t>() + in.nfiles);
-      out->nl.assign(ln.rb_nl.as<uint16_t>(), ln.rb_nl.as<uint16_t>() + nchunks);
+      out->rb_cands = ln.rb_cands.as<CandDev>();
+      out->rb_ff = ln.rb_ff.as<uint32_t>();
+      out->rb_nl = ln.rb_nl.as<uint16_t>();
+      out->n_cands = c2;
+      out->n_ff = in.nfiles;
+      out->n_nl = nchunks;
+      out->deferred = true;
+      if (!defer_copy) out->finish_copy();
       st->d2h_ms += ms_since(t_d2h);
       if (host_profile_)
         std::fprintf(stderr, "[tsg seg] %.1f MB %u files: wall to results %.3f ms (K1 %.3f, K2 %.3f, K2 grid %u+%u), "
@@ -2344,6 +2367,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     std::unique_ptr<Job> pending;
     const std::function<void()> plan_pending = [&]() {
       if (!pending) return;
+      pending->out.finish_copy();
       if (!confirmer_idle.load(std::memory_order_acquire)) plan_confirm(segs[pending->seg], &pending->out);
       q.push(std::move(pending));
     };
@@ -2373,7 +2397,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       ScanStats sst;
       const double h_start = ms_since(t_feed0);
       ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e,
-                       &plan_pending, chain_p);
+                       &plan_pending, chain_p, /*defer_copy=*/true);
       if (!ok) break;
       plan_pending();                    // (a rerun path may not have called it)
       if (host_profile_) {
