@@ -22,6 +22,10 @@
  *   tsg_result_*            types.Secret / SecretFinding / Code / Line
  *                           pkg/fanal/types/secret.go:5-20, misconf.go:48-61
  *
+ * Test, measurement and tooling hooks (CPU models of the GPU passes, probes of
+ * single components, fault injection) are declared in trivy_secret_test.h;
+ * the same library exports them, and no product entry point calls them.
+ *
  * Conventions
  *   - status: 0 = OK, negative = error; tsg_last_error() returns a
  *     thread-local message for the last failing call on this thread.
@@ -117,9 +121,6 @@ const char* tsg_builtin_rules_json(void);
  * []iacRules.Check{Name: rule ID, Description: rule title} for the builtin
  * rules (NUL-terminated, static). */
 const char* tsg_secret_rules_metadata_json(void);
-/* Test hook: Go encoding/json string encoding of s (json.Marshal; with
- * escape_html = 0 as an Encoder with SetEscapeHTML(false)).  Free with tsg_free. */
-int tsg_go_json_string(const uint8_t* s, size_t n, int escape_html, char** out, size_t* len);
 
 int tsg_device_count(void);
 /* device_mask: bit d selects HIP device d (0 = every visible device).  With
@@ -153,10 +154,6 @@ int tsg_scan_batch(tsg_engine* e, const uint8_t* data, const uint64_t* offsets, 
 int tsg_scan_batch_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data,
                             const uint64_t* offsets, uint32_t nfiles, const char* const* paths,
                             const uint32_t* path_lens, const uint8_t* binary, tsg_result** out);
-/* Run only the two GPU passes; the result carries stats and candidates but no
- * findings (used to time the kernels in isolation). */
-int tsg_prefilter_resident(tsg_engine* e, const void* d_data, const uint8_t* h_data,
-                           const uint64_t* offsets, uint32_t nfiles, tsg_result** out);
 
 /* Host-feed ceiling: stream `bytes` of host memory (pinned for full rate) to
  * HBM through the engine's upload path in segments, with no kernels; *ms =
@@ -190,50 +187,11 @@ int tsg_result_file_error(const tsg_result* r, uint32_t file);
  * UTF-8 bytes are written as \udcXX escapes.  Free with tsg_free. */
 int tsg_result_json(const tsg_result* r, char** json, size_t* len);
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
-/* Raw GPU candidates of file i for rule j (sorted starts); for tests. */
-int tsg_result_candidates(const tsg_result* r, uint32_t file, uint32_t rule, const uint64_t** starts, size_t* n);
 /* Frees a result; one of >= 4096 files + findings is handed to a background
    thread (its memory returns shortly after the call). */
 void tsg_result_free(tsg_result* r);
 void tsg_free(void* p);
 
-/* Host exact confirmer evaluated on every (file, rule) pair with no GPU
- * prefilter (the reference algorithm restated in C++).  For tests of the
- * confirmer; never used by tsg_scan_batch. */
-int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
-                            uint32_t nfiles, const char* const* paths, const uint32_t* path_lens,
-                            const uint8_t* binary, int threads, tsg_result** out);
-/* CPU model of the GPU tables (K1+K2 semantics) feeding the confirmer; for
- * tests of the compiled prefilter without a GPU.  Never used by tsg_scan_batch. */
-int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
-                         uint32_t nfiles, const char* const* paths, const uint32_t* path_lens,
-                         const uint8_t* binary, tsg_result** out);
-/* Prefilter compile report without a GPU (NUL-terminated; free with tsg_free). */
-int tsg_prefilter_report(const tsg_ruleset* rs, char** out);
-/* Tooling (no reference analogue): scan DFA `group` as compiled for K1 --
- * next[state * nclasses + class] (state ids), byte -> class map (256 bytes),
- * states >= first_out have outputs.  Both arrays are freed with tsg_free. */
-int tsg_scan_dfa_dump(const tsg_ruleset* rs, uint32_t group, uint16_t** next, uint8_t** byte_class,
-                      uint32_t* nstates, uint32_t* nclasses, uint32_t* first_out);
-/* Test hook for the host regexp engine: compiles `pattern` (Go syntax) and,
- * for each of the n positions, writes the end of the leftmost-first match
- * anchored there (-1: none) as computed by the lazy DFA (dfa_end) and by
- * match_at's anchored path (vm_end: the bit-state backtracker where Go would
- * use it, else the Pike VM); fails with TSG_ERR_INTERNAL if the scanner's own
- * match_end (span shape / backtracker / lazy DFA) differs from vm_end.  Never
- * used by tsg_scan_batch. */
-int tsg_regex_probe(const char* pattern, const uint8_t* text, size_t len, const uint64_t* pos, size_t n,
-                    int64_t* dfa_end, int64_t* vm_end);
-/* Test hook for the Go sort.Slice restatement (gosort.h, pdqsort_func of
- * go1.23 sort/zsortfunc.go as scanner.go:452-457 uses it): order[] = 0..n-1
- * sorted by keys[order[i]] < keys[order[j]] -- unstable, so ties keep Go's
- * order only if the algorithm is Go's.  Never used by tsg_scan_batch. */
-int tsg_test_go_sort(const uint32_t* keys, size_t n, uint32_t* order);
-/* Test hook for the engine's readback kernel (tsg_readback, engine.hip) on
- * HIP device 0: copies min(nwords, count * per_count) dwords (the product in
- * 64 bits) of a device buffer filled with 1, 2, ... into host-mapped memory;
- * *copied = the dwords that arrived.  Never used by tsg_scan_batch. */
-int tsg_test_readback(uint32_t nwords, uint32_t count, uint32_t per_count, uint32_t* copied);
 
 /* ---- host feed ----
  * Batched SecretAnalyzer.Required + Analyze content preparation, replacing the
@@ -338,12 +296,6 @@ int tsg_scan_layer_stream(tsg_engine* e, tsg_read_fn read, void* user, const tsg
  * next is read.  ScanArgs.FilePath = the path relative to the root. */
 int tsg_scan_fs_tree(tsg_engine* e, const char* root, const tsg_feed_opts* opts, uint64_t batch_bytes,
                      tsg_result** out);
-/* The same two pipelines with the CPU model of the GPU passes as the scan
- * stage (tsg_scan_table_model's); tests only, never the product path. */
-int tsg_scan_layer_stream_model(const tsg_ruleset* rs, tsg_read_fn read, void* user, const tsg_feed_opts* opts,
-                                uint64_t batch_bytes, tsg_result** out);
-int tsg_scan_fs_tree_model(const tsg_ruleset* rs, const char* root, const tsg_feed_opts* opts, uint64_t batch_bytes,
-                           tsg_result** out);
 /* A streamed result's walk: {"files": [every regular file handed to the
  * analyzers], "opq_dirs": [...], "wh_files": [...], "stats": {wall_ms,
  * feed_ms, scan_ms, wait_ms, walked_bytes, read_bytes, scanned_bytes,
@@ -366,19 +318,7 @@ void tsg_queue_destroy(tsg_queue* q);
 int tsg_queue_scan(tsg_queue* q, const char* path, size_t path_len, const uint8_t* content, size_t len, int binary,
                    tsg_result** out);
 int tsg_queue_stats(tsg_queue* q, uint64_t* calls, uint64_t* batches, uint64_t* files, uint32_t* max_batch);
-/* Measurement hook: `callers` threads, each calling tsg_queue_scan on the
- * next not yet scanned file of the batch until all nfiles are done (the
- * reference's goroutines calling Scan per file); *seconds = wall time,
- * *findings = findings over all files.  Never used by tsg_scan_batch. */
-int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
-                    const char* const* paths, const uint32_t* path_lens, uint32_t callers, double* seconds,
-                    uint64_t* findings);
 
-/* Test hook: Regexp.MatchString(text) for `pattern` with the required-literal
- * gate the ruleset compiler sets on path / allow regexes (*gated) and without
- * it (*plain); *has_gate = 1 if a gate was found (2: bounded). */
-int tsg_regex_match_probe(const char* pattern, const uint8_t* text, size_t len, int* gated, int* plain,
-                          int* has_gate);
 
 /* ---- report and image semantics ---- */
 typedef struct tsg_layer {          /* ftypes.Layer, pkg/fanal/types/artifact.go:75-79 */
@@ -419,12 +359,6 @@ int tsg_image_config_content(const char* config_json, size_t config_len, char** 
  * the base image, whose layers are analysed without the secret analyzer. */
 int tsg_guess_base_layers(const char* config_json, size_t config_len, const char* const* diff_ids, uint32_t n,
                           uint8_t* is_base);
-/* Test hook: a result holding the JSON array of types.Secret given (Go field
- * names), to check report assembly against the reference's types.Secret
- * fixtures.  Never used by a scan. */
-int tsg_result_from_json(const char* json, size_t len, tsg_result** out);
-/* Test hook: time.Time JSON round trip (RFC 3339 in, MarshalJSON's form out). */
-int tsg_go_time_rfc3339(const char* in, char* out, size_t cap);
 
 /* ---- client/server wire format ---- */
 /* proto.Marshal of the trivy.common.Secret message (rpc/common/service.proto:

@@ -5,13 +5,27 @@ import re
 
 from trivy_amd import _lib
 
-HDR = os.path.join(os.path.dirname(__file__), "..", "include", "trivy_secret.h")
+INC = os.path.join(os.path.dirname(__file__), "..", "include")
+HDR = os.path.join(INC, "trivy_secret.h")             # the product C-ABI
+TEST_HDR = os.path.join(INC, "trivy_secret_test.h")   # test / measurement / tooling hooks
 
 
-def declared_functions():
-    text = open(HDR).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(tsg_[a-z0-9_]+)\s*\(", text)))
+def declared_functions(paths=(HDR, TEST_HDR)):
+    names = set()
+    for p in paths:
+        text = open(p).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names.update(re.findall(r"\b(tsg_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
+
+
+def test_product_header_holds_no_test_hooks():
+    product = declared_functions((HDR,))
+    hooks = declared_functions((TEST_HDR,))
+    assert not set(product) & set(hooks)
+    for n in ("tsg_scan_host_reference", "tsg_scan_table_model", "tsg_test_go_sort", "tsg_test_readback",
+              "tsg_regex_probe", "tsg_queue_create_model"):
+        assert n in hooks and n not in product
 
 
 def test_library_exports_every_declared_symbol():

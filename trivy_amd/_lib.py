@@ -148,6 +148,9 @@ SIGNATURES += [
     ("tsg_queue_probe", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                        c_char_pp, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_uint64)]),
+    ("tsg_queue_create_model", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    ("tsg_queue_timeouts", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
 ]
 
 

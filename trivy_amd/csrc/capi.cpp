@@ -1,6 +1,7 @@
 // C-ABI (include/trivy_secret.h) over the ruleset, the GPU engine and the
 // host confirmer.
 #include "../../include/trivy_secret.h"
+#include "../../include/trivy_secret_test.h"
 
 #include <algorithm>
 #include <atomic>
@@ -18,6 +19,7 @@
 
 #include "engine.h"
 #include "gosort.h"
+#include "guard.h"
 #include "feed.h"
 #include "tar.h"
 #include "prefilter.h"
@@ -477,28 +479,31 @@ void tsg_result_free(tsg_result* r) {
   size_t weight = r->files.size();
   for (size_t i = 0; i < r->files.size() && weight < kReapInlineFiles; ++i) weight += r->files[i].findings.size();
   if (weight < kReapInlineFiles) { delete r; return; }
-  std::lock_guard<std::mutex> lk(g_reaper_mu);
-  if (g_reaper_closed) { delete r; return; }
-  if (!g_reaper) {
-    Reaper* rp = new Reaper();
-    rp->th = std::thread([rp] { rp->loop(); });
-    g_reaper = rp;
-  }
   {
-    std::lock_guard<std::mutex> lq(g_reaper->mu);
-    // backpressure: an idle-priority reaper that never gets a core (a
-    // saturated host) must not let freed results pile up
-    if (g_reaper->q.size() >= kReapMaxQueued) {
-      g_reaper->q.push_back(r);
-      r = g_reaper->q.front();
-      g_reaper->q.pop_front();
-    } else {
-      g_reaper->q.push_back(r);
-      r = nullptr;
+    std::lock_guard<std::mutex> lk(g_reaper_mu);
+    if (!g_reaper_closed) {
+      try {
+        if (!g_reaper) {
+          std::unique_ptr<Reaper> rp(new Reaper());
+          Reaper* raw = rp.get();
+          rp->th = std::thread([raw] { raw->loop(); });
+          g_reaper = rp.release();
+        }
+        std::lock_guard<std::mutex> lq(g_reaper->mu);
+        // backpressure: an idle-priority reaper that never gets a core (a
+        // saturated host) must not let freed results pile up
+        g_reaper->q.push_back(r);
+        if (g_reaper->q.size() > kReapMaxQueued) {
+          r = g_reaper->q.front();
+          g_reaper->q.pop_front();
+        } else {
+          r = nullptr;
+        }
+      } catch (...) {}             // no reaper (thread or queue allocation failed): r is deleted inline
+      if (g_reaper) g_reaper->cv.notify_one();   // under g_reaper_mu: the owner cannot delete the reaper meanwhile
     }
   }
-  g_reaper->cv.notify_one();       // under g_reaper_mu: the owner cannot delete the reaper meanwhile
-  delete r;                        // the oldest queued result, inline (nullptr: nothing)
+  delete r;                        // the oldest queued result (or r itself), inline and outside the locks
 }
 void tsg_free(void* p) { free(p); }
 
@@ -523,11 +528,9 @@ int tsg_scan_host_reference(const tsg_ruleset* rs, const uint8_t* data, const ui
                               binary ? binary[f] != 0 : false, nullptr);
     }
   };
-  int nt = threads > 0 ? threads : 1;
-  std::vector<std::thread> pool;
-  for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
-  worker();
-  for (auto& t : pool) t.join();
+  std::unique_ptr<tsg_result> guard_r(r);      // freed if a worker throws
+  run_threads(threads > 0 ? threads : 1, worker);
+  guard_r.release();
   *out = r;
   return TSG_OK;
   TSG_API_CATCH
@@ -1307,6 +1310,8 @@ int tsg_scan_fs_tree_model(const tsg_ruleset* rs, const char* root, const tsg_fe
 }
 
 struct tsg_queue {
+  std::unique_ptr<Prefilter> pf;          // (model queues) the CPU model's tables
+  std::string fail_path;                  // (model queues) a batch holding this path throws bad_alloc
   std::unique_ptr<ScanQueue> q;
   std::shared_ptr<const Ruleset> rs;
 };
@@ -1315,11 +1320,44 @@ int tsg_queue_create(tsg_engine* e, uint32_t max_files, uint64_t max_bytes, uint
                      uint32_t max_inflight, tsg_queue** out) {
   TSG_API_TRY
   if (!e || !out) return fail(TSG_ERR_INVALID, "NULL argument");
-  auto* q = new tsg_queue();
-  q->q.reset(new ScanQueue(e->eng.get(), max_files ? max_files : 4096, max_bytes ? max_bytes : (256ull << 20),
+  std::unique_ptr<tsg_queue> q(new tsg_queue());
+  q->q.reset(new ScanQueue(engine_stage(e), max_files ? max_files : 4096, max_bytes ? max_bytes : (256ull << 20),
                            max_wait_us, max_inflight ? max_inflight : 4));
   q->rs = e->eng->ruleset();
-  *out = q;
+  *out = q.release();
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_queue_create_model(const tsg_ruleset* rs, uint32_t max_files, uint64_t max_bytes, uint32_t max_wait_us,
+                           uint32_t max_inflight, const char* fail_path, tsg_queue** out) {
+  TSG_API_TRY
+  if (!rs || !out) return fail(TSG_ERR_INVALID, "NULL argument");
+  std::unique_ptr<tsg_queue> q(new tsg_queue());
+  q->pf.reset(new Prefilter());
+  std::string err;
+  if (!build_prefilter(*rs->rs, q->pf.get(), &err)) return fail(TSG_ERR_INTERNAL, err);
+  q->rs = rs->rs;
+  q->fail_path = fail_path ? fail_path : "";
+  tsg_queue* qp = q.get();
+  BatchScanFn model = [qp](const BatchInput& in, SecretVec* res, std::string* e2) {
+    if (!qp->fail_path.empty()) {
+      for (uint32_t f = 0; f < in.nfiles; ++f)
+        if (path_of(in.paths, in.path_lens, f) == qp->fail_path) throw std::bad_alloc();   // injected host failure
+    }
+    return model_stage(*qp->rs, *qp->pf)(in, res, e2);
+  };
+  q->q.reset(new ScanQueue(std::move(model), max_files ? max_files : 4096, max_bytes ? max_bytes : (256ull << 20),
+                           max_wait_us, max_inflight ? max_inflight : 4));
+  *out = q.release();
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_queue_timeouts(tsg_queue* q, uint64_t* timeouts) {
+  TSG_API_TRY
+  if (!q || !timeouts) return fail(TSG_ERR_INVALID, "NULL argument");
+  *timeouts = q->q->stats().timeouts;
   return TSG_OK;
   TSG_API_CATCH
 }
@@ -1380,9 +1418,7 @@ int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, 
     }
   };
   const auto t0 = std::chrono::steady_clock::now();
-  std::vector<std::thread> ts;
-  for (uint32_t c = 0; c < callers; ++c) ts.emplace_back(worker);
-  for (auto& t : ts) t.join();
+  run_threads(static_cast<int>(callers), worker);
   *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   *findings = nf.load();
   if (bad) return fail(TSG_ERR_HIP, first_err);
@@ -1392,9 +1428,14 @@ int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, 
 
 const char* tsg_result_walk_json(const tsg_result* r) {
   if (!r || !r->walk) return nullptr;
-  std::lock_guard<std::mutex> lk(r->walk_mu);
-  if (r->walk_json.empty()) build_walk_json(*r->walk, &r->walk_json);
-  return r->walk_json.c_str();
+  try {
+    std::lock_guard<std::mutex> lk(r->walk_mu);
+    if (r->walk_json.empty()) build_walk_json(*r->walk, &r->walk_json);
+    return r->walk_json.c_str();
+  } catch (...) {                                // (bad_alloc) NULL, the reason in tsg_last_error
+    fail(TSG_ERR_INTERNAL, "out of memory");
+    return nullptr;
+  }
 }
 
 int tsg_prepared_paths(const tsg_prepared* p, const char* const** paths, const uint32_t** lens) {

@@ -37,6 +37,10 @@ struct BatchInput {
   const uint8_t* binary = nullptr;     // optional ScanArgs.Binary flags
 };
 
+// A batch scan stage: results[i] = Scan(ScanArgs{paths[i], data[off[i]:off[i+1]],
+// binary[i]}) -- Engine::scan, or (tests only) the CPU model of its passes.
+using BatchScanFn = std::function<bool(const BatchInput& in, SecretVec* results, std::string* err)>;
+
 struct DeviceTables;
 struct Lane;
 struct GpuOut;

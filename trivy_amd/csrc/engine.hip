@@ -219,12 +219,13 @@ __device__ __forceinline__ unsigned long long k1_end(const K1Ctx& x, const K1Str
 // U+0130 / U+017F / U+212A fold onto ASCII letters: flag every file that
 // overlaps a 16-byte word ending such a sequence (host re-scans it exactly).
 // A superset is safe (a flagged file is only scanned more carefully).
-__device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, const uint32_t w[4],
+__device__ __forceinline__ void k1_special(const K1Ctx& x, const K1Stream& t, const v4u w,
                                            unsigned long long fend, unsigned long long end) {
   uint32_t a = t.p12 & 0xffu, bb = t.p12 >> 8;
   bool hit = false;
   for (int k = 0; k < 16 && t.p + k < end; ++k) {
-    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    const uint32_t wk = (k & 8) ? ((k & 4) ? w.w : w.z) : ((k & 4) ? w.y : w.x);   // (no indexed array: scratch)
+    const uint32_t b = (wk >> ((k & 3) * 8)) & 0xffu;
     if (t.p + k == fend) { a = bb = 0; }
     if ((b == 0xB0u && a == 0xC4u) || (b == 0xBFu && a == 0xC5u) || (b == 0xAAu && a == 0x84u && bb == 0xE2u)) hit = true;
     bb = a;
@@ -296,10 +297,14 @@ __device__ __forceinline__ void k1_out_c(const K1Ctx& x, K1Stream& t, uint32_t s
 
 // One 16-byte word of one stream with file-boundary and stream-end checks.
 template <bool kC>
-__device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const uint32_t w[4], uint32_t S = 0) {
+__device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const v4u w, uint32_t S = 0) {
   const unsigned long long end = k1_end(x, t);
   unsigned long long fend = x.offsets[t.f + 1];
-  if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
+  if (x.primary && ((w.x | w.y | w.z | w.w) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
+  // rolled (the slow path runs on boundary and last lines only): unrolled, its
+  // 16 copies of the per-byte branches held ~450 scalar values live and the
+  // kernel spilled SGPRs into VGPR lanes
+#pragma unroll 1
   for (int k = 0; k < 16; ++k) {
     const unsigned long long q = t.p + k;
     if (q >= end) break;
@@ -309,7 +314,8 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
       t.s = x.s0;
       t.p12 = 0;
     }
-    const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+    const uint32_t wk = (k & 8) ? ((k & 4) ? w.w : w.z) : ((k & 4) ? w.y : w.x);   // (no indexed array: scratch)
+    const uint32_t b = (wk >> ((k & 3) * 8)) & 0xffu;
     if constexpr (kC) {
       const uint32_t c4 = x.cls[b];
       t.s = k1c_next(t.s, c4, __builtin_amdgcn_perm(0u, c4, 0u));
@@ -856,7 +862,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
             // words one by one and restart the prefetch: four exposed memory
             // latencies per boundary for the whole wave.
             if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
-#pragma unroll
+#pragma unroll 1
             for (int i = 0; i < kW; ++i) {
               if (t.p >= k1_end(x, t)) break;
               if (t.p >= t.cend && t.cend < t.end) {            // chunk ends are word-aligned
@@ -865,15 +871,19 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
                 ++t.ci;
                 t.cend = min(t.cend + chunk, t.end);
               }
-              const uint32_t w[4] = {cur[i].x, cur[i].y, cur[i].z, cur[i].w};
+              // (the word by selects, not by an indexed register array: the
+              // rolled loop would put cur[] in scratch)
+              v4u cw = cur[0];
+#pragma unroll
+              for (int j = 1; j < kW; ++j) cw = i == j ? cur[j] : cw;
               if ((kAbl & kAblDefer) && (kAbl & kAblBoundaryFastWords) && t.p + 16 <= t.lim) {
-                if (x.primary && ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) && t.p >= t.emit)
-                  k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
-                if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, w[0], w[1], w[2], w[3]);
-                else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, w[0], w[1], w[2], w[3]);
+                if (x.primary && ((cw.x | cw.y | cw.z | cw.w) & 0x80808080u) && t.p >= t.emit)
+                  k1_special(x, t, cw, x.offsets[t.f + 1], k1_end(x, t));
+                if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, cw.x, cw.y, cw.z, cw.w);
+                else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cw.x, cw.y, cw.z, cw.w);
               } else {
                 if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
-                k1_word_slow<kC>(x, t, w, S);
+                k1_word_slow<kC>(x, t, cw, S);
               }
             }
           }
@@ -895,15 +905,14 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
               t.cend = min(t.cend + chunk, t.end);
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             if ((kAbl & kAblDefer) && (kAbl & kAblBoundaryFastWords) && t.p + 16 <= t.lim) {
               if (x.primary && ((v.x | v.y | v.z | v.w) & 0x80808080u) && t.p >= t.emit)
-                k1_special(x, t, w, x.offsets[t.f + 1], k1_end(x, t));
+                k1_special(x, t, v, x.offsets[t.f + 1], k1_end(x, t));
               if constexpr (kC) k1_word_c<kAbl>(x, t, ob, smem, v.x, v.y, v.z, v.w);
               else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, v.x, v.y, v.z, v.w);
             } else {
               if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);   // before the word that may change the file
-              k1_word_slow<kC>(x, t, w, S);
+              k1_word_slow<kC>(x, t, v, S);
             }
           }
         }
@@ -2327,8 +2336,14 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     std::string e;
     ScanStats dst;
     auto tb = std::chrono::steady_clock::now();
-    Lane* ln = acquire_lane(*dt, &e);
-    bool ok = ln != nullptr;
+    Lane* ln = nullptr;
+    bool ok = false;
+    // (a host exception -- bad_alloc of a plan or a copy-out -- ends this
+    // driver like a HIP error: the queue is aborted and the call fails; it
+    // must not escape the thread)
+    try {
+    ln = acquire_lane(*dt, &e);
+    ok = ln != nullptr;
     if (ok && hipSetDevice(dt->device) != hipSuccess) { ok = false; e = "hipSetDevice failed"; }
     if (ok && !resident) {
       for (int i = 0; i < 2 && ok; ++i) {
@@ -2426,6 +2441,13 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       slot ^= 1;
     }
     if (ok) plan_pending();
+    } catch (const std::exception& x) {
+      ok = false;
+      e = std::string("host exception in the device driver: ") + x.what();
+    } catch (...) {
+      ok = false;
+      e = "host exception in the device driver";
+    }
     if (ln) {
       if (!ok) { hipStreamSynchronize(ln->copy); hipStreamSynchronize(ln->compute); }
       release_lane(*dt, ln);
@@ -2441,30 +2463,47 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
   };
   CallCtx* cc = acquire_call();
   std::vector<std::thread> threads;
-  for (DeviceTables* dt : drivers) threads.emplace_back(driver, dt);
-  // per-file result slots (hundreds of thousands for image layers) are set up
-  // while the first segment's upload and GPU passes run
-  results->clear();
-  results->resize(in.nfiles);
-  if (host_profile_) std::fprintf(stderr, "[tsg tl] %u result slots ready at %.3f ms\n", in.nfiles, ms_since(t_feed0));
   uint64_t nconf = 0, nfind = 0;
   double host_ms = 0;
-  for (;;) {
-    int left = 0;
-    confirmer_idle.store(true, std::memory_order_release);
-    std::unique_ptr<Job> job = q.pop(&left);
-    confirmer_idle.store(false, std::memory_order_release);
-    if (!job) break;
-    auto th = std::chrono::steady_clock::now();
-    const Segment& sg = segs[job->seg];
-    const double c_start = host_profile_ ? ms_since(t_feed0) : 0.0;
-    // (drivers that block on an event leave every core to the pool)
-    confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0 && !dual);
-    host_ms += ms_since(th);
-    if (host_profile_) std::fprintf(stderr, "[tsg tl] seg %zu confirm %.3f-%.3f ms\n", job->seg, c_start, ms_since(t_feed0));
+  std::string host_err;
+  try {
+    for (DeviceTables* dt : drivers) threads.emplace_back(driver, dt);
+    // per-file result slots (hundreds of thousands for image layers) are set up
+    // while the first segment's upload and GPU passes run
+    results->clear();
+    results->resize(in.nfiles);
+    if (host_profile_) std::fprintf(stderr, "[tsg tl] %u result slots ready at %.3f ms\n", in.nfiles, ms_since(t_feed0));
+    for (;;) {
+      int left = 0;
+      confirmer_idle.store(true, std::memory_order_release);
+      std::unique_ptr<Job> job = q.pop(&left);
+      confirmer_idle.store(false, std::memory_order_release);
+      if (!job) break;
+      auto th = std::chrono::steady_clock::now();
+      const Segment& sg = segs[job->seg];
+      const double c_start = host_profile_ ? ms_since(t_feed0) : 0.0;
+      // (drivers that block on an event leave every core to the pool)
+      confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0 && !dual);
+      host_ms += ms_since(th);
+      if (host_profile_) std::fprintf(stderr, "[tsg tl] seg %zu confirm %.3f-%.3f ms\n", job->seg, c_start, ms_since(t_feed0));
+    }
+  } catch (const std::exception& x) {
+    // (bad_alloc in the confirmation, or a driver thread that could not be
+    // started): stop the drivers, join them, fail the call
+    host_err = std::string("host exception: ") + x.what();
+  } catch (...) {
+    host_err = "host exception";
+  }
+  if (!host_err.empty()) {
+    q.abort();
+    for (;;) {                                   // drain what the drivers still hand over
+      int left = 0;
+      if (!q.pop(&left)) break;
+    }
   }
   for (auto& t : threads) t.join();
   release_call(cc);
+  if (!host_err.empty()) { *err = host_err; return false; }
   if (!drv_err.empty()) { *err = drv_err; return false; }
   st->bytes = total;
   st->files = in.nfiles;

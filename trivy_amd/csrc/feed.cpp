@@ -7,6 +7,7 @@
 #include "feed.h"
 
 #include "goregexp.h"
+#include "guard.h"
 
 #include <algorithm>
 #include <atomic>
@@ -84,10 +85,7 @@ void parallel_for(uint32_t n, int threads, F&& fn) {
       for (uint32_t i = b, e = std::min(n, b + blk); i < e; ++i) fn(i);
     }
   };
-  std::vector<std::thread> ts;
-  for (int t = 1; t < nt; ++t) ts.emplace_back(run);
-  run();
-  for (auto& th : ts) th.join();
+  run_threads(nt, run);
 }
 
 std::string trim_left_slash(const std::string& p) {

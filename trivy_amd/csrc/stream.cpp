@@ -16,6 +16,7 @@
 #include <mutex>
 #include <thread>
 
+#include "guard.h"
 #include "tar.h"
 
 extern "C" int tsg_alloc_pinned(size_t bytes, void** out);
@@ -359,19 +360,31 @@ class Pipeline {
         prep_q_.pop_front();
       }
       const auto t0 = Clock::now();
-      auto job = std::make_unique<Job>();
+      std::unique_ptr<Job> job;
       std::string err;
       double wait = 0;
-      BufPool* pool = &pool_;
-      FeedAlloc alloc = [pool, &wait](size_t bytes, FeedFree* free_fn) -> uint8_t* {
-        uint8_t* p = pool->get(bytes, &wait);
-        if (p) *free_fn = [pool](uint8_t* q) { pool->put(q); };
-        return p;
-      };
-      bool good = ok() && prepare_files(rs_, fo_, raw_[task->buf].get(), task->starts.data(), task->sizes.data(),
-                                        task->paths, o_.threads, &job->b, &err, alloc);
-      if (good && !job->b.data) { good = false; err = "out of memory for a prepared batch"; }
-      if (good) for (uint32_t i : job->b.index) job->scan_paths.push_back(prefix_ + task->paths[i]);
+      bool good = false;
+      // (a host exception -- bad_alloc in the prepare -- fails the stream; it
+      // must not escape this thread)
+      try {
+        job = std::make_unique<Job>();
+        BufPool* pool = &pool_;
+        FeedAlloc alloc = [pool, &wait](size_t bytes, FeedFree* free_fn) -> uint8_t* {
+          uint8_t* p = pool->get(bytes, &wait);
+          if (p) *free_fn = [pool](uint8_t* q) { pool->put(q); };
+          return p;
+        };
+        good = ok() && prepare_files(rs_, fo_, raw_[task->buf].get(), task->starts.data(), task->sizes.data(),
+                                     task->paths, o_.threads, &job->b, &err, alloc);
+        if (good && !job->b.data) { good = false; err = "out of memory for a prepared batch"; }
+        if (good) for (uint32_t i : job->b.index) job->scan_paths.push_back(prefix_ + task->paths[i]);
+      } catch (const std::exception& x) {
+        good = false;
+        err = std::string("host exception in the prepare stage: ") + x.what();
+      } catch (...) {
+        good = false;
+        err = "host exception in the prepare stage";
+      }
       std::lock_guard<std::mutex> lk(mu_);
       busy_[task->buf] = false;
       if (!good) {
@@ -398,27 +411,37 @@ class Pipeline {
         q_.pop_front();
       }
       const auto t0 = Clock::now();
-      const uint32_t nk = static_cast<uint32_t>(job->b.index.size());
-      std::vector<const char*> pp(nk);
-      std::vector<uint32_t> pl(nk);
-      for (uint32_t k = 0; k < nk; ++k) {
-        pp[k] = job->scan_paths[k].c_str();
-        pl[k] = static_cast<uint32_t>(job->scan_paths[k].size());
+      // (a host exception in the scan stage or while the results are moved
+      // fails the stream; it must not escape this thread)
+      try {
+        const uint32_t nk = static_cast<uint32_t>(job->b.index.size());
+        std::vector<const char*> pp(nk);
+        std::vector<uint32_t> pl(nk);
+        for (uint32_t k = 0; k < nk; ++k) {
+          pp[k] = job->scan_paths[k].c_str();
+          pl[k] = static_cast<uint32_t>(job->scan_paths[k].size());
+        }
+        BatchInput in;
+        in.h_data = job->b.data.get();
+        in.offsets = job->b.offsets.data();
+        in.nfiles = nk;
+        in.paths = pp.data();
+        in.path_lens = pl.data();
+        in.binary = job->b.binary.data();
+        SecretVec res;
+        std::string err;
+        if (!scan_(in, &res, &err)) { set_error(err); return; }
+        out_->st.scanned_bytes += job->b.offsets[nk];
+        out_->st.files += nk;
+        out_->st.batches += 1;
+        for (auto& r : res) out_->files.push_back(std::move(r));
+      } catch (const std::exception& x) {
+        set_error(std::string("host exception in the scan stage: ") + x.what());
+        return;
+      } catch (...) {
+        set_error("host exception in the scan stage");
+        return;
       }
-      BatchInput in;
-      in.h_data = job->b.data.get();
-      in.offsets = job->b.offsets.data();
-      in.nfiles = nk;
-      in.paths = pp.data();
-      in.path_lens = pl.data();
-      in.binary = job->b.binary.data();
-      SecretVec res;
-      std::string err;
-      if (!scan_(in, &res, &err)) { set_error(err); return; }
-      out_->st.scanned_bytes += job->b.offsets[nk];
-      out_->st.files += nk;
-      out_->st.batches += 1;
-      for (auto& r : res) out_->files.push_back(std::move(r));
       job.reset();                                // the prepared buffer goes back to the pool
       out_->st.scan_ms += ms_between(t0, Clock::now());
     }
@@ -605,10 +628,7 @@ bool plan_fs_tree(const Ruleset& rs, const FeedOpts& fo, const std::string& root
           want[i] = static_cast<uint8_t>(secret_analyzer_wants_path(rs, fo, walk->files[i].rel));
       }
     };
-    std::vector<std::thread> ts;
-    for (int t = 1; t < std::min<int>(threads, static_cast<int>(n / 256) + 1); ++t) ts.emplace_back(run);
-    run();
-    for (auto& th : ts) th.join();
+    run_threads(std::min<int>(threads, static_cast<int>(n / 256) + 1), run);
   }
   for (uint32_t i = 0; i < n; ++i) {
     if (!want[i]) continue;

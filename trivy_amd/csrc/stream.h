@@ -20,9 +20,6 @@
 
 namespace tsg {
 
-// The scan stage: results[i] = Scan(ScanArgs{paths[i], data[off[i]:off[i+1]], binary[i]}).
-using BatchScanFn = std::function<bool(const BatchInput& in, SecretVec* results, std::string* err)>;
-
 // A reader (io.Reader): > 0 bytes read into buf, 0 at the end, < 0 on an error.
 using StreamReadFn = int64_t (*)(void* user, uint8_t* buf, size_t cap);
 

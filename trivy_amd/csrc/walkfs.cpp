@@ -16,6 +16,7 @@
 #include <mutex>
 #include <thread>
 
+#include "guard.h"
 #include "tar.h"
 
 namespace tsg {
@@ -163,7 +164,14 @@ struct Walker {
           ++busy;
         }
         std::vector<std::pair<std::string, std::string>> subdirs;
-        dir(task.first, task.second, &local, &subdirs);
+        try {
+          dir(task.first, task.second, &local, &subdirs);
+        } catch (...) {                        // the other workers must not wait on this task
+          std::lock_guard<std::mutex> lk(mu);
+          --busy;
+          cv.notify_all();
+          throw;
+        }
         std::lock_guard<std::mutex> lk(mu);
         for (auto& sd : subdirs) todo.push_back(std::move(sd));
         --busy;
@@ -172,10 +180,7 @@ struct Walker {
       std::lock_guard<std::mutex> lk(mu);
       for (auto& f : local) files.push_back(std::move(f));
     };
-    std::vector<std::thread> ts;
-    for (int t = 1; t < threads; ++t) ts.emplace_back(worker);
-    worker();
-    for (auto& th : ts) th.join();
+    run_threads(threads, worker);
     std::sort(files.begin(), files.end(), [](const FsFile& a, const FsFile& b) { return walk_order_less(a.rel, b.rel); });
   }
 };
@@ -274,10 +279,7 @@ bool stat_fs_files(FsWalk* walk, int threads) {
     }
   };
   const int nt = std::max(1, std::min<int>(threads, static_cast<int>(std::max<uint32_t>(n / 64, 1))));
-  std::vector<std::thread> ts;
-  for (int t = 1; t < nt; ++t) ts.emplace_back(run);
-  run();
-  for (auto& th : ts) th.join();
+  run_threads(nt, run);
   for (uint32_t i = 0; i < n; ++i) {
     if (!errs[i]) continue;
     // d.Info() (fs.go:67-70): xerrors-wrapped, so not even a permission error
@@ -324,10 +326,7 @@ bool read_fs_files(const FsWalk& walk, const std::vector<uint32_t>& idx, const s
     }
   };
   const int nt = std::max(1, std::min<int>(threads, static_cast<int>(std::max<uint32_t>(n, 1))));
-  std::vector<std::thread> ts;
-  for (int t = 1; t < nt; ++t) ts.emplace_back(run);
-  run();
-  for (auto& th : ts) th.join();
+  run_threads(nt, run);
   const uint32_t k = first_bad.load();
   if (k != UINT32_MAX) {
     const FsFile& f = walk.files[idx[k]];

@@ -468,16 +468,30 @@ def ScanFsTree(scanner, root, skip_files=(), skip_dirs=(), file_patterns=(), con
     return _stream_result(L, rc, res, as_result)
 
 
+# ScanQueue::kPeakHold (queue.h): a peak of concurrent callers not seen
+# again for this long is over
+QUEUE_PEAK_HOLD_S = 0.010
+
+
 class ScanQueue:
     """Per-file Scanner.Scan for unchanged callers (tsg_queue_*): concurrent
     Scan calls (SecretAnalyzer.Analyze, secret.go:137, from --parallel
     goroutines) share one engine batch."""
 
-    def __init__(self, scanner, max_files=0, max_bytes=0, max_wait_us=200, max_inflight=0):
+    def __init__(self, scanner, max_files=0, max_bytes=0, max_wait_us=200, max_inflight=0, model=False,
+                 fail_path=None):
+        """model=True (tests only): the CPU model of the GPU passes as the
+        batch stage (tsg_queue_create_model), no GPU needed; a batch holding
+        `fail_path` then fails with an injected bad_alloc."""
         self._sc = scanner
         self._q = ctypes.c_void_p()
-        _lib.check(_lib.lib().tsg_queue_create(scanner.engine(), max_files, max_bytes, max_wait_us, max_inflight,
-                                               ctypes.byref(self._q)))
+        if model:
+            fp = fail_path.encode("utf-8", "surrogateescape") if fail_path else None
+            _lib.check(_lib.lib().tsg_queue_create_model(scanner._rs, max_files, max_bytes, max_wait_us,
+                                                         max_inflight, fp, ctypes.byref(self._q)))
+        else:
+            _lib.check(_lib.lib().tsg_queue_create(scanner.engine(), max_files, max_bytes, max_wait_us,
+                                                   max_inflight, ctypes.byref(self._q)))
 
     def Scan(self, args):
         L = _lib.lib()
@@ -496,7 +510,10 @@ class ScanQueue:
     def stats(self):
         v = [ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()]
         _lib.check(_lib.lib().tsg_queue_stats(self._q, *[ctypes.byref(x) for x in v]))
-        return {"calls": v[0].value, "batches": v[1].value, "files": v[2].value, "max_batch": v[3].value}
+        t = ctypes.c_uint64()
+        _lib.check(_lib.lib().tsg_queue_timeouts(self._q, ctypes.byref(t)))
+        return {"calls": v[0].value, "batches": v[1].value, "files": v[2].value, "max_batch": v[3].value,
+                "timeouts": t.value}
 
     def probe(self, args_list, callers):
         """callers threads scanning args_list file by file through the queue

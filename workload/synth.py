@@ -357,6 +357,8 @@ def _sizes(kind, n_or_bytes, rng):
             s = int(np.exp(rng.uniform(np.log(64), np.log(64 << 20))))
         elif kind == "tiny":             # offset-table stress: ~300 B files
             s = int(min(max(rng.lognormvariate(np.log(200), 1.0), 1), 64 << 10))
+        elif kind == "one":              # K1 probes: the whole batch as one file (no file boundaries)
+            s = n_or_bytes
         else:                            # small files (config 3): mean ~25 KB
             s = int(min(max(rng.lognormvariate(np.log(9000), 1.3), 16), 4 << 20))
         s = min(s, n_or_bytes - total) if n_or_bytes - total > 16 else s
