@@ -106,13 +106,14 @@ def test_k1_probe_variants_agree_gpu():
     assert os.path.exists(probe), "build the probe library: python -m trivy_amd.build --probe"
     env = dict(os.environ, TSG_LIB="libtrivysecret_probe.so")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_k1_probe_variants.py"),
-                        "16:4096,0:8192,2512:1024,2448:2048,4560:2048,8656:1024,12752:2048"],
+                        "16:4096,0:8192,2512:1024,2448:2048,464:2048,464:512,8656:1024,12752:2048"],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert r.stdout.count("agree") == 7, r.stdout
+    assert r.stdout.count("agree") == 8, r.stdout
 
 
-@pytest.mark.parametrize("abl,chunk", [("464", "2048"), ("464", "1024"), ("464", "4096"), ("464", "256")])
+@pytest.mark.parametrize("abl,chunk", [("4560", "2048"), ("4560", "1024"), ("4560", "4096"), ("4560", "512"),
+                                       ("4560", "256")])
 def test_k1_variants_agree_gpu(monkeypatch, abl, chunk):
     # the product K1 build over every chunk size gives the host confirmer's
     # result (the measurement builds: test_k1_probe_variants_agree_gpu)

@@ -10,7 +10,9 @@ there is no GPU here), then runs the driver over
 Each run must finish with no sanitizer report and host == table model; a
 third run (--parsers) feeds the parsers of untrusted input (layer tars, image
 configs, protobuf messages, an fs tree) with fixtures and truncated /
-mutated copies.
+mutated copies; a fourth (--concurrency) runs the concurrent host code: the
+per-file queue with 16 callers and with an injected failure, the streamed
+layer / tree pipelines, the result reaper and threaded SecretVec construction.
 
   python tools/asan_check.py [--mb 8] [--out profiles/r3n_asan.log]
 """
@@ -191,8 +193,13 @@ def main():
                    TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
         write_parsers_case(os.path.join(td, "parsers"))
         rc_all = 0
-        for case in ("c2", "c5", "parsers"):
-            argv = [exe, "--parsers", os.path.join(td, case)] if case == "parsers" else [exe, os.path.join(td, case)]
+        for case in ("c2", "c5", "parsers", "concurrency"):
+            if case == "parsers":
+                argv = [exe, "--parsers", os.path.join(td, case)]
+            elif case == "concurrency":      # queue, stream pipelines, reaper, threaded SecretVec
+                argv = [exe, "--concurrency", os.path.join(td, "c2"), os.path.join(td, "parsers")]
+            else:
+                argv = [exe, os.path.join(td, case)]
             p = subprocess.run(argv, capture_output=True, text=True, env=env)
             lines.append("%s rc=%d %s%s" % (case, p.returncode, p.stdout, p.stderr[-4000:]))
             rc_all |= p.returncode

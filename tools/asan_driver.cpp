@@ -10,13 +10,22 @@
 // tsg_prepare_fs_tree (tree/), tsg_image_config_content and
 // tsg_guess_base_layers (configs/), tsg_result_to_proto /
 // tsg_result_from_proto round trips with truncations and bit flips, and
-// tsg_report_json over the results.
+// tsg_report_json over the results;
+// with --concurrency <case dir> <parsers dir>: the concurrent host code --
+// the per-file queue (tsg_queue_create_model: 16 callers through
+// tsg_queue_probe, then 8 caller threads with a batch stage that throws,
+// then a lone caller), the streamed layer and tree pipelines
+// (tsg_scan_layer_stream_model / tsg_scan_fs_tree_model: producer, prepare
+// and scan threads, small batches), large results freed from several
+// threads at once (the idle-priority reaper) and a table-model result of
+// 70k files (threaded SecretVec construction).
 // The two scan paths must give byte-identical JSON (the superset argument of
 // DESIGN.md §2).  Usage: asan_driver <dir> where <dir> holds config.json
 // (may be empty = builtin rules), data.bin, offsets.bin (uint64 nfiles+1),
 // paths.txt (one path per line).
 #include <pthread.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,7 +34,11 @@
 #include <string>
 #include <vector>
 
+#include <atomic>
+#include <thread>
+
 #include "trivy_secret.h"
+#include "trivy_secret_test.h"
 
 static std::string slurp(const std::string& p) {
   std::ifstream f(p, std::ios::binary);
@@ -267,6 +280,123 @@ static int run_parsers(const std::string& dir) {
   return 0;
 }
 
+struct MemReader {
+  const std::string* buf;
+  size_t pos;
+  size_t step;
+};
+
+static int64_t mem_read(void* user, uint8_t* out, size_t cap) {
+  auto* r = static_cast<MemReader*>(user);
+  const size_t n = std::min({cap, r->step, r->buf->size() - r->pos});
+  std::memcpy(out, r->buf->data() + r->pos, n);
+  r->pos += n;
+  return static_cast<int64_t>(n);
+}
+
+static int run_concurrency(const std::string& dir, const std::string& pdir) {
+  const std::string data = slurp(dir + "/data.bin");
+  const std::string offs_raw = slurp(dir + "/offsets.bin");
+  std::vector<uint64_t> offs(offs_raw.size() / 8);
+  std::memcpy(offs.data(), offs_raw.data(), offs.size() * 8);
+  std::vector<std::string> paths;
+  {
+    std::istringstream in(slurp(dir + "/paths.txt"));
+    for (std::string l; std::getline(in, l);) paths.push_back(l);
+  }
+  const uint32_t n = static_cast<uint32_t>(offs.size() - 1);
+  std::vector<const char*> pp(n);
+  std::vector<uint32_t> pl(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    pp[i] = paths[i].c_str();
+    pl[i] = static_cast<uint32_t>(paths[i].size());
+  }
+  const uint8_t* d = reinterpret_cast<const uint8_t*>(data.data());
+  tsg_ruleset* rs = nullptr;
+  if (tsg_ruleset_compile(nullptr, 0, &rs) != 0) return fail("ruleset_compile");
+  // 1. the per-file queue: 16 callers sharing batches
+  tsg_queue* q = nullptr;
+  if (tsg_queue_create_model(rs, 0, 0, 200, 4, nullptr, &q) != 0) return fail("queue_create_model");
+  double sec = 0;
+  uint64_t nf = 0;
+  if (tsg_queue_probe(q, d, offs.data(), n, pp.data(), pl.data(), 16, &sec, &nf) != 0) return fail("queue_probe");
+  uint64_t calls = 0, batches = 0, files = 0;
+  uint32_t maxb = 0;
+  if (tsg_queue_stats(q, &calls, &batches, &files, &maxb) != 0) return fail("queue_stats");
+  std::printf("queue: %u files, 16 callers, %llu batches (max %u files), %llu findings\n", n,
+              static_cast<unsigned long long>(batches), maxb, static_cast<unsigned long long>(nf));
+  tsg_queue_destroy(q);
+  // 2. the queue with a batch stage that throws (a file named as fail_path)
+  if (tsg_queue_create_model(rs, 0, 0, 200, 2, pp[n / 2], &q) != 0) return fail("queue_create_model");
+  std::atomic<uint32_t> next{0}, errs{0};
+  auto caller = [&]() {
+    for (uint32_t i; (i = next.fetch_add(1)) < std::min<uint32_t>(n, 400);) {
+      tsg_result* r = nullptr;
+      if (tsg_queue_scan(q, pp[i], pl[i], d + offs[i], offs[i + 1] - offs[i], 0, &r) != 0) ++errs;
+      else tsg_result_free(r);
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t) ts.emplace_back(caller);
+  for (auto& t : ts) t.join();
+  ts.clear();
+  tsg_result* lone = nullptr;
+  if (tsg_queue_scan(q, pp[0], pl[0], d + offs[0], offs[1] - offs[0], 0, &lone) != 0) return fail("queue_scan after failure");
+  tsg_result_free(lone);
+  std::printf("queue with an injected failure: %u calls failed, the queue went on\n", errs.load());
+  if (errs.load() == 0) { std::fprintf(stderr, "asan_driver: injected failure not seen\n"); return 1; }
+  tsg_queue_destroy(q);
+  // 3. streamed layer tars and an fs tree through the pipelines (small batches)
+  {
+    std::istringstream idx(slurp(pdir + "/tars/index.txt"));
+    int done = 0;
+    for (std::string name; std::getline(idx, name) && done < 4; ++done) {
+      const std::string tar = slurp(pdir + "/tars/" + name);
+      MemReader mr{&tar, 0, 777};
+      tsg_feed_opts o{};
+      o.threads = 4;
+      tsg_result* r = nullptr;
+      if (tsg_scan_layer_stream_model(rs, mem_read, &mr, &o, 4096, &r) == 0) {
+        const char* js = tsg_result_walk_json(r);
+        if (!js) return fail("walk_json");
+        tsg_result_free(r);
+      }
+    }
+    tsg_feed_opts o{};
+    o.threads = 4;
+    tsg_result* r = nullptr;
+    if (tsg_scan_fs_tree_model(rs, (pdir + "/tree").c_str(), &o, 8192, &r) != 0) return fail("scan_fs_tree_model");
+    std::printf("fs tree streamed: %u files\n", tsg_result_num_files(r));
+    tsg_result_free(r);
+  }
+  // 4. large results (>= 4096 files) freed from several threads at once: the reaper
+  {
+    const uint32_t m = 70000;                       // > 65536: SecretVec constructs its slots on threads
+    std::vector<uint64_t> o2(m + 1);
+    std::string body;
+    for (uint32_t i = 0; i < m; ++i) {
+      o2[i] = body.size();
+      body += (i % 97 == 0) ? "key = AKIAIOSFODNN7EXAMPL" + std::to_string(i % 10) + "\n" : "x = 1\n";
+    }
+    o2[m] = body.size();
+    std::vector<std::string> names(m);
+    std::vector<const char*> np(m);
+    for (uint32_t i = 0; i < m; ++i) {
+      names[i] = "f" + std::to_string(i) + ".txt";
+      np[i] = names[i].c_str();
+    }
+    std::vector<tsg_result*> rs_out(6, nullptr);
+    for (auto& r : rs_out)
+      if (tsg_scan_table_model(rs, reinterpret_cast<const uint8_t*>(body.data()), o2.data(), m, np.data(), nullptr,
+                               nullptr, &r) != 0) return fail("scan_table_model");
+    for (auto* r : rs_out) ts.emplace_back([r] { tsg_result_free(r); });
+    for (auto& t : ts) t.join();
+    std::printf("reaper: 6 results of %u files freed from 6 threads\n", m);
+  }
+  tsg_ruleset_free(rs);
+  return 0;
+}
+
 // Regexp compile recurses once per nesting level, and simplify turns x{0,N}
 // into N nested quests (Go's regexp/syntax does the same; its goroutine
 // stacks grow).  ASan's redzones make each frame several times larger than
@@ -280,6 +410,7 @@ struct Args {
 static void* run_thread(void* p) {
   auto* a = static_cast<Args*>(p);
   if (a->argc == 3 && std::string(a->argv[1]) == "--parsers") a->rc = run_parsers(a->argv[2]);
+  else if (a->argc == 4 && std::string(a->argv[1]) == "--concurrency") a->rc = run_concurrency(a->argv[2], a->argv[3]);
   else a->rc = run(a->argc, a->argv);
   return nullptr;
 }

@@ -6,7 +6,7 @@
 
 Prints per-launch K1 / K2 times and GB/s; used for K1 tuning and for
 rocprofv3 runs (a short program with few dispatches).  Variants other than
-the product build (TSG_K1_ABL != 464) need the probe library
+the product build (TSG_K1_ABL != 4560) need the probe library
 (python -m trivy_amd.build --probe), selected here through TSG_LIB.
 """
 import argparse
@@ -36,7 +36,7 @@ def main():
                     help="comma list of ABL[:CHUNK[:NAME=V+NAME=V]] (TSG_K1_ABL build bits / TSG_K1_CHUNK / extra "
                          "TSG_* settings), one engine each")
     args = ap.parse_args()
-    if any(v.split(":")[0] not in ("", "464") for v in args.variants.split(",") if v):
+    if any(v.split(":")[0] not in ("", "4560") for v in args.variants.split(",") if v):
         os.environ.setdefault("TSG_LIB", "libtrivysecret_probe.so")
     import torch
 
@@ -57,7 +57,7 @@ def main():
     for v in variants:
         if v is not None:
             parts = v.split(":") + ["", ""]
-            os.environ["TSG_K1_ABL"] = parts[0] or "464"
+            os.environ["TSG_K1_ABL"] = parts[0] or "4560"
             if parts[1]:
                 os.environ["TSG_K1_CHUNK"] = parts[1]
             else:

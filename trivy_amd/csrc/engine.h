@@ -112,10 +112,11 @@ class Engine {
   std::vector<CallCtx*> free_calls_;
   // tuning (TSG_* environment knobs, read once at create)
   uint32_t chunk_ = 0;                  // K1 bytes per lane chunk (TSG_K1_CHUNK); 0 = by launch size (k1_chunk_for)
-  // TSG_K1_ABL: K1 build (kAbl* bits).  Default 464 = deferred outputs +
-  // rolled word loop + 64-byte lines + temporal loads (layout bits, results
-  // valid); the other bits are measurement builds whose results are invalid.
-  int k1_abl_ = 464;
+  // TSG_K1_ABL: K1 build (kAbl* bits).  Default 4560 = deferred outputs +
+  // rolled word loop + 64-byte lines + temporal loads + fast words in boundary
+  // lines (layout bits, results valid); the other bits are measurement builds
+  // whose results are invalid.
+  int k1_abl_ = 4560;
   uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
   // drivers per device for resident batches (TSG_RESIDENT_DRIVERS; 2 =
   // K1Chain: measured no gain, config 2 1530 vs 1528 GB/s, config 3 766 vs

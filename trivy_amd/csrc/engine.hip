@@ -49,16 +49,30 @@ struct CandDev { uint32_t file, rule; unsigned long long start; };
 // Readback of a segment's results into host-mapped, fine-grained pinned
 // memory with plain vector stores over PCIe: no copy engine, so a readback
 // never queues behind an upload, and no DMA setup latency per small copy.
-// Copies nwords dwords, or min(*count * per_count, nwords) with a count
-// (16-byte granules: both buffers carry slack past the end).
-__global__ __launch_bounds__(256) void tsg_readback(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                    uint32_t nwords, const uint32_t* __restrict__ count,
-                                                    uint32_t per_count) {
-  uint32_t n = nwords;
-  if (count) n = static_cast<uint32_t>(min(static_cast<unsigned long long>(n),
-                                           static_cast<unsigned long long>(*count) * per_count));
+// One launch moves up to kRbMax regions (blockIdx.y selects one): region k
+// copies nwords dwords, or min(*count * per_count, nwords) with a count
+// (16-byte granules: both buffers carry slack past the end).  (A launch per
+// region cost ~4 us of dispatch each on small segments: per-file batches.)
+constexpr int kRbMax = 5;
+struct RbRegion { const uint4* src; uint4* dst; const uint32_t* count; uint32_t nwords, per_count; };
+struct RbList { RbRegion r[kRbMax]; };
+__global__ __launch_bounds__(256) void tsg_readback(RbList L) {
+  const RbRegion& g = L.r[blockIdx.y];
+  uint32_t n = g.nwords;
+  if (g.count) n = static_cast<uint32_t>(min(static_cast<unsigned long long>(n),
+                                             static_cast<unsigned long long>(*g.count) * g.per_count));
   const uint32_t n4 = (n + 3) / 4;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) dst[i] = src[i];
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) g.dst[i] = g.src[i];
+}
+
+// Zeroes up to four dword ranges in one launch (K1's per-segment scratch:
+// keyword bits, file flags, counters, per-region hit counts; four memsets
+// were four dispatches).
+struct ClearList { uint32_t* p[4]; uint32_t n[4]; };
+__global__ __launch_bounds__(256) void tsg_clear(ClearList L) {
+  uint32_t* p = L.p[blockIdx.y];
+  const uint32_t n = L.n[blockIdx.y];
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0;
 }
 
 #define HIP_OK(expr)                                                              \
@@ -86,7 +100,9 @@ constexpr uint32_t kWaveHits = kK1WaveHits;   // largest per-wave LDS hit buffer
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
 constexpr double kDenseFilesPerGB = 8000.0;   // upload segmentation: "many small files" (image layers: ~48k/GB)
-constexpr size_t kCntBytes = 1024;     // per-lane device counters: [0] cands, [1] K2 count, [2] overflow, [3] LDS-base error, [4 + g] K1 items of group g
+constexpr size_t kCntBytes = 1024;
+constexpr size_t kInlineConfirmFiles = 4;          // confirmations this small run on the calling thread
+constexpr uint64_t kInlineConfirmBytes = 512 << 10;     // per-lane device counters: [0] cands, [1] K2 count, [2] overflow, [3] LDS-base error, [4 + g] K1 items of group g
 constexpr int kItemChunks = 4;         // a K1 wave item: 64 lanes x (up to) 4 chunks
 
 // Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
@@ -104,6 +120,19 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // read only costs a redundant atomic.
 __device__ __forceinline__ void or_bits(uint32_t* w, uint32_t bits) {
   if (bits && (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bits) != bits) atomicOr(w, bits);
+}
+
+// At a file boundary inside a lane's range: no-return atomics only (the
+// lane's next file starts at once; a read-first or_bits would stall the whole
+// wave on an L2 round trip per word at every boundary)
+__device__ __forceinline__ void flush_kw_blind(uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t f,
+                                               unsigned long long& kw0, unsigned long long& kw1) {
+  uint32_t* w = kwbits + static_cast<size_t>(f) * kw_words;
+  if (static_cast<uint32_t>(kw0)) atomicOr(w + 0, static_cast<uint32_t>(kw0));
+  if (static_cast<uint32_t>(kw0 >> 32)) atomicOr(w + 1, static_cast<uint32_t>(kw0 >> 32));
+  if (static_cast<uint32_t>(kw1)) atomicOr(w + 2, static_cast<uint32_t>(kw1));
+  if (static_cast<uint32_t>(kw1 >> 32)) atomicOr(w + 3, static_cast<uint32_t>(kw1 >> 32));
+  kw0 = kw1 = 0;
 }
 
 __device__ __forceinline__ void flush_kw(uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t f,
@@ -295,11 +324,28 @@ __device__ __forceinline__ void k1_out_c(const K1Ctx& x, K1Stream& t, uint32_t s
   }
 }
 
+// measurement / layout bits for file boundaries inside a lane's range:
+// kAblBndRead keeps the read-first keyword flush (rounds 1-4; valid results);
+// kAblBndNoFlush drops the flush (invalid results: prices it)
+constexpr int kAblBndRead = 65536, kAblBndNoFlush = 131072;
+// measurement (results valid): per-workgroup and per-item wall-clock stamps
+// (s_memrealtime, 100 MHz) in the slack half of the deferred-output buffer,
+// copied to $TSG_K1_TRACE_FILE by the probe library (tools/k1_trace.py)
+constexpr int kAblTrace = 262144;
+constexpr uint32_t kTraceItemCap = 1u << 18;
+
 // One 16-byte word of one stream with file-boundary and stream-end checks.
-template <bool kC>
+template <int kAbl, bool kC>
 __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const v4u w, uint32_t S = 0) {
   const unsigned long long end = k1_end(x, t);
-  unsigned long long fend = x.offsets[t.f + 1];
+  // the current file's end from the stream state (lim = min(range end, file
+  // end)): a file ending at or past the range end never ends inside it.  (The
+  // offsets load this replaces cost every slow word an L2 round trip, four
+  // per boundary line, for the whole wave.)  The next file's end is fetched
+  // now if the file ends in this word, so its latency overlaps the bytes
+  // before the boundary.
+  unsigned long long fend = t.lim < end ? t.lim : ~0ull;
+  unsigned long long fnext = fend < end && fend < t.p + 16 ? x.offsets[t.f + 2] : ~0ull;   // (fend < end: file t.f + 1 < nfiles)
   if (x.primary && ((w.x | w.y | w.z | w.w) & 0x80808080u) && t.p >= t.emit) k1_special(x, t, w, fend, end);
   // rolled (the slow path runs on boundary and last lines only): unrolled, its
   // 16 copies of the per-byte branches held ~450 scalar values live and the
@@ -309,8 +355,13 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
     const unsigned long long q = t.p + k;
     if (q >= end) break;
     if (q >= fend) {
-      flush_kw(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
-      do { ++t.f; fend = x.offsets[t.f + 1]; } while (q >= fend);
+      if (kAbl & kAblBndNoFlush) t.kw0 = t.kw1 = 0;
+      else if (kAbl & kAblBndRead) flush_kw(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
+      else flush_kw_blind(x.kwmask, x.kw_words, t.f, t.kw0, t.kw1);
+      ++t.f;
+      fend = fnext;
+      while (q >= fend) { ++t.f; fend = x.offsets[t.f + 1]; }   // (empty files, files under 16 bytes)
+      fnext = fend < end && fend < t.p + 16 ? x.offsets[t.f + 2] : ~0ull;   // a second boundary in this word
       t.s = x.s0;
       t.p12 = 0;
     }
@@ -361,18 +412,32 @@ template <bool kStats>
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const unsigned long long* __restrict__ hits, const uint32_t* __restrict__ block_hits, uint32_t region_cap,
-    uint32_t nregions, const AnchorDev* __restrict__ anchors, const RuleDev* __restrict__ rules,
+    uint32_t nregions, uint32_t nsub_main, const unsigned long long* __restrict__ over_hits,
+    const uint32_t* __restrict__ over_cnt, uint32_t over_cap,
+    const AnchorDev* __restrict__ anchors, const RuleDev* __restrict__ rules,
     const uint32_t* __restrict__ rule_kw, const uint32_t* __restrict__ kwbits, uint32_t kw_words,
     const VDfaDev* __restrict__ vd, const uint16_t* __restrict__ v_next,
     const uint8_t* __restrict__ v_acc, const uint8_t* __restrict__ v_cls,
     CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap,
     unsigned long long* __restrict__ k2s) {
-  // K2 workgroup (r, k) verifies region r's hits k*256+tid, stride 256*(grid/nregions)
-  const uint32_t r = blockIdx.x % nregions;
-  const uint32_t nsub = gridDim.x / nregions;
-  const uint32_t nhits = min(block_hits[r], region_cap);
-  const unsigned long long* __restrict__ rh = hits + static_cast<size_t>(r) * region_cap;
-  for (uint32_t i = (blockIdx.x / nregions) * blockDim.x + threadIdx.x; i < nhits; i += nsub * blockDim.x) {
+  // The first nregions * nsub_main workgroups: workgroup (r, k) verifies K1
+  // region r's hits k*256+tid, stride 256*nsub_main; the rest verify the
+  // shared overflow pool the same way (one launch for both)
+  uint32_t nhits, sub, nsub;
+  const unsigned long long* __restrict__ rh;
+  if (blockIdx.x < nregions * nsub_main) {
+    const uint32_t r = blockIdx.x % nregions;
+    nhits = min(block_hits[r], region_cap);
+    rh = hits + static_cast<size_t>(r) * region_cap;
+    sub = blockIdx.x / nregions;
+    nsub = nsub_main;
+  } else {
+    nhits = min(*over_cnt, over_cap);
+    rh = over_hits;
+    sub = blockIdx.x - nregions * nsub_main;
+    nsub = gridDim.x - nregions * nsub_main;
+  }
+  for (uint32_t i = sub * blockDim.x + threadIdx.x; i < nhits; i += nsub * blockDim.x) {
     const unsigned long long h = rh[i];
     const unsigned long long q = h >> 24;
     const AnchorDev an = anchors[h & 0xffffffu];
@@ -720,6 +785,12 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
   constexpr uint32_t kTabOff = 256;
+  // kAblTrace: [4 per workgroup: entry, table loaded, exit, hw id][4 per item: start, end, wg << 8 | wave, kU]
+  uint32_t* const trc = obuf + static_cast<size_t>(gridDim.x) * kThreads * kOutSlots;
+  if ((kAbl & kAblTrace) && threadIdx.x == 0) {
+    trc[4 * blockIdx.x] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+    trc[4 * blockIdx.x + 3] = __smid();
+  }
   if (!(kAbl & kAblPtrAddr) && !k1_lds_base_ok(smem)) {   // the integer LDS addresses assume a zero base
     if (threadIdx.x == 0) atomicOr(over_cnt + 1, 1u);
     return;
@@ -774,8 +845,10 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   const unsigned long long n4 = nchunks - n1 - n2;
   const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
   const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
+  if ((kAbl & kAblTrace) && threadIdx.x == 0) trc[4 * blockIdx.x + 1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
   for (;;) {
     unsigned long long item = 0;
+    const uint32_t t_item = (kAbl & kAblTrace) ? static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) : 0u;
     if (lane == 0) {
       item = atomicAdd(item_ctr, 1u);
       *x.w_hitcnt = 0;
@@ -883,7 +956,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
                 else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, cw.x, cw.y, cw.z, cw.w);
               } else {
                 if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
-                k1_word_slow<kC>(x, t, cw, S);
+                k1_word_slow<kAbl, kC>(x, t, cw, S);
               }
             }
           }
@@ -912,7 +985,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
               else k1_word_v3<kAbl, kC>(x, t, ob, smem, S, v.x, v.y, v.z, v.w);
             } else {
               if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);   // before the word that may change the file
-              k1_word_slow<kC>(x, t, v, S);
+              k1_word_slow<kAbl, kC>(x, t, v, S);
             }
           }
         }
@@ -949,16 +1022,27 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if ((kAbl & kAblTrace) && lane == 0 && item < kTraceItemCap) {
+      uint32_t* r = trc + 4 * gridDim.x + 4 * item;
+      r[0] = t_item;
+      r[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+      r[2] = (blockIdx.x << 8) | wid;
+      r[3] = kU;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) block_hits[blockIdx.x] = s_block[0];
+  if ((kAbl & kAblTrace) && threadIdx.x == 0) trc[4 * blockIdx.x + 2] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
 }
 
-// K1 builds: the product's default (464, K1 and K1c).  The measurement
+// K1 builds: the product's default (4560, K1 and K1c: 464 until round 5,
+// plus the fast word step for the words of a boundary line that lie wholly
+// in one file -- config-1 files 250 MB launch 0.249 -> 0.229 ms, image-layer
+// files 0.277 -> 0.227 ms, config 2 unchanged, profiles/r5d_*).  The measurement
 // builds of the DESIGN.md 4.1 ablations (kAbl bits; tools/k1_probe.py
 // --variants 3:ABL) exist only in the probe library
 // (python -m trivy_amd.build --probe -> libtrivysecret_probe.so, -DTSG_K1_PROBE).
-constexpr int kK1Default = 464;
+constexpr int kK1Default = 4560;
 const void* k1_kernel(int abl, bool compressed) {
   if (compressed) {
     if (abl == kK1Default) return reinterpret_cast<const void*>(&tsg_k1_scan_v3<1024, kK1Default, true>);
@@ -974,8 +1058,10 @@ const void* k1_kernel(int abl, bool compressed) {
 #ifdef TSG_K1_PROBE
     TSG_K1_V3(0) TSG_K1_V3(16) TSG_K1_V3(18) TSG_K1_V3(20) TSG_K1_V3(24) TSG_K1_V3(32) TSG_K1_V3(48)
     TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448)
-    TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
-    TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4560) TSG_K1_V3(8656) TSG_K1_V3(12752)
+    TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
+    TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4592) TSG_K1_V3(8656) TSG_K1_V3(12752)
+    TSG_K1_V3(4562) TSG_K1_V3(5072) TSG_K1_V3(65536 + 4560) TSG_K1_V3(131072 + 4560) TSG_K1_V3(131072 + 4592)
+    TSG_K1_V3(262144 + 464) TSG_K1_V3(262144 + 4592) TSG_K1_V3(262144 + 4560)
 #endif
 #undef TSG_K1_V3
     default: return nullptr;
@@ -1008,11 +1094,14 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // Default K1 chunk for a launch of `bytes`.  K1 walks ranges of 1-4 chunks
 // per lane (guided schedule): its chunk is the '\n'-count granularity and the
 // last round's range: 2 KiB for launches of 2 GiB and more (measured r2r:
-// 3.34 vs 3.21 TB/s at 4 GB), else 1 KiB; batches under 8 MB (per-file Scan
-// batches of a few files) 256 B, so a one-workgroup launch spreads its bytes
-// over four times the lanes (a lane walks ~12 MB/s: a 1 KiB range is ~85 us).
+// 3.34 vs 3.21 TB/s at 4 GB), else 512 B (round 5: a 250 MB launch 0.249 ->
+// 0.231 ms, 1 GB 0.583 -> 0.529 ms against 1 KiB, profiles/r5a_*: the lanes
+// of a 125-250 MB launch each get a range instead of half of them one chunk);
+// batches under 8 MB (per-file Scan batches of a few files) 256 B, so a
+// one-workgroup launch spreads its bytes over more lanes (a lane walks ~13
+// MB/s: a 1 KiB range is ~80 us).
 uint32_t k1_chunk_for(uint64_t bytes) {
-  return bytes >= (2ull << 30) ? 2048 : bytes >= (8ull << 20) ? 1024 : 256;
+  return bytes >= (2ull << 30) ? 2048 : bytes >= (8ull << 20) ? 512 : 256;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -1047,7 +1136,8 @@ struct DeviceTables {
   uint8_t* v_acc = nullptr;
   uint8_t* v_cls = nullptr;
   uint32_t kw_words = 1;
-  std::mutex mu;                               // guards the lane pool
+  std::mutex mu;                               // guards the lane pool and lds_set
+  std::vector<std::pair<const void*, int>> lds_set;   // K1 builds whose dynamic-LDS limit is set (per device)
   std::vector<std::unique_ptr<Lane>> lanes;
   std::vector<Lane*> free_lanes;
   ~DeviceTables();
@@ -1076,15 +1166,33 @@ bool ensure_pinned(PinnedBuf* b, size_t bytes, std::string* err) {
   return true;
 }
 
+// Readbacks of one segment: dwords of device buffers into host-mapped
+// pinned buffers, queued together as one tsg_readback launch on stream s
+struct Readbacks {
+  RbList L{};
+  int n = 0;
+  size_t max_words = 0;
+  void add(const void* src, const PinnedBuf& b, size_t nwords, const uint32_t* d_count = nullptr, uint32_t per_count = 0) {
+    if (nwords == 0) return;
+    L.r[n++] = RbRegion{static_cast<const uint4*>(src), static_cast<uint4*>(b.d), d_count,
+                        static_cast<uint32_t>(nwords), per_count};
+    max_words = std::max(max_words, nwords);
+  }
+  bool launch(hipStream_t s, std::string* err) {
+    if (n == 0) return true;
+    const uint32_t blocks = static_cast<uint32_t>(std::min<size_t>(1024, (max_words / 4 + 256) / 256));
+    hipLaunchKernelGGL(tsg_readback, dim3(blocks, n), dim3(256), 0, s, L);
+    HIP_OK(hipGetLastError());
+    return true;
+  }
+};
+
 // dwords of src (device) into b (host-mapped) on stream s
 bool readback(const void* src, const PinnedBuf& b, size_t nwords, const uint32_t* d_count, uint32_t per_count,
               hipStream_t s, std::string* err) {
-  if (nwords == 0) return true;
-  const uint32_t blocks = static_cast<uint32_t>(std::min<size_t>(1024, (nwords / 4 + 256) / 256));
-  hipLaunchKernelGGL(tsg_readback, dim3(blocks), dim3(256), 0, s, static_cast<const uint4*>(src),
-                     static_cast<uint4*>(b.d), static_cast<uint32_t>(nwords), d_count, per_count);
-  HIP_OK(hipGetLastError());
-  return true;
+  Readbacks rb;
+  rb.add(src, b, nwords, d_count, per_count);
+  return rb.launch(s, err);
 }
 
 // Two drivers of one device (resident batches): each queues its segment's
@@ -1659,9 +1767,6 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint32_t sms = static_cast<uint32_t>(dt.sms);
   const Prefilter& pf = pf_;
   for (int attempt = 0; attempt < 3; ++attempt) {
-    HIP_OK(hipMemsetAsync(ln.d_kw, 0, kw_n * sizeof(uint32_t), s));
-    HIP_OK(hipMemsetAsync(ln.d_ff, 0, std::max<uint32_t>(in.nfiles, 1) * sizeof(uint32_t), s));
-    HIP_OK(hipMemsetAsync(ln.d_cnt, 0, kCntBytes, s));
     constexpr uint32_t nthr = 1024;
     const uint64_t want_blocks = (nchunks + nthr - 1) / nthr;
     // one resident workgroup per CU (the LDS table takes most of the CU's
@@ -1673,7 +1778,14 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     // one hit region per (group, workgroup); K2 walks all of them
     const uint32_t nregions = blocks * std::max<uint32_t>(ngroups, 1);
     const uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(ln.hit_cap / nregions, 0xffffffffu));
-    HIP_OK(hipMemsetAsync(ln.d_bh, 0, nregions * sizeof(uint32_t), s));
+    {
+      // keyword bits, file flags, counters, per-region hit counts: one launch
+      ClearList cl{{ln.d_kw, ln.d_ff, reinterpret_cast<uint32_t*>(ln.d_cnt), ln.d_bh},
+                   {static_cast<uint32_t>(kw_n), std::max<uint32_t>(in.nfiles, 1), static_cast<uint32_t>(kCntBytes / 4), nregions}};
+      const uint32_t mx = std::max(std::max(cl.n[0], cl.n[1]), std::max(cl.n[2], cl.n[3]));
+      hipLaunchKernelGGL(tsg_clear, dim3(std::min<uint32_t>(256, (mx + 255) / 256), 4), dim3(256), 0, s, cl);
+      HIP_OK(hipGetLastError());
+    }
     // per-wave LDS hit buffers as large as the group's table leaves room for
     // (512 entries for the builtin rules; large config-5 groups get fewer,
     // further hits go straight to the workgroup's global region)
@@ -1691,7 +1803,17 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       const void* kfn = k1_kernel(k1_abl_, g.compressed);
       if (!kfn) { *err = "unsupported K1 build (TSG_K1_ABL; the measurement builds are in the probe library)"; return false; }
       if (!g.in_lds || lds_of(g) > kLdsBytes) { *err = "K1 LDS budget exceeded"; return false; }
-      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_of(g))));
+      const int want = static_cast<int>(lds_of(g));
+      bool set = false;
+      {
+        std::lock_guard<std::mutex> lk(dt.mu);
+        for (const auto& e : dt.lds_set) set = set || (e.first == kfn && e.second >= want);
+      }
+      if (!set) {
+        HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, want));
+        std::lock_guard<std::mutex> lk(dt.mu);
+        dt.lds_set.emplace_back(kfn, want);
+      }
     }
     std::unique_lock<std::mutex> chain_lk;
     if (chain && attempt == 0) {
@@ -1739,7 +1861,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     bool rerun_k1 = false;
     for (int a2 = 0; a2 < 3 && !rerun_k1; ++a2) {
       if (!ensure(&ln.d_cands, &ln.d_cands_cap, ln.cand_cap, err)) return false;
-      HIP_OK(hipMemsetAsync(ln.d_cnt + 1, 0, 4, s));
+      if (a2 > 0) HIP_OK(hipMemsetAsync(ln.d_cnt + 1, 0, 4, s));   // (zeroed with the counters before K1)
       HIP_OK(hipEventRecord(ln.ev[2], s));
       const uint64_t per_block = 256ull * k2_hits_per_thread_;
       const uint64_t maxr_est = ln.k2_maxr_per_byte > 0 ? static_cast<uint64_t>(ln.k2_maxr_per_byte * total) + 1
@@ -1748,21 +1870,17 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       const uint32_t osub = static_cast<uint32_t>(std::max<uint64_t>(16, std::min<uint64_t>(4096, (ln.k2_over_est + 1023) / 1024)));
       const uint32_t ccap = static_cast<uint32_t>(ln.cand_cap);
       const uint32_t ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
-      // the region grid, then the overflow pool as one more region
+      // the region grid, then the overflow pool's workgroups, in one launch
       if (ln.d_k2s) {
-        hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
-                           ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
-                           dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
-        hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles, ln.d_over,
-                           ln.d_cnt + 2, ocap, 1u, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa,
-                           dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+        hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub + osub), dim3(256), 0, s, d_data, d_off,
+                           in.nfiles, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over, ln.d_cnt + 2, ocap,
+                           dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc,
+                           dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
       } else {
-        hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub), dim3(256), 0, s, d_data, d_off, in.nfiles,
-                           ln.d_hits, ln.d_bh, region_cap, nregions, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw,
-                           dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
-        hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(osub), dim3(256), 0, s, d_data, d_off, in.nfiles, ln.d_over,
-                           ln.d_cnt + 2, ocap, 1u, dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa,
-                           dt.v_next, dt.v_acc, dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+        hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub + osub), dim3(256), 0, s, d_data, d_off,
+                           in.nfiles, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over, ln.d_cnt + 2, ocap,
+                           dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc,
+                           dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
       }
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));
@@ -1782,13 +1900,14 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       if (!ensure_pinned(&ln.rb_bh, nregions * sizeof(uint32_t), err) || !ensure_pinned(&ln.rb_c2, 16, err) ||
           !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
           !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err) ||
-          !ensure_pinned(&ln.rb_cands, ln.cand_cap * sizeof(CandDev), err) ||
-          !readback(ln.d_bh, ln.rb_bh, nregions, nullptr, 0, s, err) ||
-          !readback(ln.d_cnt, ln.rb_c2, 4, nullptr, 0, s, err) ||
-          !readback(ln.d_ff, ln.rb_ff, in.nfiles, nullptr, 0, s, err) ||
-          !readback(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2, nullptr, 0, s, err) ||
-          !readback(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4,
-                    s, err)) return false;
+          !ensure_pinned(&ln.rb_cands, ln.cand_cap * sizeof(CandDev), err)) return false;
+      Readbacks rb;
+      rb.add(ln.d_bh, ln.rb_bh, nregions);
+      rb.add(ln.d_cnt, ln.rb_c2, 4);
+      rb.add(ln.d_ff, ln.rb_ff, in.nfiles);
+      rb.add(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2);
+      rb.add(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4);
+      if (!rb.launch(s, err)) return false;
       if (chain) {
         // polled with short sleeps: a blocking-sync event woke its driver
         // 0.3-1.2 ms after the passes ended (profiles/rd5e_bench_c2prof.log)
@@ -1845,6 +1964,24 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
                      "copy-out %.3f ms, total %.3f ms\n", total / 1e6, in.nfiles, t_k1_sync, k1, k2, nregions * nsub,
                      osub, ms_since(t_d2h), ms_since(t_seg0));
       st->candidates += c2;
+#ifdef TSG_K1_PROBE
+      if (k1_abl_ & kAblTrace) {
+        // probe builds: the K1 launch's stamps (kAblTrace) appended to
+        // $TSG_K1_TRACE_FILE as [blocks, items, nchunks, chunk][4 x blocks][4 x items] uint32
+        const uint32_t items = static_cast<uint32_t>(std::min<uint64_t>(kTraceItemCap, 3 * (nchunks + 63) / 64 + 64));
+        std::vector<uint32_t> tr(4 + 4 * static_cast<size_t>(blocks) + 4 * static_cast<size_t>(items), 0);
+        tr[0] = blocks; tr[1] = items; tr[2] = static_cast<uint32_t>(nchunks); tr[3] = kChunk;
+        HIP_OK(hipMemcpy(tr.data() + 4, ln.d_ob + static_cast<size_t>(blocks) * nthr * kOutSlots,
+                         (tr.size() - 4) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (const char* fn = std::getenv("TSG_K1_TRACE_FILE")) {
+          if (FILE* fp = std::fopen(fn, "ab")) {
+            std::fwrite(tr.data(), sizeof(uint32_t), tr.size(), fp);
+            std::fclose(fp);
+          }
+        }
+        HIP_OK(hipMemset(ln.d_ob + static_cast<size_t>(blocks) * nthr * kOutSlots, 0, (tr.size() - 4) * sizeof(uint32_t)));
+      }
+#endif
       if (ln.d_k2s) {
         std::vector<unsigned long long> h(kK2Stat * pf_.rules.size());
         HIP_OK(hipMemcpy(h.data(), ln.d_k2s, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -2128,13 +2265,20 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
     nconf.fetch_add(my_conf);
     nfind.fetch_add(my_find);
   };
-  const int nt = cc.pool->size();
+  // small confirmations (a few files, little text: per-file Scan batches) run
+  // on this thread; waking the pool costs more than the work
+  uint64_t work_bytes = 0;
+  for (size_t k = 0; k < work.size() && work_bytes <= kInlineConfirmBytes; ++k)
+    work_bytes += in.offsets[work[k] + 1] - in.offsets[work[k]];
+  const bool inline_confirm = work.size() <= kInlineConfirmFiles && work_bytes <= kInlineConfirmBytes &&
+                              light.size() <= kLightBlock;
+  const int nt = inline_confirm ? 1 : cc.pool->size();
   // while GPU passes are in flight one core stays with each thread driving
   // them (a preempted driver thread stalls its GPU)
   const int active = gpu_in_flight && nt > 1 ? nt - 1 : nt;
   const double t_setup = ms_since(t_begin);
   std::atomic<uint64_t> work_us{0}, light_us{0};
-  cc.pool->run([&](int idx) {
+  auto body = [&](int idx) {
     if (idx >= active) return;
     auto a = std::chrono::steady_clock::now();
     worker();
@@ -2142,7 +2286,9 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
     light_files();
     work_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(b - a).count());
     light_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - b).count());
-  });
+  };
+  if (inline_confirm) body(0);
+  else cc.pool->run(body);
   if (host_profile_) {
     uint64_t ph[5];
     for (int k = 0; k < 5; ++k) ph[k] = g_scan_prof[k].exchange(0);
@@ -2466,12 +2612,17 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
   uint64_t nconf = 0, nfind = 0;
   double host_ms = 0;
   std::string host_err;
+  // one segment on one device (per-file Scan batches, small batches): the
+  // driver runs on this thread -- a thread start and hand-off cost more than
+  // the segment's GPU passes
+  const bool inline_driver = segs.size() == 1 && drivers.size() == 1;
   try {
-    for (DeviceTables* dt : drivers) threads.emplace_back(driver, dt);
+    if (!inline_driver) for (DeviceTables* dt : drivers) threads.emplace_back(driver, dt);
     // per-file result slots (hundreds of thousands for image layers) are set up
     // while the first segment's upload and GPU passes run
     results->clear();
     results->resize(in.nfiles);
+    if (inline_driver) driver(drivers[0]);
     if (host_profile_) std::fprintf(stderr, "[tsg tl] %u result slots ready at %.3f ms\n", in.nfiles, ms_since(t_feed0));
     for (;;) {
       int left = 0;

@@ -3,9 +3,11 @@
 
 #include <array>
 #include "gosort.h"
+#include "guard.h"
 #include "prefilter.h"
 
 #include <algorithm>
+#include <atomic>
 #include <emmintrin.h>
 #include <chrono>
 #include <cstring>
@@ -1021,13 +1023,14 @@ void SecretVec::resize(size_t n) {
   if (nt <= 1) {
     for (size_t i = n_; i < n; ++i) new (p_ + i) Secret();
   } else {
-    std::vector<std::thread> ts;
     const size_t per = (add + nt - 1) / nt;
-    for (size_t t = 0; t < nt; ++t) {
-      const size_t a = n_ + t * per, b = std::min(n, a + per);
-      ts.emplace_back([this, a, b] { for (size_t i = a; i < b; ++i) new (p_ + i) Secret(); });
-    }
-    for (auto& t : ts) t.join();
+    std::atomic<size_t> next{0};
+    run_threads(static_cast<int>(nt), [&] {
+      for (size_t t; (t = next.fetch_add(1)) < nt;) {
+        const size_t a = n_ + t * per, b = std::min(n, a + per);
+        for (size_t i = a; i < b; ++i) new (p_ + i) Secret();
+      }
+    });
   }
   n_ = n;
 }
