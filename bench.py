@@ -1016,7 +1016,11 @@ def main():
                 if isinstance(v, dict):
                     v["vs_cpu_baseline_cxx"] = round(v["gbps"] / (nb / cdt / 1e9), 2)
         out["parity"] = {"sample_files": len(idx), "sample_bytes": nb, "sample_findings": ofind,
-                         "diff_files": len(diff), "diff_examples": diff[:5], "cxx_diff_files": cdiff}
+                         "sample_share": round(nb / max(batch.nbytes, 1), 4),
+                         "sample_files_share": round(len(idx) / max(batch.nfiles, 1), 4),
+                         "diff_files": len(diff), "diff_examples": diff[:5], "cxx_diff_files": cdiff,
+                         "note": "the oracle checks this seeded sample of the step's batch (half of it files above "
+                                 "8 MB); the rest of the batch is covered by the GPU parity tests at smaller sizes"}
         failed = bool(diff) or cdiff > 0
         log("cpu baseline %.4f GB/s (oracle, %d procs), %.4f GB/s (C++ restatement, %d threads); "
             "parity diff files: %d (findings in sample: %d)" % (

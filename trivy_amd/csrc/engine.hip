@@ -41,9 +41,6 @@ namespace {
 
 constexpr uint32_t kLdsBytes = 160 * 1024;     // LDS per CU
 
-struct AnchorDev { uint32_t rule, min_len, max_len, dmin, dmax; };
-struct RuleDev { uint32_t mode, gate_on_gpu, always_gate, kw_begin, kw_count, verify_dfa, verify_limit, rev_dfa; };
-struct VDfaDev { uint32_t next_off, acc_off, cls_off, nclasses, dead, pad0, pad1, pad2; };
 struct CandDev { uint32_t file, rule; unsigned long long start; };
 
 // Readback of a segment's results into host-mapped, fine-grained pinned
@@ -408,16 +405,61 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
 // bytes, the most verify bytes of one hit
 constexpr uint32_t kK2Stat = 5;
 
+// K2's per-anchor record (built on the host from AnchorInfo, RuleGpuInfo and
+// the rule's verify / reverse DFA): everything a hit needs in four 16-byte
+// loads issued together (rounds 1-4 walked anchor -> rule -> DFA records, three
+// dependent L2 round trips before the first verify byte).
+struct K2Anchor {
+  uint32_t rule, min_len, max_len, dmin;
+  uint32_t dmax, flags, kw_begin, kw_count;     // flags: mode | gate_on_gpu << 8 | always_gate << 9 | acc0 << 10 | racc0 << 11
+  uint32_t verify_limit, v_next, v_cls, v_ncls_dead;   // ncls | dead << 16
+  uint32_t r_next, r_cls, r_ncls_dead, kw0;     // reverse DFA (mode 4); kw0 = the rule's first keyword id
+};
+static_assert(sizeof(K2Anchor) == 64, "K2Anchor is four 16-byte loads");
+// verify DFA transitions: next state | accepting << 15 (the accept flag rides
+// with the state: one dependent load per byte instead of two)
+constexpr uint32_t kVAcc = 0x8000u, kVState = 0x7fffu;
+
+// The file of segment offset q from K1's per-chunk file (a lower bound: the
+// file of the chunk's first byte or one before it), stepped forward; a chunk
+// of many tiny files falls back to a binary search above the bound.
+__device__ __forceinline__ uint32_t k2_file_of(const uint64_t* __restrict__ off, uint32_t nfiles,
+                                               const uint32_t* __restrict__ chunk_file, uint32_t chunk,
+                                               unsigned long long q) {
+  uint32_t f = chunk_file[q / chunk];
+  for (int k = 0; k < 4; ++k) {
+    if (f >= nfiles || off[f + 1] > q) return f;
+    ++f;
+  }
+  uint32_t lo = f, hi = nfiles;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi + 1) >> 1;
+    if (off[m] <= q) lo = m; else hi = m - 1;
+  }
+  f = lo;
+  while (f < nfiles && off[f + 1] <= q) ++f;
+  return f;
+}
+
+// K2: one thread per anchor hit.  The rule's keyword gate (K1's per-file
+// bits), then the anchored relaxed verify DFA from every start the anchor's
+// offset window allows (mode 0), or from every start a backward walk of the
+// reverse DFA accepts (mode 4); mode 3 hits are presence candidates.
+// Forward walks from up to kK2Walk starts run interleaved: their byte chains
+// are independent, so one thread keeps kK2Walk dependent L2 round trips in
+// flight instead of one.
+constexpr int kK2Walk = 4;
+
 template <bool kStats>
 __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
+    const uint32_t* __restrict__ chunk_file, uint32_t chunk,
     const unsigned long long* __restrict__ hits, const uint32_t* __restrict__ block_hits, uint32_t region_cap,
     uint32_t nregions, uint32_t nsub_main, const unsigned long long* __restrict__ over_hits,
     const uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    const AnchorDev* __restrict__ anchors, const RuleDev* __restrict__ rules,
-    const uint32_t* __restrict__ rule_kw, const uint32_t* __restrict__ kwbits, uint32_t kw_words,
-    const VDfaDev* __restrict__ vd, const uint16_t* __restrict__ v_next,
-    const uint8_t* __restrict__ v_acc, const uint8_t* __restrict__ v_cls,
+    const K2Anchor* __restrict__ anchors, const uint32_t* __restrict__ rule_kw,
+    const uint32_t* __restrict__ kwbits, uint32_t kw_words,
+    const uint16_t* __restrict__ v_next, const uint8_t* __restrict__ v_cls,
     CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap,
     unsigned long long* __restrict__ k2s) {
   // The first nregions * nsub_main workgroups: workgroup (r, k) verifies K1
@@ -440,37 +482,11 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
   for (uint32_t i = sub * blockDim.x + threadIdx.x; i < nhits; i += nsub * blockDim.x) {
     const unsigned long long h = rh[i];
     const unsigned long long q = h >> 24;
-    const AnchorDev an = anchors[h & 0xffffffu];
-    const RuleDev r = rules[an.rule];
-    const uint32_t f = file_of(offsets, nfiles, q);
+    const K2Anchor an = anchors[h & 0xffffffu];
+    const uint32_t f = k2_file_of(offsets, nfiles, chunk_file, chunk, q);
+    const uint32_t mode = an.flags & 0xffu;
     if (kStats) atomicAdd(&k2s[kK2Stat * an.rule], 1ull);
-    if (r.mode == 3) {
-      // presence anchor of a rule evaluated in full on the host: the hit is
-      // the candidate (any one per file suffices)
-      const unsigned int idx = atomicAdd(&counters[1], 1u);
-      if (idx < cand_cap) {
-        cands[idx].file = f;
-        cands[idx].rule = an.rule;
-        cands[idx].start = q - offsets[f];
-      }
-      continue;
-    }
-    if (!r.always_gate && r.gate_on_gpu) {
-      uint32_t g = 0;
-      for (uint32_t k = 0; k < r.kw_count && !g; ++k) {
-        const uint32_t id = rule_kw[r.kw_begin + k];
-        g = (kwbits[static_cast<size_t>(f) * kw_words + (id >> 5)] >> (id & 31)) & 1u;
-      }
-      if (!g) continue;
-    }
-    if (kStats) atomicAdd(&k2s[kK2Stat * an.rule + 1], 1ull);
-    const long long fstart = static_cast<long long>(offsets[f]);
-    const long long fend = static_cast<long long>(offsets[f + 1]);
-    unsigned long long hit_bytes = 0;
-    const VDfaDev d = vd[r.verify_dfa];
-    const uint16_t* nx = v_next + d.next_off;
-    const uint8_t* acc = v_acc + d.acc_off;
-    const uint8_t* cl = v_cls + d.cls_off;
+    const unsigned long long fstart_u = offsets[f];
     auto emit = [&](unsigned long long start) {
       const unsigned int idx = atomicAdd(&counters[1], 1u);
       if (idx < cand_cap) {
@@ -479,63 +495,118 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
         cands[idx].start = start;
       }
     };
-    // anchored verify DFA from s: does a prefix of the text from s lie in the
-    // rule's relaxed language?
-    // the text is read 16 aligned bytes at a time (the batch is 16-byte
-    // aligned with 64 readable bytes past its end): one memory round trip per
-    // 16 steps instead of one per byte next to the table's
-    auto verify = [&](long long s) {
-      uint32_t st = 0;
-      bool ok = acc[0] != 0;
-      long long p = s;
-      const long long lim = min(fend, s + static_cast<long long>(r.verify_limit));
-      long long wb = -1;
-      v4u win{0, 0, 0, 0};
-      for (; !ok && p < lim; ++p) {
-        if ((p & ~15ll) != wb) {
-          wb = p & ~15ll;
-          win = *reinterpret_cast<const v4u*>(data + wb);
+    if (mode == 3) {
+      // presence anchor of a rule evaluated in full on the host: the hit is
+      // the candidate (any one per file suffices)
+      emit(q - fstart_u);
+      continue;
+    }
+    if (!(an.flags & 0x200u) && (an.flags & 0x100u)) {
+      // keyword gate: any of the rule's keywords in the file (K1's bits)
+      const uint32_t* kb = kwbits + static_cast<size_t>(f) * kw_words;
+      uint32_t g = an.kw_count ? (kb[an.kw0 >> 5] >> (an.kw0 & 31)) & 1u : 0u;
+      for (uint32_t k = 1; k < an.kw_count && !g; ++k) {
+        const uint32_t id = rule_kw[an.kw_begin + k];
+        g = (kb[id >> 5] >> (id & 31)) & 1u;
+      }
+      if (!g) continue;
+    }
+    if (kStats) atomicAdd(&k2s[kK2Stat * an.rule + 1], 1ull);
+    const long long fstart = static_cast<long long>(fstart_u);
+    const long long fend = static_cast<long long>(offsets[f + 1]);
+    unsigned long long hit_bytes = 0;
+    const uint16_t* nx = v_next + an.v_next;
+    const uint8_t* cl = v_cls + an.v_cls;
+    const uint32_t ncls = an.v_ncls_dead & 0xffffu, dead = an.v_ncls_dead >> 16;
+    const bool acc0 = (an.flags & 0x400u) != 0;
+    // up to kK2Walk anchored verify walks from starts s0 .. s0+n-1 (ascending),
+    // interleaved; *res bit j: a prefix of the text from start j lies in the
+    // rule's relaxed language (or the walk gave up alive at its byte limit:
+    // conservative)
+    auto verify_n = [&](const long long* st0, int n) -> uint32_t {
+      uint32_t res = 0, live = 0;
+      uint32_t stt[kK2Walk];
+      long long p[kK2Walk], lim[kK2Walk];
+#pragma unroll
+      for (int j = 0; j < kK2Walk; ++j) {
+        stt[j] = 0;
+        p[j] = j < n ? st0[j] : 0;
+        lim[j] = j < n ? min(fend, p[j] + static_cast<long long>(an.verify_limit)) : 0;
+        if (j < n) {
+          if (acc0) res |= 1u << j;
+          else if (p[j] < lim[j]) live |= 1u << j;
+          else if (lim[j] < fend && dead != 0) res |= 1u << j;   // a zero byte limit before the file end: gave up alive
         }
-        const uint32_t wd = (p & 8) ? ((p & 4) ? win.w : win.z) : ((p & 4) ? win.y : win.x);
-        st = nx[st * d.nclasses + cl[(wd >> ((p & 3) * 8)) & 0xffu]];
-        if (acc[st]) ok = true;
-        else if (st == d.dead) break;
+      }
+      while (live) {
+        uint32_t b[kK2Walk];
+#pragma unroll
+        for (int j = 0; j < kK2Walk; ++j) b[j] = (live >> j) & 1u ? data[p[j]] : 0u;
+        uint32_t c[kK2Walk];
+#pragma unroll
+        for (int j = 0; j < kK2Walk; ++j) c[j] = cl[b[j]];
+#pragma unroll
+        for (int j = 0; j < kK2Walk; ++j) {
+          if (!((live >> j) & 1u)) continue;
+          const uint32_t e = nx[stt[j] * ncls + c[j]];
+          stt[j] = e & kVState;
+          ++p[j];
+          if (kStats) hit_bytes += 1;
+          if (e & kVAcc) { res |= 1u << j; live &= ~(1u << j); }
+          else if (stt[j] == dead) live &= ~(1u << j);
+          else if (p[j] >= lim[j]) {
+            live &= ~(1u << j);
+            if (p[j] < fend) res |= 1u << j;           // gave up alive at the byte limit: conservative
+          }
+        }
       }
       if (kStats) {
-        atomicAdd(&k2s[kK2Stat * an.rule + 2], 1ull);
-        atomicAdd(&k2s[kK2Stat * an.rule + 3], static_cast<unsigned long long>(p - s + 1));
-        hit_bytes += static_cast<unsigned long long>(p - s + 1);
+        atomicAdd(&k2s[kK2Stat * an.rule + 2], static_cast<unsigned long long>(n));
       }
-      if (!ok && st != d.dead && p < fend && p >= lim) ok = true;   // gave up: conservative
-      return ok;
+      return res;
     };
-    if (r.mode == 4) {
+    if (mode == 4) {
       // reverse-anchored: walk the reverse DFA backwards from the hit's last
       // byte; every accepting position may start a match and is verified
       // forwards.  A walk still alive after kRevLimit bytes gives up: the
       // host evaluates the rule on the whole file (kFullScanStart).
-      const VDfaDev rd = vd[r.rev_dfa];
-      const uint16_t* rnx = v_next + rd.next_off;
-      const uint8_t* racc = v_acc + rd.acc_off;
-      const uint8_t* rcl = v_cls + rd.cls_off;
+      const uint16_t* rnx = v_next + an.r_next;
+      const uint8_t* rcl = v_cls + an.r_cls;
+      const uint32_t rncls = an.r_ncls_dead & 0xffffu, rdead = an.r_ncls_dead >> 16;
       uint32_t st = 0;
-      for (long long p = static_cast<long long>(q); p >= fstart; --p) {
-        if (static_cast<long long>(q) - p >= static_cast<long long>(kRevLimit)) { emit(kFullScanStart); break; }
-        st = rnx[st * rd.nclasses + rcl[data[p]]];
+      for (long long pp = static_cast<long long>(q); pp >= fstart; --pp) {
+        if (static_cast<long long>(q) - pp >= static_cast<long long>(kRevLimit)) { emit(kFullScanStart); break; }
+        const uint32_t e = rnx[st * rncls + rcl[data[pp]]];
+        st = e & kVState;
         if (kStats) ++hit_bytes;
-        if (st == rd.dead) break;
-        if (racc[st] && verify(p)) emit(static_cast<unsigned long long>(p - fstart));
+        if (st == rdead) break;
+        if (e & kVAcc) {
+          const long long s1 = pp;
+          if (verify_n(&s1, 1) & 1u) emit(static_cast<unsigned long long>(pp - fstart));
+        }
       }
-      if (kStats) atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
+      if (kStats) {
+        atomicAdd(&k2s[kK2Stat * an.rule + 3], hit_bytes);
+        atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
+      }
       continue;
     }
     long long hi = static_cast<long long>(q) + 1 - an.min_len - an.dmin;
     long long lo = static_cast<long long>(q) + 1 - an.max_len - an.dmax;
     if (lo < fstart) lo = fstart;
-    for (long long s = lo; s <= hi; ++s) {
-      if (verify(s)) emit(static_cast<unsigned long long>(s - fstart));
+    for (long long s0 = lo; s0 <= hi; s0 += kK2Walk) {
+      long long st0[kK2Walk];
+      const int n = static_cast<int>(min(static_cast<long long>(kK2Walk), hi - s0 + 1));
+#pragma unroll
+      for (int j = 0; j < kK2Walk; ++j) st0[j] = s0 + j;
+      const uint32_t res = verify_n(st0, n);
+      for (int j = 0; j < n; ++j)
+        if ((res >> j) & 1u) emit(static_cast<unsigned long long>(s0 + j - fstart));
     }
-    if (kStats) atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
+    if (kStats) {
+      atomicAdd(&k2s[kK2Stat * an.rule + 3], hit_bytes);
+      atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
+    }
   }
 }
 
@@ -780,8 +851,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     uint32_t* __restrict__ kwbits, uint32_t kw_words, uint32_t kw_base, uint32_t primary,
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
-    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ fflags, uint32_t* __restrict__ item_ctr,
-    uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
+    uint16_t* __restrict__ nl_count, uint32_t* __restrict__ chunk_file, uint32_t* __restrict__ fflags,
+    uint32_t* __restrict__ item_ctr, uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
   constexpr uint32_t kTabOff = 256;
@@ -870,6 +941,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
       t.end = min(min(c + kU, rend) * chunk, total);
       t.cend = min(t.emit + chunk, t.end);
       t.ci = c;
+      if (x.primary) chunk_file[c] = t.f;            // K2's file lookup: a file at or before the chunk's first byte
       if (t.p < t.end) t.lim = min(t.end, x.offsets[t.f + 1]);
       OutBuf ob{obuf + blockIdx.x * kThreads + threadIdx.x, gridDim.x * kThreads, 0};
       constexpr int kW = (kAbl & kAblLine64) ? 4 : 8;     // words per line
@@ -882,6 +954,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
           if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);   // count before any byte of the next
           t.nl = 0;
           ++t.ci;
+          if (x.primary) chunk_file[t.ci] = t.f;        // (a lower bound of the chunk's first file: K2)
           t.cend = min(t.cend + chunk, t.end);
         }
         // a whole line inside the lane's range is loaded (and the next one
@@ -942,6 +1015,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
                 if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
                 t.nl = 0;
                 ++t.ci;
+                if (x.primary) chunk_file[t.ci] = t.f;        // (a lower bound of the chunk's first file: K2)
                 t.cend = min(t.cend + chunk, t.end);
               }
               // (the word by selects, not by an indexed register array: the
@@ -975,6 +1049,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
               if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);
               t.nl = 0;
               ++t.ci;
+              if (x.primary) chunk_file[t.ci] = t.f;        // (a lower bound of the chunk's first file: K2)
               t.cend = min(t.cend + chunk, t.end);
             }
             const v4u v = *reinterpret_cast<const v4u*>(data + t.p);
@@ -1128,12 +1203,9 @@ struct DeviceTables {
   int device = 0;
   int sms = 256;
   std::vector<K1Group> k1g;
-  AnchorDev* anchors = nullptr;
-  RuleDev* rules = nullptr;
+  K2Anchor* anchors = nullptr;                 // K2's per-anchor records
   uint32_t* rule_kw = nullptr;
-  VDfaDev* vdfa = nullptr;
   uint16_t* v_next = nullptr;
-  uint8_t* v_acc = nullptr;
   uint8_t* v_cls = nullptr;
   uint32_t kw_words = 1;
   std::mutex mu;                               // guards the lane pool and lds_set
@@ -1234,6 +1306,7 @@ struct Lane {
   uint32_t* d_bh = nullptr; size_t d_bh_cap = 0;    // hits written per K1 workgroup (its region of d_hits)
   CandDev* d_cands = nullptr; size_t d_cands_cap = 0;
   uint16_t* d_nl = nullptr; size_t d_nl_cap = 0;   // '\n' per K1 chunk (chunk <= 32 KiB)
+  uint32_t* d_cf = nullptr; size_t d_cf_cap = 0;   // per K1 chunk: a file at or before its first byte (K2's file lookup)
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   uint32_t* d_ob = nullptr; size_t d_ob_cap = 0;    // K1 v3 deferred-output slots (kOutSlots per thread)
   unsigned long long* d_k2s = nullptr;              // TSG_K2_STATS: per-rule K2 counters (4 per rule)
@@ -1302,7 +1375,7 @@ struct Engine::Segment {
 DeviceTables::~DeviceTables() {
   hipSetDevice(device);
   lanes.clear();
-  void* ps[] = {anchors, rules, rule_kw, vdfa, v_next, v_acc, v_cls};
+  void* ps[] = {anchors, rule_kw, v_next, v_cls};
   for (void* p : ps) if (p) hipFree(p);
   for (K1Group& g : k1g) {
     void* gs[] = {g.next, g.cls, g.meta, g.list};
@@ -1316,7 +1389,7 @@ Lane::~Lane() {
   if (copy) hipStreamSynchronize(copy);
   for (uint64_t* h : h_off_pin) if (h) hipHostFree(h);
   for (PinnedBuf* b : {&rb_bh, &rb_c2, &rb_cands, &rb_ff, &rb_nl}) if (b->p) hipHostFree(b->p);
-  void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_ff, d_ob, d_cnt, d_k2s, d_cr};
+  void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_cf, d_ff, d_ob, d_cnt, d_k2s, d_cr};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
   if (ev_sync) hipEventDestroy(ev_sync);
@@ -1481,28 +1554,43 @@ bool build_tables(const Prefilter& pf, DeviceTables* dt, std::string* err) {
     dt->kw_words = std::max<uint32_t>(dt->kw_words, g.kw_base / 32 + 4);   // a group's masks span 4 words from kw_base
     dt->k1g.push_back(g);
   }
-  std::vector<AnchorDev> an;
-  for (const auto& a : pf.anchors) an.push_back({a.rule, a.min_len, a.max_len, a.dmin, a.dmax});
-  std::vector<RuleDev> rd;
-  for (const auto& r : pf.rules) rd.push_back({r.mode, r.gate_on_gpu, r.always_gate, r.kw_begin, r.kw_count, r.verify_dfa, r.verify_limit, r.rev_dfa});
-  std::vector<VDfaDev> vd;
+  // K2: the verify DFAs' transitions with the accept flag in bit 15, and
+  // one record per anchor (its rule's fields and DFA offsets inline)
   std::vector<uint16_t> vn;
-  std::vector<uint8_t> va, vc;
+  std::vector<uint8_t> vc;
+  std::vector<uint32_t> v_next_off, v_cls_off;
   for (const auto& t : pf.verify) {
-    VDfaDev d{};
-    d.next_off = static_cast<uint32_t>(vn.size());
-    d.acc_off = static_cast<uint32_t>(va.size());
-    d.cls_off = static_cast<uint32_t>(vc.size());
-    d.nclasses = t.nclasses;
-    d.dead = t.dead;
-    vn.insert(vn.end(), t.next.begin(), t.next.end());
-    va.insert(va.end(), t.accept.begin(), t.accept.end());
+    if (t.nstates > kVState || t.nclasses > 0xffff || t.dead > 0xffff) { *err = "verify DFA too large for K2's records"; return false; }
+    v_next_off.push_back(static_cast<uint32_t>(vn.size()));
+    v_cls_off.push_back(static_cast<uint32_t>(vc.size()));
+    for (uint16_t x : t.next) vn.push_back(static_cast<uint16_t>(x | (t.accept[x] ? kVAcc : 0u)));
     vc.insert(vc.end(), t.byte_class, t.byte_class + 256);
-    vd.push_back(d);
   }
-  return dev_upload(an, &dt->anchors, err) && dev_upload(rd, &dt->rules, err) &&
-         dev_upload(pf.rule_kw, &dt->rule_kw, err) && dev_upload(vd, &dt->vdfa, err) &&
-         dev_upload(vn, &dt->v_next, err) && dev_upload(va, &dt->v_acc, err) && dev_upload(vc, &dt->v_cls, err);
+  std::vector<K2Anchor> an;
+  for (const auto& a : pf.anchors) {
+    const RuleGpuInfo& r = pf.rules[a.rule];
+    K2Anchor k{};
+    k.rule = a.rule; k.min_len = a.min_len; k.max_len = a.max_len; k.dmin = a.dmin; k.dmax = a.dmax;
+    k.kw_begin = r.kw_begin; k.kw_count = r.kw_count;
+    k.kw0 = r.kw_count ? pf.rule_kw[r.kw_begin] : 0;
+    k.verify_limit = r.verify_limit;
+    uint32_t flags = r.mode | (r.gate_on_gpu ? 0x100u : 0u) | (r.always_gate ? 0x200u : 0u);
+    if (r.mode == 0 || r.mode == 4) {
+      const DfaTable& v = pf.verify[r.verify_dfa];
+      k.v_next = v_next_off[r.verify_dfa]; k.v_cls = v_cls_off[r.verify_dfa];
+      k.v_ncls_dead = v.nclasses | (v.dead << 16);
+      if (!v.accept.empty() && v.accept[0]) flags |= 0x400u;
+    }
+    if (r.mode == 4) {
+      const DfaTable& v = pf.verify[r.rev_dfa];
+      k.r_next = v_next_off[r.rev_dfa]; k.r_cls = v_cls_off[r.rev_dfa];
+      k.r_ncls_dead = v.nclasses | (v.dead << 16);
+    }
+    k.flags = flags;
+    an.push_back(k);
+  }
+  return dev_upload(an, &dt->anchors, err) && dev_upload(pf.rule_kw, &dt->rule_kw, err) &&
+         dev_upload(vn, &dt->v_next, err) && dev_upload(vc, &dt->v_cls, err);
 }
 
 // Device of a device pointer (-1: not a device allocation).
@@ -1752,6 +1840,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   if (!ensure(&ln.d_kw, &ln.d_kw_cap, kw_n, err)) return false;
   const unsigned long long nchunks = (total + kChunk - 1) / kChunk;
   if (!ensure(&ln.d_nl, &ln.d_nl_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
+  if (!ensure(&ln.d_cf, &ln.d_cf_cap, std::max<unsigned long long>(nchunks, 1), err)) return false;
   ln.hit_cap = std::max<size_t>(ln.hit_cap, total / 256);   // ~1 hit per 670 B on source text
   if (!ensure(&ln.d_hits, &ln.d_hits_cap, ln.hit_cap, err)) return false;
   ln.over_cap = std::max<size_t>(ln.over_cap, total / 2048);
@@ -1847,7 +1936,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       void* args[] = {&a_data, &a_total, &d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
-                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
+                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_cf, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
       HIP_OK(hipLaunchKernel(k1_kernel(k1_abl_, g.compressed), dim3(blocks), dim3(nthr), args, lds, s));
       ++launches;
     }
@@ -1873,14 +1962,14 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       // the region grid, then the overflow pool's workgroups, in one launch
       if (ln.d_k2s) {
         hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub + osub), dim3(256), 0, s, d_data, d_off,
-                           in.nfiles, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over, ln.d_cnt + 2, ocap,
-                           dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc,
-                           dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+                           in.nfiles, ln.d_cf, kChunk, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over,
+                           ln.d_cnt + 2, ocap, dt.anchors, dt.rule_kw, ln.d_kw, dt.kw_words, dt.v_next, dt.v_cls,
+                           ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
       } else {
         hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub + osub), dim3(256), 0, s, d_data, d_off,
-                           in.nfiles, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over, ln.d_cnt + 2, ocap,
-                           dt.anchors, dt.rules, dt.rule_kw, ln.d_kw, dt.kw_words, dt.vdfa, dt.v_next, dt.v_acc,
-                           dt.v_cls, ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+                           in.nfiles, ln.d_cf, kChunk, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over,
+                           ln.d_cnt + 2, ocap, dt.anchors, dt.rule_kw, ln.d_kw, dt.kw_words, dt.v_next, dt.v_cls,
+                           ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
       }
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));

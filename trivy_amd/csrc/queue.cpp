@@ -149,11 +149,18 @@ bool ScanQueue::scan(const char* path, size_t path_len, const uint8_t* content, 
         expect_ = callers_;
         expect_at_ = t_lead;
       }
-      const auto deadline = t_lead + std::chrono::microseconds(max_wait_us_);
       auto gathered = [&] {
         return pending_.size() >= max_files_ || pending_bytes_ >= max_bytes_ ||
                pending_.size() + in_batches_ >= expect_;
       };
+#if defined(__SANITIZE_THREAD__)
+      // (ThreadSanitizer of GCC 11 does not intercept pthread_cond_clockwait,
+      // which a steady_clock wait uses, and reports the relock as a double
+      // lock: sanitized builds wait on the system clock, pthread_cond_timedwait)
+      const auto deadline = std::chrono::system_clock::now() + std::chrono::microseconds(max_wait_us_);
+#else
+      const auto deadline = t_lead + std::chrono::microseconds(max_wait_us_);
+#endif
       if (!cv_.wait_until(lk, deadline, gathered)) {
         // the expected callers did not come: expect the ones that did (the
         // next leader does not wait for them again)
