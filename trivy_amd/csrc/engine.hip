@@ -62,14 +62,41 @@ __global__ __launch_bounds__(256) void tsg_readback(RbList L) {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) g.dst[i] = g.src[i];
 }
 
-// Zeroes up to four dword ranges in one launch (K1's per-segment scratch:
-// keyword bits, file flags, counters, per-region hit counts; four memsets
-// were four dispatches).
-struct ClearList { uint32_t* p[4]; uint32_t n[4]; };
-__global__ __launch_bounds__(256) void tsg_clear(ClearList L) {
-  uint32_t* p = L.p[blockIdx.y];
-  const uint32_t n = L.n[blockIdx.y];
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0;
+// A segment's prologue in one launch: zeroes up to four dword ranges (K1's
+// per-segment scratch: keyword bits, file flags, counters, per-region hit
+// counts; four memsets were four dispatches) and, for a small batch in
+// pinned host memory, copies its bytes and offsets into the lane's buffers
+// over PCIe itself (blockIdx.y 4 and 5) -- no copy-engine upload and no
+// cross-stream wait in front of K1 (~25 us of a one-file batch), with the
+// 64 bytes past the data zeroed (K1 reads 16-byte words past the end).
+struct Prologue {
+  uint32_t* p[4];
+  uint32_t n[4];
+  const uint8_t* src[2];       // device view of pinned host memory
+  uint8_t* dst[2];
+  uint32_t bytes[2];
+  uint32_t zpad[2];            // bytes to zero after the copy
+};
+__global__ __launch_bounds__(256) void tsg_prologue(Prologue L) {
+  const uint32_t y = blockIdx.y;
+  const uint32_t tid = blockIdx.x * 256 + threadIdx.x, step = gridDim.x * 256;
+  if (y < 4) {
+    uint32_t* p = L.p[y];
+    for (uint32_t i = tid; i < L.n[y]; i += step) p[i] = 0;
+    return;
+  }
+  const uint8_t* src = L.src[y - 4];
+  uint8_t* dst = L.dst[y - 4];
+  const uint32_t n = L.bytes[y - 4];
+  uint32_t done = 0;
+  if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+    const uint32_t n16 = n / 16;
+    for (uint32_t i = tid; i < n16; i += step)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    done = n16 * 16;
+  }
+  for (uint32_t i = done + tid; i < n; i += step) dst[i] = src[i];
+  for (uint32_t i = tid; i < L.zpad[y - 4]; i += step) dst[n + i] = 0;
 }
 
 #define HIP_OK(expr)                                                              \
@@ -97,9 +124,11 @@ constexpr uint32_t kWaveHits = kK1WaveHits;   // largest per-wave LDS hit buffer
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
 constexpr double kDenseFilesPerGB = 8000.0;   // upload segmentation: "many small files" (image layers: ~48k/GB)
+// per-lane device counters: [0] cands, [1] K2 count, [2] overflow, [3] LDS-base
+// error, [4 + g] K1 items of group g
 constexpr size_t kCntBytes = 1024;
 constexpr size_t kInlineConfirmFiles = 4;          // confirmations this small run on the calling thread
-constexpr uint64_t kInlineConfirmBytes = 512 << 10;     // per-lane device counters: [0] cands, [1] K2 count, [2] overflow, [3] LDS-base error, [4 + g] K1 items of group g
+constexpr uint64_t kInlineConfirmBytes = 512 << 10;
 constexpr int kItemChunks = 4;         // a K1 wave item: 64 lanes x (up to) 4 chunks
 
 // Largest K1 chunk whose wave item (64 lanes x kS chunks) fits the LDS hit
@@ -449,10 +478,14 @@ __device__ __forceinline__ uint32_t k2_file_of(const uint64_t* __restrict__ off,
 // are independent, so one thread keeps kK2Walk dependent L2 round trips in
 // flight instead of one.
 constexpr int kK2Walk = 4;
+// K2 builds: bit 0 = TSG_K2_STATS counters; probe library only (TSG_K2_ABL):
+// bit 1 = per-wave wall-clock trace (results valid), bit 2 = no verify walks
+// (results invalid: prices the setup of a hit)
+constexpr int kK2Stats = 1, kK2Trace = 2, kK2NoWalk = 4;
 
-template <bool kStats>
-__global__ __launch_bounds__(256) void tsg_k2_verify(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t nfiles,
+template <int kK2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void tsg_k2_verify(
+    const uint8_t* __restrict__ data, unsigned long long total, const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint32_t* __restrict__ chunk_file, uint32_t chunk,
     const unsigned long long* __restrict__ hits, const uint32_t* __restrict__ block_hits, uint32_t region_cap,
     uint32_t nregions, uint32_t nsub_main, const unsigned long long* __restrict__ over_hits,
@@ -461,7 +494,13 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint32_t* __restrict__ kwbits, uint32_t kw_words,
     const uint16_t* __restrict__ v_next, const uint8_t* __restrict__ v_cls,
     CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap,
-    unsigned long long* __restrict__ k2s) {
+    unsigned long long* __restrict__ k2s, uint32_t* __restrict__ trace) {
+  constexpr bool kStats = (kK2 & kK2Stats) != 0;
+  // this lane's 32 verify classes of a text window (verify_n), in LDS
+  __shared__ uint32_t k2_cls[256 * 8];
+  uint32_t* const cwin = k2_cls + threadIdx.x * 8;
+  const uint32_t t_wave0 = (kK2 & kK2Trace) ? static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) : 0u;
+  uint32_t tr_hits = 0, tr_bytes = 0;
   // The first nregions * nsub_main workgroups: workgroup (r, k) verifies K1
   // region r's hits k*256+tid, stride 256*nsub_main; the rest verify the
   // shared overflow pool the same way (one launch for both)
@@ -483,6 +522,7 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     const unsigned long long h = rh[i];
     const unsigned long long q = h >> 24;
     const K2Anchor an = anchors[h & 0xffffffu];
+    if (kK2 & kK2Trace) ++tr_hits;
     const uint32_t f = k2_file_of(offsets, nfiles, chunk_file, chunk, q);
     const uint32_t mode = an.flags & 0xffu;
     if (kStats) atomicAdd(&k2s[kK2Stat * an.rule], 1ull);
@@ -525,38 +565,70 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     // conservative)
     auto verify_n = [&](const long long* st0, int n) -> uint32_t {
       uint32_t res = 0, live = 0;
-      uint32_t stt[kK2Walk];
-      long long p[kK2Walk], lim[kK2Walk];
+      if (kK2 & kK2NoWalk) return 0u;
+      // positions as 32-bit offsets from wb, the 16-byte boundary at or below
+      // the first start (a walk spans at most verify_limit + 3 bytes)
+      const long long wb = st0[0] & ~15ll;
+      const uint32_t ofend = static_cast<uint32_t>(min(fend - wb, 0x7fffffffll));
+      uint32_t stt[kK2Walk], o[kK2Walk], olim[kK2Walk];
 #pragma unroll
       for (int j = 0; j < kK2Walk; ++j) {
         stt[j] = 0;
-        p[j] = j < n ? st0[j] : 0;
-        lim[j] = j < n ? min(fend, p[j] + static_cast<long long>(an.verify_limit)) : 0;
+        o[j] = j < n ? static_cast<uint32_t>(st0[j] - wb) : 0u;
+        olim[j] = j < n ? min(ofend, o[j] + an.verify_limit) : 0u;
         if (j < n) {
           if (acc0) res |= 1u << j;
-          else if (p[j] < lim[j]) live |= 1u << j;
-          else if (lim[j] < fend && dead != 0) res |= 1u << j;   // a zero byte limit before the file end: gave up alive
+          else if (o[j] < olim[j]) live |= 1u << j;
+          else if (olim[j] < ofend && dead != 0) res |= 1u << j;   // a zero byte limit before the file end: gave up alive
         }
       }
-      while (live) {
-        uint32_t b[kK2Walk];
+      // the classes of the text bytes [wb, wb + 32), looked up 16 at a time
+      // (independent loads: one round trip each half; the second half only
+      // once a walk gets there) into this lane's LDS slot: a walk then waits
+      // on one dependent load per byte (the transition) instead of three
+      // (byte, class, transition).  Bytes past the window take the per-byte
+      // path.
+      auto fill = [&](uint32_t half) {
+        v4u w{0, 0, 0, 0};
+        const unsigned long long a = static_cast<unsigned long long>(wb) + 16 * half;
+        if (a < total) w = *reinterpret_cast<const v4u*>(data + a);
+        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-        for (int j = 0; j < kK2Walk; ++j) b[j] = (live >> j) & 1u ? data[p[j]] : 0u;
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t c0 = cl[wd[k] & 0xffu], c1 = cl[(wd[k] >> 8) & 0xffu];
+          const uint32_t c2 = cl[(wd[k] >> 16) & 0xffu], c3 = cl[wd[k] >> 24];
+          cwin[4 * half + k] = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+        }
+      };
+      uint32_t filled = 0;                      // window halves with classes
+      if (live) { fill(0); filled = 1; }
+      while (live) {
+        if (filled == 1) {
+          bool need = false;
+#pragma unroll
+          for (int j = 0; j < kK2Walk; ++j) need = need || (((live >> j) & 1u) && o[j] >= 16 && o[j] < 32);
+          if (need) { fill(1); filled = 2; }
+        }
         uint32_t c[kK2Walk];
 #pragma unroll
-        for (int j = 0; j < kK2Walk; ++j) c[j] = cl[b[j]];
+        for (int j = 0; j < kK2Walk; ++j) {
+          c[j] = !((live >> j) & 1u) ? 0u
+               : o[j] < 16 * filled ? static_cast<uint32_t>(reinterpret_cast<const uint8_t*>(cwin)[o[j]])
+               : static_cast<uint32_t>(cl[data[wb + o[j]]]);
+        }
 #pragma unroll
         for (int j = 0; j < kK2Walk; ++j) {
           if (!((live >> j) & 1u)) continue;
           const uint32_t e = nx[stt[j] * ncls + c[j]];
           stt[j] = e & kVState;
-          ++p[j];
+          ++o[j];
           if (kStats) hit_bytes += 1;
+          if (kK2 & kK2Trace) ++tr_bytes;
           if (e & kVAcc) { res |= 1u << j; live &= ~(1u << j); }
           else if (stt[j] == dead) live &= ~(1u << j);
-          else if (p[j] >= lim[j]) {
+          else if (o[j] >= olim[j]) {
             live &= ~(1u << j);
-            if (p[j] < fend) res |= 1u << j;           // gave up alive at the byte limit: conservative
+            if (o[j] < ofend) res |= 1u << j;           // gave up alive at the byte limit: conservative
           }
         }
       }
@@ -606,6 +678,22 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     if (kStats) {
       atomicAdd(&k2s[kK2Stat * an.rule + 3], hit_bytes);
       atomicMax(&k2s[kK2Stat * an.rule + 4], hit_bytes);
+    }
+  }
+  if (kK2 & kK2Trace) {
+    // per wave: [start, end, hits (sum over lanes), walk bytes (sum), most hits of a lane, most bytes of a lane]
+    uint32_t sh = tr_hits, sb = tr_bytes, mh = tr_hits, mb = tr_bytes;
+    for (int o = 32; o > 0; o >>= 1) {
+      sh += __shfl_xor(sh, o);
+      sb += __shfl_xor(sb, o);
+      mh = max(mh, static_cast<uint32_t>(__shfl_xor(mh, o)));
+      mb = max(mb, static_cast<uint32_t>(__shfl_xor(mb, o)));
+    }
+    if ((threadIdx.x & 63u) == 0) {
+      uint32_t* r = trace + 8 * (static_cast<size_t>(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64);
+      r[0] = t_wave0;
+      r[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+      r[2] = sh; r[3] = sb; r[4] = mh; r[5] = mb; r[6] = blockIdx.x; r[7] = 0;
     }
   }
 }
@@ -1166,17 +1254,19 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
   return true;
 }
 
-// Default K1 chunk for a launch of `bytes`.  K1 walks ranges of 1-4 chunks
-// per lane (guided schedule): its chunk is the '\n'-count granularity and the
-// last round's range: 2 KiB for launches of 2 GiB and more (measured r2r:
-// 3.34 vs 3.21 TB/s at 4 GB), else 512 B (round 5: a 250 MB launch 0.249 ->
-// 0.231 ms, 1 GB 0.583 -> 0.529 ms against 1 KiB, profiles/r5a_*: the lanes
-// of a 125-250 MB launch each get a range instead of half of them one chunk);
-// batches under 8 MB (per-file Scan batches of a few files) 256 B, so a
-// one-workgroup launch spreads its bytes over more lanes (a lane walks ~13
-// MB/s: a 1 KiB range is ~80 us).
-uint32_t k1_chunk_for(uint64_t bytes) {
-  return bytes >= (2ull << 30) ? 2048 : bytes >= (8ull << 20) ? 512 : 256;
+// Default K1 chunk for a launch of `bytes` on `lanes` lanes (CUs x 1024).  K1
+// walks ranges of 1-4 chunks per lane (guided schedule): its chunk is the
+// '\n'-count granularity and the last round's range.  2 KiB for launches of 2
+// GiB and more (measured r2r: 3.34 vs 3.21 TB/s at 4 GB); below, the chunk
+// that gives every lane about one (128 B - 512 B): a lane walks ~13 MB/s
+// whatever the load, so a small launch is as fast as its lanes' ranges are
+// short (round 5: a 250 MB launch 0.249 -> 0.231 ms with 512-B chunks against
+// 1 KiB, 1 GB 0.583 -> 0.529 ms, profiles/r5a_*; a 77 MB launch used 147 of
+// 256 CUs with 512-B chunks; a 15 KB file's launch took 22 us at 256 B).
+uint32_t k1_chunk_for(uint64_t bytes, uint32_t lanes) {
+  if (bytes >= (2ull << 30)) return 2048;
+  const uint64_t per = (bytes / std::max<uint32_t>(lanes, 1)) & ~uint64_t(127);
+  return static_cast<uint32_t>(std::min<uint64_t>(512, std::max<uint64_t>(128, per)));
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -1280,8 +1370,18 @@ struct K1Chain {
   hipEvent_t last = nullptr;                    // end of the last K2 queued on the device
 };
 
+// A small batch in pinned host memory staged by the segment prologue kernel
+// (tsg_prologue) instead of the copy engine: device views of its bytes and
+// offsets, and their destinations.
+struct StageIn {
+  const uint8_t* src = nullptr; uint8_t* dst = nullptr; uint64_t bytes = 0;
+  const uint8_t* off_src = nullptr; uint8_t* off_dst = nullptr; uint64_t off_bytes = 0;
+};
+constexpr uint64_t kDirectStageBytes = 1u << 20;     // batches up to this size (and pinned) are staged by the prologue
+
 struct Lane {
   int device = 0;
+  StageIn stage;                                // set by the driver for the next run_segment (consumed there)
   hipStream_t compute = nullptr, copy = nullptr;
   hipEvent_t ev[4] = {};                        // K1 start/end, K2 start/end (compute stream)
   hipEvent_t ev_sync = nullptr;                 // blocking-sync event (K1Chain drivers)
@@ -1699,6 +1799,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   }
   if (const char* c = std::getenv("TSG_K1_ABL")) e->k1_abl_ = std::atoi(c);   // K1 measurement builds (kAbl bits)
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_K2_ABL")) e->k2_abl_ = std::atoi(c) & (kK2Trace | kK2NoWalk);   // probe library builds
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
   if (e->host_profile_) g_scan_prof_on.store(true, std::memory_order_relaxed);
@@ -1822,7 +1923,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
-  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total);
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u);
   if (kChunk > k1_max_chunk(kItemChunks) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   if ((k1_abl_ & kAblNoLoad) && total < (1u << 20) + 64) { *err = "TSG_K1_ABL no-load build needs a batch of >= 1 MiB"; return false; }
   st->chunk_bytes = kChunk;
@@ -1869,10 +1970,23 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     const uint32_t region_cap = static_cast<uint32_t>(std::min<size_t>(ln.hit_cap / nregions, 0xffffffffu));
     {
       // keyword bits, file flags, counters, per-region hit counts: one launch
-      ClearList cl{{ln.d_kw, ln.d_ff, reinterpret_cast<uint32_t*>(ln.d_cnt), ln.d_bh},
-                   {static_cast<uint32_t>(kw_n), std::max<uint32_t>(in.nfiles, 1), static_cast<uint32_t>(kCntBytes / 4), nregions}};
-      const uint32_t mx = std::max(std::max(cl.n[0], cl.n[1]), std::max(cl.n[2], cl.n[3]));
-      hipLaunchKernelGGL(tsg_clear, dim3(std::min<uint32_t>(256, (mx + 255) / 256), 4), dim3(256), 0, s, cl);
+      Prologue pl{};
+      uint32_t* ptrs[4] = {ln.d_kw, ln.d_ff, reinterpret_cast<uint32_t*>(ln.d_cnt), ln.d_bh};
+      const uint32_t ns[4] = {static_cast<uint32_t>(kw_n), std::max<uint32_t>(in.nfiles, 1),
+                              static_cast<uint32_t>(kCntBytes / 4), nregions};
+      uint32_t mx = 0;
+      for (int k = 0; k < 4; ++k) { pl.p[k] = ptrs[k]; pl.n[k] = ns[k]; mx = std::max(mx, ns[k]); }
+      uint32_t rows = 4;
+      if (ln.stage.bytes && attempt == 0) {             // a small pinned batch: staged by this launch
+        pl.src[0] = ln.stage.src; pl.dst[0] = ln.stage.dst;
+        pl.bytes[0] = static_cast<uint32_t>(ln.stage.bytes); pl.zpad[0] = 64;
+        pl.src[1] = ln.stage.off_src; pl.dst[1] = ln.stage.off_dst;
+        pl.bytes[1] = static_cast<uint32_t>(ln.stage.off_bytes); pl.zpad[1] = 0;
+        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(ln.stage.bytes / 16 + 64));
+        rows = 6;
+      }
+      ln.stage = StageIn();
+      hipLaunchKernelGGL(tsg_prologue, dim3(std::min<uint32_t>(256, (mx + 255) / 256), rows), dim3(256), 0, s, pl);
       HIP_OK(hipGetLastError());
     }
     // per-wave LDS hit buffers as large as the group's table leaves room for
@@ -1951,7 +2065,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     for (int a2 = 0; a2 < 3 && !rerun_k1; ++a2) {
       if (!ensure(&ln.d_cands, &ln.d_cands_cap, ln.cand_cap, err)) return false;
       if (a2 > 0) HIP_OK(hipMemsetAsync(ln.d_cnt + 1, 0, 4, s));   // (zeroed with the counters before K1)
-      HIP_OK(hipEventRecord(ln.ev[2], s));
+      // (K2's start is K1's end marker on the first attempt: a marker between
+      // two kernels costs ~5 us of device time on a small segment)
+      if (a2 > 0) HIP_OK(hipEventRecord(ln.ev[2], s));
       const uint64_t per_block = 256ull * k2_hits_per_thread_;
       const uint64_t maxr_est = ln.k2_maxr_per_byte > 0 ? static_cast<uint64_t>(ln.k2_maxr_per_byte * total) + 1
                                                         : 2 * (total / 2048) / nregions + 1;
@@ -1960,16 +2076,31 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       const uint32_t ccap = static_cast<uint32_t>(ln.cand_cap);
       const uint32_t ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
       // the region grid, then the overflow pool's workgroups, in one launch
-      if (ln.d_k2s) {
-        hipLaunchKernelGGL(tsg_k2_verify<true>, dim3(nregions * nsub + osub), dim3(256), 0, s, d_data, d_off,
-                           in.nfiles, ln.d_cf, kChunk, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over,
-                           ln.d_cnt + 2, ocap, dt.anchors, dt.rule_kw, ln.d_kw, dt.kw_words, dt.v_next, dt.v_cls,
-                           ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
-      } else {
-        hipLaunchKernelGGL(tsg_k2_verify<false>, dim3(nregions * nsub + osub), dim3(256), 0, s, d_data, d_off,
-                           in.nfiles, ln.d_cf, kChunk, ln.d_hits, ln.d_bh, region_cap, nregions, nsub, ln.d_over,
-                           ln.d_cnt + 2, ocap, dt.anchors, dt.rule_kw, ln.d_kw, dt.kw_words, dt.v_next, dt.v_cls,
-                           ln.d_cands, ln.d_cnt, ccap, ln.d_k2s);
+      const uint32_t k2_grid = nregions * nsub + osub;
+      const int k2v = (ln.d_k2s ? kK2Stats : 0) | k2_abl_;
+      uint32_t* k2_trace = ln.d_ob;                    // (probe builds: K1's deferred-output slots are free now)
+      const void* k2fn = k2v == 0 ? reinterpret_cast<const void*>(&tsg_k2_verify<0>)
+                       : k2v == kK2Stats ? reinterpret_cast<const void*>(&tsg_k2_verify<kK2Stats>)
+#ifdef TSG_K1_PROBE
+                       : k2v == kK2Trace ? reinterpret_cast<const void*>(&tsg_k2_verify<kK2Trace>)
+                       : k2v == kK2NoWalk ? reinterpret_cast<const void*>(&tsg_k2_verify<kK2NoWalk>)
+                       : k2v == (kK2Trace | kK2NoWalk) ? reinterpret_cast<const void*>(&tsg_k2_verify<kK2Trace | kK2NoWalk>)
+#endif
+                       : nullptr;
+      if (!k2fn) { *err = "unsupported K2 build (TSG_K2_ABL: probe library only)"; return false; }
+      if ((k2_abl_ & kK2Trace) && static_cast<size_t>(k2_grid) * 4 * 8 > ln.d_ob_cap / 2) { *err = "K2 trace buffer too small"; return false; }
+      {
+        const uint32_t a_nf = in.nfiles, a_chunk = kChunk, a_rcap = region_cap, a_nreg = nregions, a_nsub = nsub;
+        const uint32_t a_ocap = ocap, a_kww = dt.kw_words, a_ccap = ccap;
+        const uint8_t* a_data = d_data;
+        unsigned int* a_over_cnt = ln.d_cnt + 2;
+        unsigned long long a_total = total;
+        void* k2args[] = {&a_data, &a_total, &d_off, const_cast<uint32_t*>(&a_nf), &ln.d_cf, const_cast<uint32_t*>(&a_chunk),
+                          &ln.d_hits, &ln.d_bh, const_cast<uint32_t*>(&a_rcap), const_cast<uint32_t*>(&a_nreg),
+                          const_cast<uint32_t*>(&a_nsub), &ln.d_over, &a_over_cnt, const_cast<uint32_t*>(&a_ocap),
+                          &dt.anchors, &dt.rule_kw, &ln.d_kw, const_cast<uint32_t*>(&a_kww), &dt.v_next, &dt.v_cls,
+                          &ln.d_cands, &ln.d_cnt, const_cast<uint32_t*>(&a_ccap), &ln.d_k2s, &k2_trace};
+        HIP_OK(hipLaunchKernel(k2fn, dim3(k2_grid), dim3(256), k2args, 0, s));
       }
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));
@@ -2009,6 +2140,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
           std::this_thread::sleep_for(std::chrono::microseconds(10));
         }
       } else {
+        // (round 5 measured a host-mapped completion word written by the
+        // readback's last block, spun on instead: the events' times were then
+        // not yet ready and waiting for them cost a one-file batch 0.25 ms,
+        // profiles/r5i_small.log; the stream synchronization stays)
         HIP_OK(hipStreamSynchronize(s));
       }
       const double t_k1_sync = ms_since(t_seg0);
@@ -2017,7 +2152,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       if (h_cnt[3] != 0) { *err = "K1: dynamic LDS does not start at address 0"; return false; }
       float k1 = 0, k2 = 0;
       HIP_OK(hipEventElapsedTime(&k1, ln.ev[0], ln.ev[1]));
-      HIP_OK(hipEventElapsedTime(&k2, ln.ev[2], ln.ev[3]));
+      HIP_OK(hipEventElapsedTime(&k2, a2 > 0 ? ln.ev[2] : ln.ev[1], ln.ev[3]));
       if (a2 == 0) st->k1_ms += k1;
       st->k2_ms += k2;
       const uint32_t nover = h_cnt[2];
@@ -2054,6 +2189,20 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
                      osub, ms_since(t_d2h), ms_since(t_seg0));
       st->candidates += c2;
 #ifdef TSG_K1_PROBE
+      if (k2_abl_ & kK2Trace) {
+        // probe builds: K2's per-wave stamps appended to $TSG_K2_TRACE_FILE as
+        // [waves, 0, 0, 0][8 x waves] uint32
+        const size_t waves = static_cast<size_t>(k2_grid) * 4;
+        std::vector<uint32_t> tr(4 + 8 * waves, 0);
+        tr[0] = static_cast<uint32_t>(waves);
+        HIP_OK(hipMemcpy(tr.data() + 4, k2_trace, 8 * waves * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (const char* fn = std::getenv("TSG_K2_TRACE_FILE")) {
+          if (FILE* fp = std::fopen(fn, "ab")) {
+            std::fwrite(tr.data(), sizeof(uint32_t), tr.size(), fp);
+            std::fclose(fp);
+          }
+        }
+      }
       if (k1_abl_ & kAblTrace) {
         // probe builds: the K1 launch's stamps (kAblTrace) appended to
         // $TSG_K1_TRACE_FILE as [blocks, items, nchunks, chunk][4 x blocks][4 x items] uint32
@@ -2255,6 +2404,10 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
   std::atomic<uint32_t> next_light{0};
   std::atomic<uint32_t> next{0};
   std::atomic<uint64_t> nfind{0}, nconf{0};
+  // TSG_HOST_PROFILE: worker thread-ns in the plan (candidates sorted and
+  // grouped), scan_file and storing the result
+  std::atomic<uint64_t> ph_plan{0}, ph_scan{0}, ph_store{0};
+  const bool prof = host_profile_;
   auto light_files = [&]() {
     for (;;) {
       const uint32_t b = next_light.fetch_add(1);
@@ -2274,7 +2427,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
     std::vector<std::vector<uint64_t>> spare;
     // per-thread counts and work taken a few files at a time: 15 threads
     // hitting shared counters once per file serialised on their cache lines
-    uint64_t my_conf = 0, my_find = 0;
+    uint64_t my_conf = 0, my_find = 0, my_plan = 0, my_scan = 0, my_store = 0;
     constexpr uint32_t kTake = 4;
     uint32_t wi = 0, wend = 0;
     for (;;) {
@@ -2284,6 +2437,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         wend = std::min<uint32_t>(wi + kTake, static_cast<uint32_t>(work.size()));
       }
       uint32_t f = work[wi++];
+      const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
       std::string path = in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]);
       const uint8_t* content = in.h_data + in.offsets[f];
       const size_t len = in.offsets[f + 1] - in.offsets[f];
@@ -2347,12 +2501,21 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       nls.data = in.h_data;
       nls.file_off = in.offsets[f];
       nls.chunk = g.chunk;
+      const auto tp1 = prof ? std::chrono::steady_clock::now() : tp0;
       Secret s = scan_file(rs, std::move(path), content, len, binary, &plan, &nls);
+      const auto tp2 = prof ? std::chrono::steady_clock::now() : tp0;
       my_find += s.findings.size();
       results[f] = std::move(s);
+      if (prof) {
+        const auto tp3 = std::chrono::steady_clock::now();
+        my_plan += std::chrono::duration_cast<std::chrono::nanoseconds>(tp1 - tp0).count();
+        my_scan += std::chrono::duration_cast<std::chrono::nanoseconds>(tp2 - tp1).count();
+        my_store += std::chrono::duration_cast<std::chrono::nanoseconds>(tp3 - tp2).count();
+      }
     }
     nconf.fetch_add(my_conf);
     nfind.fetch_add(my_find);
+    if (prof) { ph_plan += my_plan; ph_scan += my_scan; ph_store += my_store; }
   };
   // small confirmations (a few files, little text: per-file Scan batches) run
   // on this thread; waking the pool costs more than the work
@@ -2382,9 +2545,10 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
     uint64_t ph[5];
     for (int k = 0; k < 5; ++k) ph[k] = g_scan_prof[k].exchange(0);
     std::fprintf(stderr, "[tsg host] files %u (work %zu, light %zu) cands %zu: setup %.2f ms, wall %.2f ms, "
-                 "work %.1f + light %.1f thread-ms on %d threads; scan_file thread-ms: keywords %.1f, find %.1f, "
-                 "blocks %.1f, findings %.1f, sort %.1f\n", in.nfiles, work.size(), light.size(),
-                 g.cands.size(), t_setup, ms_since(t_begin), work_us.load() / 1e3, light_us.load() / 1e3, active,
+                 "work %.1f + light %.1f thread-ms on %d threads (plan %.1f, scan_file %.1f, store %.1f); scan_file "
+                 "thread-ms: keywords %.1f, find %.1f, blocks %.1f, findings %.1f, sort %.1f\n", in.nfiles,
+                 work.size(), light.size(), g.cands.size(), t_setup, ms_since(t_begin), work_us.load() / 1e3,
+                 light_us.load() / 1e3, active, ph_plan.load() / 1e6, ph_scan.load() / 1e6, ph_store.load() / 1e6,
                  ph[0] / 1e6, ph[1] / 1e6, ph[2] / 1e6, ph[3] / 1e6, ph[4] / 1e6);
   }
   *nconf_out += nconf.load();
@@ -2567,6 +2731,20 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
   auto t_feed0 = std::chrono::steady_clock::now();
   std::atomic<int64_t> feed_end_ns{0};
   std::atomic<bool> confirmer_idle{true};
+  // a batch small enough for one segment in pinned host memory: staged by the
+  // segment prologue over PCIe (tsg_prologue) instead of the copy engine
+  const uint8_t* h_dev = nullptr;
+  if (!resident && segs.size() == 1 && drivers.size() == 1 && total <= kDirectStageBytes && in.h_data) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, in.h_data) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer) {
+      // (the attributes may describe the allocation's base: offset the device view likewise)
+      const uint8_t* hp = a.hostPointer ? static_cast<const uint8_t*>(a.hostPointer) : in.h_data;
+      h_dev = static_cast<const uint8_t*>(a.devicePointer) + (in.h_data - hp);
+    } else
+
+      (void)hipGetLastError();
+  }
+  const bool direct = h_dev != nullptr;
   auto driver = [&](DeviceTables* dt) {
     std::string e;
     ScanStats dst;
@@ -2624,7 +2802,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     size_t cur = ok ? next_seg.fetch_add(1) : segs.size();
     int slot = 0;
     if (ok && host_profile_) hipEventRecord(ln->anchor, resident ? ln->compute : ln->copy);
-    if (ok && cur < segs.size() && !resident) ok = upload(cur, slot);
+    if (ok && cur < segs.size() && !resident && !direct) ok = upload(cur, slot);
     while (ok && cur < segs.size() && !q.aborted()) {
       // (resident data: the next segment is taken when this one is done, so
       // two drivers take them in order)
@@ -2634,7 +2812,23 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       // kernels have completed (run_segment returns after its D2H)
       if (nxt < segs.size() && !resident && !(ok = upload(nxt, slot ^ 1))) break;
       const void* d_data = resident ? segs[cur].in.d_data : ln->ring[slot];
-      if (!resident) {
+      if (direct) {
+        // one small pinned batch: the segment prologue copies it (StageIn)
+        const Segment& sg = segs[cur];
+        std::memcpy(ln->h_off_pin[slot], sg.in.offsets, (sg.in.nfiles + 1) * sizeof(uint64_t));
+        void* off_dev = nullptr;
+        if (hipHostGetDevicePointer(&off_dev, ln->h_off_pin[slot], 0) != hipSuccess || !off_dev) {
+          ok = false;
+          e = "pinned offsets staging has no device view";
+          break;
+        }
+        ln->stage.src = h_dev + sg.b0;
+        ln->stage.dst = ln->ring[slot];
+        ln->stage.bytes = sg.bytes;
+        ln->stage.off_src = static_cast<const uint8_t*>(off_dev);
+        ln->stage.off_dst = reinterpret_cast<uint8_t*>(ln->off_slot[slot]);
+        ln->stage.off_bytes = (sg.in.nfiles + 1) * sizeof(uint64_t);
+      } else if (!resident) {
         std::string* err = &e;
         auto wait_up = [&]() -> bool {
           HIP_OK(hipStreamWaitEvent(ln->compute, ln->up_done[slot], 0));
@@ -2653,7 +2847,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       if (host_profile_) {
         // GPU timeline of this segment from the scan's anchor event
         float ub = 0, ud = 0, k1a = 0, k1b = 0, k2b = 0;
-        if (!resident) {
+        if (!resident && !direct) {
           hipEventElapsedTime(&ub, ln->anchor, ln->up_begin[slot]);
           hipEventElapsedTime(&ud, ln->anchor, ln->up_done[slot]);
         }
@@ -2663,7 +2857,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
         std::fprintf(stderr, "[tsg tl] seg %zu: host %.3f-%.3f ms; gpu upload %.3f-%.3f, K1 %.3f-%.3f, K2 done %.3f\n",
                      cur, h_start, ms_since(t_feed0), ub, ud, k1a, k1b, k2b);
       }
-      if (!resident) {
+      if (!resident && !direct) {
         float h2d = 0;
         if (hipEventElapsedTime(&h2d, ln->up_begin[slot], ln->up_done[slot]) == hipSuccess) sst.h2d_ms += h2d;
         const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_feed0).count();
