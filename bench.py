@@ -505,13 +505,13 @@ def launch_ranks(n, argv, dry=False):
 
 
 def k1_build():
-    """Build hash of the scan kernels' source (the device part of
-    trivy_amd/csrc/engine.hip, up to its "==== host side" line): a committed
-    traffic measurement applies only to the kernel build it was taken on."""
+    """Build hash of K1's source (trivy_amd/csrc/engine.hip up to its
+    "==== K2" line: the scan kernels and everything they include): a committed
+    traffic measurement applies only to the K1 build it was taken on."""
     import hashlib
     with open(os.path.join(ROOT, "trivy_amd", "csrc", "engine.hip"), "rb") as f:
         src = f.read()
-    cut = src.find(b"\n// ==== host side")
+    cut = src.find(b"\n// ==== K2")
     return hashlib.sha256(src[:cut] if cut >= 0 else src).hexdigest()[:16]
 
 

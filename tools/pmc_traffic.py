@@ -9,7 +9,7 @@ WRITE_SIZE is reported as read (exact for streaming stores per the guide;
 K1's writes are keyword bits, hit records and per-chunk counts).
 
   python tools/pmc_traffic.py gpurun_out/<run> > profiles/traffic_c<config>.json
-(bench.py uses it only while the kernels' build hash -- engine.hip up to its "==== host side" line -- equals its k1_build)
+(bench.py uses it only while K1's build hash -- engine.hip up to its "==== K2" line -- equals its k1_build)
 """
 import collections
 import csv

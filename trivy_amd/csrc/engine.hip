@@ -430,6 +430,8 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
   t.lim = min(end, x.offsets[t.f + 1]);
 }
 
+// ==== K2: everything above this line is K1's build hash (bench.k1_build)
+
 // TSG_K2_STATS counters per rule: hits, gated hits, verify starts, verify
 // bytes, the most verify bytes of one hit
 constexpr uint32_t kK2Stat = 5;
@@ -484,7 +486,7 @@ constexpr int kK2Walk = 4;
 constexpr int kK2Stats = 1, kK2Trace = 2, kK2NoWalk = 4;
 
 template <int kK2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void tsg_k2_verify(
+__global__ __launch_bounds__(256) void tsg_k2_verify(
     const uint8_t* __restrict__ data, unsigned long long total, const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint32_t* __restrict__ chunk_file, uint32_t chunk,
     const unsigned long long* __restrict__ hits, const uint32_t* __restrict__ block_hits, uint32_t region_cap,
@@ -496,9 +498,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     CandDev* __restrict__ cands, unsigned int* __restrict__ counters, uint32_t cand_cap,
     unsigned long long* __restrict__ k2s, uint32_t* __restrict__ trace) {
   constexpr bool kStats = (kK2 & kK2Stats) != 0;
-  // this lane's 32 verify classes of a text window (verify_n), in LDS
-  __shared__ uint32_t k2_cls[256 * 8];
-  uint32_t* const cwin = k2_cls + threadIdx.x * 8;
   const uint32_t t_wave0 = (kK2 & kK2Trace) ? static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) : 0u;
   uint32_t tr_hits = 0, tr_bytes = 0;
   // The first nregions * nsub_main workgroups: workgroup (r, k) verifies K1
@@ -582,40 +581,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
           else if (olim[j] < ofend && dead != 0) res |= 1u << j;   // a zero byte limit before the file end: gave up alive
         }
       }
-      // the classes of the text bytes [wb, wb + 32), looked up 16 at a time
-      // (independent loads: one round trip each half; the second half only
-      // once a walk gets there) into this lane's LDS slot: a walk then waits
-      // on one dependent load per byte (the transition) instead of three
-      // (byte, class, transition).  Bytes past the window take the per-byte
-      // path.
-      auto fill = [&](uint32_t half) {
-        v4u w{0, 0, 0, 0};
-        const unsigned long long a = static_cast<unsigned long long>(wb) + 16 * half;
-        if (a < total) w = *reinterpret_cast<const v4u*>(data + a);
-        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t c0 = cl[wd[k] & 0xffu], c1 = cl[(wd[k] >> 8) & 0xffu];
-          const uint32_t c2 = cl[(wd[k] >> 16) & 0xffu], c3 = cl[wd[k] >> 24];
-          cwin[4 * half + k] = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
-        }
-      };
-      uint32_t filled = 0;                      // window halves with classes
-      if (live) { fill(0); filled = 1; }
+      // (round 5 measured a class window -- the classes of the 32 text bytes
+      // from wb looked up together into an LDS slot, one dependent load per
+      // step instead of three -- and a walk budget with a deferred pass for
+      // long-walking lanes: both slower, profiles/r5k_*, r5l_*, r5n_*)
       while (live) {
-        if (filled == 1) {
-          bool need = false;
+        uint32_t b[kK2Walk];
 #pragma unroll
-          for (int j = 0; j < kK2Walk; ++j) need = need || (((live >> j) & 1u) && o[j] >= 16 && o[j] < 32);
-          if (need) { fill(1); filled = 2; }
-        }
+        for (int j = 0; j < kK2Walk; ++j) b[j] = (live >> j) & 1u ? data[wb + o[j]] : 0u;
         uint32_t c[kK2Walk];
 #pragma unroll
-        for (int j = 0; j < kK2Walk; ++j) {
-          c[j] = !((live >> j) & 1u) ? 0u
-               : o[j] < 16 * filled ? static_cast<uint32_t>(reinterpret_cast<const uint8_t*>(cwin)[o[j]])
-               : static_cast<uint32_t>(cl[data[wb + o[j]]]);
-        }
+        for (int j = 0; j < kK2Walk; ++j) c[j] = cl[b[j]];
 #pragma unroll
         for (int j = 0; j < kK2Walk; ++j) {
           if (!((live >> j) & 1u)) continue;
