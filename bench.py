@@ -932,7 +932,7 @@ def main():
         L.tsg_result_free(res)
         rst = []
         t0 = time.perf_counter()
-        for k in range(max(2, args.steps)):
+        for k in range(max(8, args.steps)):
             res = rstep()
             rst.append(_lib.result_stats(res))
             L.tsg_result_free(res)

@@ -106,6 +106,64 @@ def test_pipelined_pieces_on_gpu(monkeypatch):
         assert g == w, a.FilePath
 
 
+@pytest.fixture(scope="module")
+def pieces_corpus():
+    from oracle import secret_oracle as so
+    from workload import synth
+    c = synth.generate(3_000_000, seed=17, sizes="lognormal", plant_rate=3e-3, base_bytes=1 << 20)
+    ref = so.Scanner(None)
+    want = [ref.scan(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    assert sum(len(w["Findings"]) for w in want) > 20
+    return c, want
+
+
+@pytest.mark.parametrize("env,base", [
+    ({"TSG_RESIDENT_DRIVERS": "1"}, 0),
+    ({"TSG_RESIDENT_DRIVERS": "2", "TSG_CHAIN_K1": "0"}, 0),      # round-4 chain: next K1 after this K2
+    ({"TSG_RESIDENT_DRIVERS": "2", "TSG_CHAIN_K1": "1"}, 16),     # default: next K1 beside this K2
+    ({"TSG_LAST_PIECE": "0.2"}, 48),                              # a short last piece
+    ({"TSG_LAST_PIECE": "0"}, 112),                               # no short last piece
+    ({"TSG_PIECES": "9", "TSG_FIRST_PIECE": "0.03"}, 208),
+])
+def test_resident_pipeline_modes_on_gpu(monkeypatch, pieces_corpus, env, base):
+    # every resident pipeline mode (one driver; two drivers chained after
+    # K2 or after K1; a short last piece or none; many pieces) gives the oracle's
+    # result, with the batch at `base` bytes past a 256-byte boundary so the
+    # pieces after the first start off the L2 line grid (a lead file of the
+    # bytes down to the boundary below, dropped from the results)
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from trivy_amd import _lib
+    c, want = pieces_corpus
+    monkeypatch.setenv("TSG_PIECES", env.get("TSG_PIECES", "5"))
+    monkeypatch.setenv("TSG_MIN_PIECE_BYTES", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = S.Scanner(None)
+    full = torch.zeros(len(c.data) + base, dtype=torch.uint8, device="cuda:0")
+    assert full.data_ptr() % 256 == 0
+    d = full[base:]
+    d.copy_(torch.from_numpy(np.ascontiguousarray(c.data)))
+    paths, lens, _keep = _lib.pack_paths(c.paths)
+    L = _lib.lib()
+    res = ctypes.c_void_p()
+    _lib.check(L.tsg_scan_batch_resident(sc.engine(), ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
+                                         c.offsets.ctypes.data, len(c.paths), paths, lens, None, ctypes.byref(res)))
+    try:
+        got = _lib.result_json(res)
+        st = _lib.result_stats(res)
+    finally:
+        L.tsg_result_free(res)
+    assert st["pieces"] >= 3
+    assert len(got) == len(want)
+    for p, g, w in zip(c.paths, got, want):
+        g.pop("Error", None)
+        assert g == w, p
+
+
 @pytest.mark.parametrize("n", [13, 60])
 def test_equal_findings_tie_order_on_gpu(n):
     # n findings of equal (RuleID, Match) in one file: sort.Slice

@@ -129,6 +129,25 @@ def test_k1_variants_agree_gpu(monkeypatch, abl, chunk):
     assert sum(len(w["Findings"]) for w in want) > 20
 
 
+@pytest.mark.parametrize("chunk", ["256", "128"])
+def test_small_chunks_large_batch_gpu(monkeypatch, chunk):
+    # the chunk sizes the per-launch policy picks for small launches (128-512
+    # B: one chunk per lane) forced onto a 300 MB batch: >= 1.2 M chunks, so
+    # the per-chunk newline counts and file table, the wave items' chunk
+    # ranges and the hit records' chunk-relative offsets run far past their
+    # small-launch values; the result is the host confirmer's
+    c = synth.generate(300_000_000, seed=37, sizes="lognormal", plant_rate=1e-3)
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    assert sum(len(w["Findings"]) for w in want) > 200
+    monkeypatch.setenv("TSG_K1_CHUNK", chunk)
+    monkeypatch.setenv("TSG_SEGMENT_BYTES", str(1 << 30))   # one segment (no geometric tail)
+    monkeypatch.setenv("TSG_SEGMENT_MIN", str(1 << 30))
+    got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
+    assert stats["chunk_bytes"] == int(chunk) and stats["pieces"] == 1
+    assert got == want
+
+
 def test_line_numbers_at_chunk_edges_gpu():
     # K1 stores one '\n' count per chunk while a lane walks a range of
     # chunks; a file boundary in the last line before a chunk edge sends that

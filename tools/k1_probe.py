@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--full", action="store_true",
+                    help="the whole resident scan (tsg_scan_batch_resident: pieces, K1/K2, host confirmation) "
+                         "instead of the two GPU passes")
     ap.add_argument("--prewarm-ms", type=float, default=0.0,
                     help="keep the GPU busy (torch elementwise kernels) this long right before each K1/K2 run")
     ap.add_argument("--variants", default="",
@@ -75,6 +78,8 @@ def probe(args, sc, c, d, L):
     from trivy_amd import _lib
     eng = sc.engine()
     rows = []
+    if args.full:
+        cpaths, clens, keep = _lib.pack_paths(c.paths)
     import torch
     busy = torch.ones(1 << 26, device="cuda:0") if args.prewarm_ms > 0 else None
     for r in range(args.reps + 1):
@@ -86,19 +91,27 @@ def probe(args, sc, c, d, L):
                 torch.cuda.synchronize()
         res = ctypes.c_void_p()
         t0 = time.perf_counter()
-        _lib.check(L.tsg_prefilter_resident(eng, ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
-                                            c.offsets.ctypes.data, len(c.paths), ctypes.byref(res)))
+        if args.full:
+            _lib.check(L.tsg_scan_batch_resident(eng, ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
+                                                 c.offsets.ctypes.data, len(c.paths), cpaths, clens, None,
+                                                 ctypes.byref(res)))
+        else:
+            _lib.check(L.tsg_prefilter_resident(eng, ctypes.c_void_p(d.data_ptr()), c.data.ctypes.data,
+                                                c.offsets.ctypes.data, len(c.paths), ctypes.byref(res)))
         wall = (time.perf_counter() - t0) * 1e3
         st = _lib.result_stats(res)
         L.tsg_result_free(res)
         if r == 0:
             continue                              # warm-up (allocations)
-        rows.append((st["k1_ms"], st["k2_ms"], wall, st["hits"], st["candidates"], st["k1_launches"]))
+        rows.append((st["k1_ms"], st["k2_ms"], wall, st["hits"], st["candidates"], st["k1_launches"],
+                     st.get("host_ms", 0.0), st.get("pieces", 1)))
     k1 = float(np.median([x[0] for x in rows]))
     k2 = float(np.median([x[1] for x in rows]))
     out = {"bytes": c.nbytes, "files": len(c.paths), "k1_ms": round(k1, 4), "k2_ms": round(k2, 4),
            "k1_gbps": round(c.nbytes / k1 / 1e6, 1), "k1_launches": rows[-1][5], "hits": rows[-1][3],
            "candidates": rows[-1][4], "wall_ms": round(float(np.median([x[2] for x in rows])), 3),
+           "wall_gbps": round(c.nbytes / float(np.median([x[2] for x in rows])) / 1e6, 1),
+           "host_ms": round(float(np.median([x[6] for x in rows])), 3), "pieces": rows[-1][7],
            "env": {k: v for k, v in os.environ.items() if k.startswith("TSG_")}}
     print(json.dumps(out) if args.json else out, flush=True)
 

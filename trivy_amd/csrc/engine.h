@@ -119,18 +119,29 @@ class Engine {
   int k1_abl_ = 4560;
   uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
   // drivers per device for resident batches (TSG_RESIDENT_DRIVERS; 2 =
-  // K1Chain: measured no gain, config 2 1530 vs 1528 GB/s, config 3 766 vs
-  // 803 -- the second driver's launch lands behind the first's next segment)
-  int resident_drivers_ = 1;
+  // K1Chain).  Round 4 chained the second driver's K1 behind the first's K2:
+  // no gain (config 2 1530 vs 1528 GB/s).  Chained behind the first's K1
+  // (TSG_CHAIN_K1, round 5) a piece's K2 runs beside the next piece's K1 and
+  // leaves the critical chain: config 2 1632 -> 1862 GB/s, 1 GB of config-1
+  // files 482 -> 570 (profiles/r5p_resident_variants.log).
+  int resident_drivers_ = 2;
+  bool chain_k1_ = true;
   uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
   bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
   int k2_abl_ = 0;                      // TSG_K2_ABL (probe library): K2 trace / no-walk measurement builds
   bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr
   std::mutex k2s_mu_;
   std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
-  uint32_t pieces_ = 4;                 // resident data: pipeline pieces (TSG_PIECES; r3za config 2: 4 pieces, first 10%: 1286 GB/s, 2 at 70/30: 919)
-  double first_piece_ = 0.1;            // resident data: share of the first piece (TSG_FIRST_PIECE)
-  double last_piece_ = 0.0;             // resident data: share of a short last piece (TSG_LAST_PIECE; 0: none)
+  // resident data: pipeline pieces (TSG_PIECES; r3za config 2: 4 pieces,
+  // first 10%: 1286 GB/s, 2 at 70/30: 919), the first piece's share
+  // (TSG_FIRST_PIECE) and a short last piece's (TSG_LAST_PIECE, 0: none; used
+  // from 5 pieces on).  Round 5, K2 beside the next K1 (K1Chain): 5 pieces
+  // with an 8% last piece 1921 GB/s vs 4 pieces 1796 on config 2 -- the last
+  // piece's K2 and host confirmation are the step's tail; 1 GB of config-1
+  // files gains nothing from more pieces (profiles/r5t_resident_pieces.log)
+  uint32_t pieces_ = 5;
+  double first_piece_ = 0.1;
+  double last_piece_ = 0.08;
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
   uint64_t segment_min_ = 64ull << 20;   // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1; r4p: 64 MB 53.2 vs 128 MB 52.5)
   uint64_t segment_tail_ = 0;           // uploaded data: a short last segment (TSG_SEGMENT_TAIL; 0 = none: the

@@ -1777,6 +1777,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_K2_ABL")) e->k2_abl_ = std::atoi(c) & (kK2Trace | kK2NoWalk);   // probe library builds
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
+  if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
   if (e->host_profile_) g_scan_prof_on.store(true, std::memory_order_relaxed);
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
@@ -1792,7 +1793,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     // 32 bits and a wave item spans 64 lanes x 4 chunks: larger chunks are
     // clamped so the offset cannot wrap
     const long v = std::atol(c);
-    if (v >= 256 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(kItemChunks)));
+    if (v >= 128 && v % 128 == 0) e->chunk_ = static_cast<uint32_t>(std::min<long>(v, k1_max_chunk(kItemChunks)));
   }
   for (int d : devices) {
     std::unique_ptr<DeviceTables> dt(new DeviceTables());
@@ -1909,8 +1910,26 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   // offsets: landed with the upload (d_off_up), or copied here (resident data)
   uint64_t* d_off = const_cast<uint64_t*>(d_off_up);
   if (!d_off) {
+    // staged through the lane's pinned buffer and copied by the segment
+    // prologue (StageIn): a hipMemcpyAsync from the caller's pageable array
+    // is a synchronous staged copy that held a resident driver thread up to
+    // ~1 ms while the other driver's passes ran (r5r host timelines)
     if (!ensure(&ln.d_off, &ln.d_off_cap, in.nfiles + 1, err)) return false;
-    HIP_OK(hipMemcpyAsync(ln.d_off, in.offsets, (in.nfiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    const size_t nb = (in.nfiles + 1) * sizeof(uint64_t);
+    if (ln.h_off_pin_cap[0] < in.nfiles + 1) {
+      if (ln.h_off_pin[0]) hipHostFree(ln.h_off_pin[0]);
+      ln.h_off_pin[0] = nullptr;
+      ln.h_off_pin_cap[0] = 0;
+      HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&ln.h_off_pin[0]), nb, hipHostMallocDefault));
+      ln.h_off_pin_cap[0] = in.nfiles + 1;
+    }
+    std::memcpy(ln.h_off_pin[0], in.offsets, nb);
+    void* off_dev = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&off_dev, ln.h_off_pin[0], 0));
+    if (!off_dev || nb > 0xffffffffull) { *err = "pinned offsets staging has no device view"; return false; }
+    ln.stage.off_src = static_cast<const uint8_t*>(off_dev);
+    ln.stage.off_dst = reinterpret_cast<uint8_t*>(ln.d_off);
+    ln.stage.off_bytes = nb;
     d_off = ln.d_off;
   }
   const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * dt.kw_words;
@@ -1953,12 +1972,12 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t mx = 0;
       for (int k = 0; k < 4; ++k) { pl.p[k] = ptrs[k]; pl.n[k] = ns[k]; mx = std::max(mx, ns[k]); }
       uint32_t rows = 4;
-      if (ln.stage.bytes && attempt == 0) {             // a small pinned batch: staged by this launch
+      if ((ln.stage.bytes || ln.stage.off_bytes) && attempt == 0) {   // a small pinned batch / offsets: staged by this launch
         pl.src[0] = ln.stage.src; pl.dst[0] = ln.stage.dst;
-        pl.bytes[0] = static_cast<uint32_t>(ln.stage.bytes); pl.zpad[0] = 64;
+        pl.bytes[0] = static_cast<uint32_t>(ln.stage.bytes); pl.zpad[0] = ln.stage.bytes ? 64 : 0;   // (no pad when only offsets are staged)
         pl.src[1] = ln.stage.off_src; pl.dst[1] = ln.stage.off_dst;
         pl.bytes[1] = static_cast<uint32_t>(ln.stage.off_bytes); pl.zpad[1] = 0;
-        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(ln.stage.bytes / 16 + 64));
+        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(std::max(ln.stage.bytes, ln.stage.off_bytes) / 16 + 64));
         rows = 6;
       }
       ln.stage = StageIn();
@@ -2081,7 +2100,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));
       if (chain_lk.owns_lock()) {            // the other driver's next K1 follows this K2
-        chain->last = ln.ev[3];
+        chain->last = chain_k1_ ? ln.ev[1] : ln.ev[3];
         chain_lk.unlock();
       }
       // (before this segment's readbacks are queued: the callback may copy
@@ -2583,7 +2602,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       // piece 0 takes first_piece_ of the bytes; with last_piece_ a short
       // last piece of that share follows the others (its confirmation is the
       // tail left after the GPU's last pass); the rest share what remains
-      const bool short_last = last_piece_ > 0.0 && want >= 3;
+      const bool short_last = last_piece_ > 0.0 && want >= 5;
       const double mid = 1.0 - first_piece_ - (short_last ? last_piece_ : 0.0);
       const uint32_t nmid = want - 1 - (short_last ? 1 : 0);
       for (uint32_t p = 1; p < want; ++p) {
