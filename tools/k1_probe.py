@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x71215EC7)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--threads", type=int, default=16, help="host confirm threads (--full)")
     ap.add_argument("--full", action="store_true",
                     help="the whole resident scan (tsg_scan_batch_resident: pieces, K1/K2, host confirmation) "
                          "instead of the two GPU passes")
@@ -69,7 +70,7 @@ def main():
                 if "=" in kv:
                     k, _, val = kv.partition("=")
                     os.environ[k] = val
-        sc = S.Scanner(S.ParseConfig(cfg) if cfg else None)
+        sc = S.Scanner(S.ParseConfig(cfg) if cfg else None, threads=args.threads)
         probe(args, sc, c, d, L)
         del sc                                    # engine destroyed here (TSG_K2_STATS prints its counters)
 

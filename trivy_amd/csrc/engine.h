@@ -126,6 +126,13 @@ class Engine {
   // files 482 -> 570 (profiles/r5p_resident_variants.log).
   int resident_drivers_ = 2;
   bool chain_k1_ = true;
+  // K1Chain drivers poll their readback event yielding instead of sleeping
+  // 10 us (TSG_POLL_YIELD), and the confirmer polls the job queue up to
+  // pop_spin_us_ before it sleeps (TSG_POP_SPIN_US): a wake-up under the busy
+  // confirm pool came 0.1-0.2 ms late; config 2 resident 1838 -> 1920-1945
+  // GB/s, config 1 unchanged (profiles/r6a_resident_poll.log)
+  bool poll_yield_ = true;
+  int pop_spin_us_ = 2000;
   uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
   bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
   int k2_abl_ = 0;                      // TSG_K2_ABL (probe library): K2 trace / no-walk measurement builds

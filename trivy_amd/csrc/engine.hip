@@ -1703,9 +1703,19 @@ class JobQueue {
     std::lock_guard<std::mutex> lk(mu_);
     return aborted_;
   }
-  // nullptr once every producer is done and the queue is drained
-  std::unique_ptr<T> pop(int* producers_left) {
+  // nullptr once every producer is done and the queue is drained; with
+  // spin_us > 0 the caller first polls that long (yielding) before it sleeps
+  // on the condition variable (a futex wake-up under a busy pool took ~0.1 ms)
+  std::unique_ptr<T> pop(int* producers_left, int spin_us = 0) {
     std::unique_lock<std::mutex> lk(mu_);
+    if (spin_us > 0) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+      while (q_.empty() && producers_ != 0 && !aborted_ && std::chrono::steady_clock::now() < until) {
+        lk.unlock();
+        std::this_thread::yield();
+        lk.lock();
+      }
+    }
     ready_.wait(lk, [&] { return !q_.empty() || producers_ == 0 || aborted_; });
     *producers_left = producers_;
     if (q_.empty()) return nullptr;
@@ -1778,6 +1788,8 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K2_ABL")) e->k2_abl_ = std::atoi(c) & (kK2Trace | kK2NoWalk);   // probe library builds
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_POLL_YIELD")) e->poll_yield_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_POP_SPIN_US")) e->pop_spin_us_ = std::max(0, std::min(std::atoi(c), 100000));
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
   if (e->host_profile_) g_scan_prof_on.store(true, std::memory_order_relaxed);
   if (const char* c = std::getenv("TSG_K1_TAIL_ROUNDS")) {
@@ -2132,7 +2144,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
           const hipError_t q = hipEventQuery(ln.ev_sync);
           if (q == hipSuccess) break;
           if (q != hipErrorNotReady) HIP_OK(q);
-          std::this_thread::sleep_for(std::chrono::microseconds(10));
+          if (poll_yield_) std::this_thread::yield();
+          else std::this_thread::sleep_for(std::chrono::microseconds(10));
         }
       } else {
         // (round 5 measured a host-mapped completion word written by the
@@ -2905,7 +2918,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     for (;;) {
       int left = 0;
       confirmer_idle.store(true, std::memory_order_release);
-      std::unique_ptr<Job> job = q.pop(&left);
+      std::unique_ptr<Job> job = q.pop(&left, pop_spin_us_);
       confirmer_idle.store(false, std::memory_order_release);
       if (!job) break;
       auto th = std::chrono::steady_clock::now();
