@@ -90,7 +90,8 @@ def test_pipelined_pieces_on_gpu(monkeypatch):
     assert stats["pieces"] > 1
     for a, g, w in zip(args, got, want):
         assert g == w, a.FilePath
-    # resident: the corpus in HBM, piece starts 16-byte aligned inside it
+    # resident: the corpus in HBM; pieces after the first start at the 256-byte
+    # boundary below their first file (a lead file, results dropped)
     L = _lib.lib()
     d = torch.from_numpy(np.ascontiguousarray(c.data)).to("cuda:0")
     paths, lens, _keep = _lib.pack_paths(c.paths)
