@@ -305,11 +305,14 @@ const char* tsg_result_walk_json(const tsg_result* r);
 /* ---- per-file Scan for unchanged callers ----
  * SecretAnalyzer.Analyze calls Scanner.Scan once per file (pkg/fanal/analyzer/
  * secret/secret.go:137) from --parallel goroutines (analyzer.go:434-451,
- * default 5).  A queue gathers concurrent tsg_queue_scan calls into one engine
- * batch: a caller that finds no batch forming leads one, waits until every
- * caller not already in a running batch has joined (or max_files / max_bytes
- * is reached, or max_wait_us has passed), scans it, and hands each caller its
- * own result; up to max_inflight batches run at once.  Thread-safe. */
+ * default 5).  A queue gathers concurrent tsg_queue_scan calls into engine
+ * batches: a caller that finds no batch forming leads one, waits until its
+ * share of the expected callers has joined -- the recent peak of concurrent
+ * callers split over the max_inflight batch slots (default 8), so 5 callers
+ * run as 5 concurrent one-file batches and 64 as batches of 8 -- (or
+ * max_files / max_bytes is reached, or max_wait_us has passed), scans it,
+ * and hands each caller its own result; up to max_inflight batches run at
+ * once.  Thread-safe. */
 typedef struct tsg_queue tsg_queue;
 int tsg_queue_create(tsg_engine* e, uint32_t max_files, uint64_t max_bytes, uint32_t max_wait_us,
                      uint32_t max_inflight, tsg_queue** out);

@@ -26,7 +26,7 @@ def test_queue_scan_equals_batch_gpu(callers):
     sc = S.Scanner(None)
     args = _files(21 + callers)
     want = sc.ScanBatch(args)
-    q = S.ScanQueue(sc)
+    q = S.ScanQueue(sc, max_inflight=2)       # more callers than batch slots: calls share batches
     got = [None] * len(args)
     nxt = [0]
     lock = threading.Lock()

@@ -46,9 +46,11 @@ def _run(q, args, callers, results, errors):
 
 
 def test_model_queue_equals_oracle():
+    # one batch slot: a batch waits for every expected caller, so calls
+    # share batches
     sc = S.Scanner(None)
     args = _files(7)[:600]
-    q = S.ScanQueue(sc, model=True)
+    q = S.ScanQueue(sc, model=True, max_inflight=1)
     got = [None] * len(args)
     errs = {}
     _run(q, args, 8, got, errs)
@@ -93,7 +95,7 @@ def test_lone_caller_after_burst_does_not_wait():
     sc = S.Scanner(None)
     args = _files(9)[:400]
     max_wait_s = 0.2
-    q = S.ScanQueue(sc, model=True, max_wait_us=int(max_wait_s * 1e6))
+    q = S.ScanQueue(sc, model=True, max_wait_us=int(max_wait_s * 1e6), max_inflight=1)
     got = [None] * len(args)
     errs = {}
     _run(q, args, 16, got, errs)
@@ -107,3 +109,26 @@ def test_lone_caller_after_burst_does_not_wait():
     assert q.stats()["timeouts"] == t_burst           # no lone call waited for the burst's callers
     assert dt < 20 * max_wait_s / 4, dt
     q.close()
+
+
+@pytest.mark.parametrize("spread", ["1", "0"])
+def test_spread_batches_over_slots(monkeypatch, spread):
+    # fewer callers than batch slots: with the spread policy (default) every
+    # call runs as its own concurrent batch; with TSG_QUEUE_SPREAD=0 a leader
+    # gathers every expected caller into one batch (how many overlap depends
+    # on thread timing here).  Results equal either way.
+    monkeypatch.setenv("TSG_QUEUE_SPREAD", spread)
+    sc = S.Scanner(None)
+    args = _files(11)[:300]
+    q = S.ScanQueue(sc, model=True, max_inflight=8)
+    got = [None] * len(args)
+    errs = {}
+    _run(q, args, 4, got, errs)
+    assert not errs
+    st = q.stats()
+    q.close()
+    assert st["calls"] == st["files"] == len(args)
+    if spread == "1":
+        assert st["max_batch"] == 1 and st["batches"] == len(args)
+    ref = so.Scanner(None)
+    assert got == [ref.scan(a.FilePath, a.Content) for a in args]

@@ -1346,7 +1346,7 @@ int tsg_queue_create(tsg_engine* e, uint32_t max_files, uint64_t max_bytes, uint
   if (!e || !out) return fail(TSG_ERR_INVALID, "NULL argument");
   std::unique_ptr<tsg_queue> q(new tsg_queue());
   q->q.reset(new ScanQueue(engine_stage(e), max_files ? max_files : 4096, max_bytes ? max_bytes : (256ull << 20),
-                           max_wait_us, max_inflight ? max_inflight : 4));
+                           max_wait_us, max_inflight ? max_inflight : 8));
   q->rs = e->eng->ruleset();
   *out = q.release();
   return TSG_OK;
@@ -1372,7 +1372,7 @@ int tsg_queue_create_model(const tsg_ruleset* rs, uint32_t max_files, uint64_t m
     return model_stage(*qp->rs, *qp->pf)(in, res, e2);
   };
   q->q.reset(new ScanQueue(std::move(model), max_files ? max_files : 4096, max_bytes ? max_bytes : (256ull << 20),
-                           max_wait_us, max_inflight ? max_inflight : 4));
+                           max_wait_us, max_inflight ? max_inflight : 8));
   *out = q.release();
   return TSG_OK;
   TSG_API_CATCH

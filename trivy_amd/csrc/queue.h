@@ -73,6 +73,7 @@ class ScanQueue {
   uint32_t in_batches_ = 0;    // of them, in a running batch
   uint32_t inflight_ = 0;      // running batches
   bool forming_ = false;       // a leader is gathering a batch
+  bool spread_ = true;         // expected callers split over the batch slots (TSG_QUEUE_SPREAD=0: one batch gathers them all)
   std::vector<Staging> free_staging_;
   QueueStats st_;
 };
