@@ -132,6 +132,7 @@ class Engine {
   // confirm pool came 0.1-0.2 ms late; config 2 resident 1838 -> 1920-1945
   // GB/s, config 1 unchanged (profiles/r6a_resident_poll.log)
   bool poll_yield_ = true;
+  bool confirm_prefetch_ = true;        // confirm pool: prefetch the next file's result slot and candidate text (TSG_CONFIRM_PREFETCH)
   int pop_spin_us_ = 2000;
   uint32_t k2_hits_per_thread_ = 1;     // K2 grid: hits of the fullest region per thread (TSG_K2_HITS_PER_THREAD)
   bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction

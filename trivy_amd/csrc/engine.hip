@@ -1788,6 +1788,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K2_ABL")) e->k2_abl_ = std::atoi(c) & (kK2Trace | kK2NoWalk);   // probe library builds
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_CONFIRM_PREFETCH")) e->confirm_prefetch_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POLL_YIELD")) e->poll_yield_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POP_SPIN_US")) e->pop_spin_us_ = std::max(0, std::min(std::atoi(c), 100000));
   if (const char* c = std::getenv("TSG_HOST_PROFILE")) e->host_profile_ = std::atoi(c) != 0;
@@ -2445,6 +2446,24 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         wend = std::min<uint32_t>(wi + kTake, static_cast<uint32_t>(work.size()));
       }
       uint32_t f = work[wi++];
+      if (confirm_prefetch_ && wi < wend) {
+        // the next file of this take: its result slot and the text at its
+        // first candidate starts, fetched while this file is confirmed (the
+        // host has not touched the batch's bytes since they were written):
+        // resident config 5 602-611 -> 614-657 GB/s (profiles/r6j_confirm_prefetch_c5.log; two files
+        // ahead and a wider window were no better)
+        const uint32_t fn = work[wi];
+        __builtin_prefetch(results + fn, 1);
+        const uint8_t* cn = in.h_data + in.offsets[fn];
+        const uint64_t ln = in.offsets[fn + 1] - in.offsets[fn];
+        for (uint32_t k = per_file[fn], ke = std::min(per_file[fn + 1], per_file[fn] + 4); k < ke; ++k) {
+          const uint64_t st = sorted[k].start;
+          if (st < ln) {
+            __builtin_prefetch(cn + st);
+            if (st + 64 < ln) __builtin_prefetch(cn + st + 64);
+          }
+        }
+      }
       const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
       std::string path = in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]);
       const uint8_t* content = in.h_data + in.offsets[f];
