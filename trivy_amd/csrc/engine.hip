@@ -1361,6 +1361,7 @@ struct Lane {
   hipStream_t compute = nullptr, copy = nullptr;
   hipEvent_t ev[4] = {};                        // K1 start/end, K2 start/end (compute stream)
   hipEvent_t ev_sync = nullptr;                 // blocking-sync event (K1Chain drivers)
+  const std::atomic<bool>* pool_idle = nullptr; // set by a scan's driver: its confirm pool has no work
   hipEvent_t up_begin[2] = {}, up_done[2] = {}; // upload ring slot: H2D start / done (copy stream)
   hipEvent_t anchor = nullptr;                   // TSG_HOST_PROFILE: start of a scan() on the copy stream
   uint8_t* ring[2] = {nullptr, nullptr};
@@ -2145,7 +2146,10 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
           const hipError_t q = hipEventQuery(ln.ev_sync);
           if (q == hipSuccess) break;
           if (q != hipErrorNotReady) HIP_OK(q);
-          if (poll_yield_) std::this_thread::yield();
+          // yielding only while the confirm pool is idle: on a box whose
+          // CPU share is a cgroup quota, drivers spinning beside a busy pool
+          // spend the pool's quota (config 5 resident steps 16.9-20.2 ms)
+          if (poll_yield_ && (!ln.pool_idle || ln.pool_idle->load(std::memory_order_relaxed))) std::this_thread::yield();
           else std::this_thread::sleep_for(std::chrono::microseconds(10));
         }
       } else {
@@ -2784,6 +2788,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     try {
     ln = acquire_lane(*dt, &e);
     ok = ln != nullptr;
+    if (ok) ln->pool_idle = &confirmer_idle;
     if (ok && hipSetDevice(dt->device) != hipSuccess) { ok = false; e = "hipSetDevice failed"; }
     if (ok && !resident) {
       for (int i = 0; i < 2 && ok; ++i) {
@@ -2906,6 +2911,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     }
     if (ln) {
       if (!ok) { hipStreamSynchronize(ln->copy); hipStreamSynchronize(ln->compute); }
+      ln->pool_idle = nullptr;                   // (the flag is this scan's)
       release_lane(*dt, ln);
     }
     {
