@@ -1788,7 +1788,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K2_STATS")) e->k2_stats_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_K2_ABL")) e->k2_abl_ = std::atoi(c) & (kK2Trace | kK2NoWalk);   // probe library builds
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
-  if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::max(0, std::min(2, std::atoi(c)));
   if (const char* c = std::getenv("TSG_CONFIRM_PREFETCH")) e->confirm_prefetch_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POLL_YIELD")) e->poll_yield_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POP_SPIN_US")) e->pop_spin_us_ = std::max(0, std::min(std::atoi(c), 100000));
@@ -2030,7 +2030,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     std::unique_lock<std::mutex> chain_lk;
     if (chain && attempt == 0) {
       chain_lk = std::unique_lock<std::mutex>(chain->mu);
-      if (chain->last) HIP_OK(hipStreamWaitEvent(s, chain->last, 0));
+      if (chain->last && chain_k1_ != 2) HIP_OK(hipStreamWaitEvent(s, chain->last, 0));   // (2: no wait, K1s overlap)
     }
     HIP_OK(hipEventRecord(ln.ev[0], s));
     uint32_t launches = 0;
@@ -2114,7 +2114,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ln.ev[3], s));
       if (chain_lk.owns_lock()) {            // the other driver's next K1 follows this K2
-        chain->last = chain_k1_ ? ln.ev[1] : ln.ev[3];
+        chain->last = chain_k1_ == 0 ? ln.ev[3] : ln.ev[1];
         chain_lk.unlock();
       }
       // (before this segment's readbacks are queued: the callback may copy
