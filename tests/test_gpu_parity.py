@@ -122,6 +122,7 @@ def pieces_corpus():
     ({"TSG_RESIDENT_DRIVERS": "1"}, 0),
     ({"TSG_RESIDENT_DRIVERS": "2", "TSG_CHAIN_K1": "0"}, 0),      # round-4 chain: next K1 after this K2
     ({"TSG_RESIDENT_DRIVERS": "2", "TSG_CHAIN_K1": "1"}, 16),     # default: next K1 beside this K2
+    ({"TSG_RESIDENT_DRIVERS": "2", "TSG_CHAIN_K1": "2"}, 80),     # no wait: the two drivers' K1s overlap
     ({"TSG_LAST_PIECE": "0.2"}, 48),                              # a short last piece
     ({"TSG_LAST_PIECE": "0"}, 112),                               # no short last piece
     ({"TSG_PIECES": "9", "TSG_FIRST_PIECE": "0.03"}, 208),

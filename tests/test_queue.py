@@ -65,3 +65,34 @@ def test_queue_probe_and_single_caller_gpu():
     assert q.Scan(args[0]) == want[0]                      # one caller alone: a batch of one, no waiting
     assert q.Scan(S.ScanArgs("empty.txt", b"")) == {"FilePath": "", "Findings": []}
     q.close()
+
+
+def test_queue_spread_default_gpu():
+    # the default queue (8 batch slots) with Trivy's default --parallel 5:
+    # every call runs as its own concurrent one-file batch on its own lane,
+    # and every caller gets exactly its file's result
+    sc = S.Scanner(None)
+    args = _files(41)
+    want = sc.ScanBatch(args)
+    q = S.ScanQueue(sc)
+    got = [None] * len(args)
+    nxt = [0]
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= len(args):
+                return
+            got[i] = q.Scan(args[i])
+    ts = [threading.Thread(target=worker) for _ in range(5)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    st = q.stats()
+    q.close()
+    assert got == want
+    assert st["calls"] == st["files"] == st["batches"] == len(args) and st["max_batch"] == 1
