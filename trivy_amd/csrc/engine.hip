@@ -2428,6 +2428,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       const size_t e = std::min<size_t>(light.size(), (static_cast<size_t>(b) + 1) * kLightBlock);
       for (size_t k = static_cast<size_t>(b) * kLightBlock; k < e; ++k) {
         const uint32_t f = light[k];
+        if (confirm_prefetch_ && k + 8 < e) __builtin_prefetch(in.paths[light[k + 8]]);   // (path strings: scattered)
         // no candidates, no host-evaluated rule: only the global allow-path outcome remains
         const char* p = in.paths[f];
         const size_t pn = in.path_lens ? in.path_lens[f] : std::strlen(p);
@@ -2458,6 +2459,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         // ahead and a wider window were no better)
         const uint32_t fn = work[wi];
         __builtin_prefetch(results + fn, 1);
+        __builtin_prefetch(in.paths[fn]);
         const uint8_t* cn = in.h_data + in.offsets[fn];
         const uint64_t ln = in.offsets[fn + 1] - in.offsets[fn];
         for (uint32_t k = per_file[fn], ke = std::min(per_file[fn + 1], per_file[fn] + 4); k < ke; ++k) {
