@@ -27,8 +27,13 @@ constexpr uint32_t kScanStateCap = 60000;
 // K2 gives up on a verify walk after this many bytes and passes the start on
 // (the host decides it exactly): one thread walking an exclude block's
 // `.*?END NOSCAN` over 8 KiB held a 3 GB config-5 piece's K2 for 2.4 ms
-// (profiles/rd4z_bench_c5k2.log, max_hit_bytes 8193)
-constexpr uint32_t kVerifyLimitCap = 1024;
+// (profiles/rd4z_bench_c5k2.log, max_hit_bytes 8193).  Round 5: 1024 -> 64
+// bytes: a K2 launch lasts as long as its longest walk (one dependent
+// transition per byte), and the few walks past 64 bytes (lane maxima p90 66,
+// max 159 on config 2) set it: K2 per 4 GB 0.378 -> 0.338 ms, per resident
+// step config 2 1.45 -> 1.27 ms, config 5 1.69 -> 1.26 ms, for +2% / +0.8%
+// host candidates (profiles/r6x_verify_cap.log)
+constexpr uint32_t kVerifyLimitCap = 64;
 constexpr double kWeakAnchor = 3.0;
 constexpr size_t kHostKeywordLen = 3;     // keywords this short gate on the host      // literal anchors scoring below this get class extensions
 
@@ -735,7 +740,11 @@ bool build_verify(const std::vector<const Node*>& items, size_t min_items, DfaTa
     std::vector<uint32_t> order(raw.subsets.size());
     for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
     *out = to_table(raw, order, acc);
-    *limit = std::min(hi, kVerifyLimitCap);
+    // TSG_VERIFY_CAP (measurement): a lower cap on the bytes a K2 walk may
+    // take before it gives up and emits the start for the host (exact either way)
+    uint32_t cap = kVerifyLimitCap;
+    if (const char* v = std::getenv("TSG_VERIFY_CAP")) cap = static_cast<uint32_t>(std::max(16, std::min(4096, std::atoi(v))));
+    *limit = std::min(hi, cap);
     if (j < items.size()) *note += " verify-truncated:" + std::to_string(j) + "/" + std::to_string(items.size());
     return true;
   }
