@@ -42,6 +42,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# the bench owns its process: keep the confirmation's freed heap across steps
+# (the library's opt-in allocator policy; TSG_MALLOC_TUNE=0 to
+# measure without it)
+os.environ.setdefault("TSG_MALLOC_TUNE", "1")
 
 HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PCIE_PEAK_GBPS = 63.0     # PCIe Gen5 x16 spec per direction (MI355X_MICROARCH.md "Host link")
@@ -504,15 +508,23 @@ def launch_ranks(n, argv, dry=False):
     return rc
 
 
-def k1_build():
-    """Build hash of K1's source (trivy_amd/csrc/engine.hip up to its
-    "==== K2" line: the scan kernels and everything they include): a committed
-    traffic measurement applies only to the K1 build it was taken on."""
+def k1_build(src=None):
+    """Build hash of K1's source in trivy_amd/csrc/engine.hip: the file up to
+    its "==== K2 begin" line (the readback / prologue kernels, K1's stream
+    state, word steps and output handling) plus "==== K2 end" .. "==== host
+    side" (K1's line loop, tsg_k1_scan_v3 itself and its build table).  K2 and
+    the host code are left out.  A committed traffic measurement applies only
+    to the K1 build it was taken on.  src: the file's bytes (tests)."""
     import hashlib
-    with open(os.path.join(ROOT, "trivy_amd", "csrc", "engine.hip"), "rb") as f:
-        src = f.read()
-    cut = src.find(b"\n// ==== K2")
-    return hashlib.sha256(src[:cut] if cut >= 0 else src).hexdigest()[:16]
+    if src is None:
+        with open(os.path.join(ROOT, "trivy_amd", "csrc", "engine.hip"), "rb") as f:
+            src = f.read()
+    a = src.find(b"\n// ==== K2 begin")
+    b = src.find(b"\n// ==== K2 end")
+    c = src.find(b"\n// ==== host side")
+    if min(a, b, c) < 0 or not a < b < c:
+        raise RuntimeError("engine.hip lacks the K1 build-hash markers")
+    return hashlib.sha256(src[:a] + src[b:c]).hexdigest()[:16]
 
 
 def gather_ranks(dist, world, mine):

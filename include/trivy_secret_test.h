@@ -66,6 +66,17 @@ int tsg_test_go_sort(const uint32_t* keys, size_t n, uint32_t* order);
  * *copied = the dwords that arrived.  Never used by tsg_scan_batch. */
 int tsg_test_readback(uint32_t nwords, uint32_t count, uint32_t per_count, uint32_t* copied);
 
+/* Test hook: the engine's host footprint so far -- lanes (a compute and a
+ * copy stream plus device scratch each) created over all its devices, call
+ * contexts, and confirm-pool threads started.  Never used by tsg_scan_batch. */
+int tsg_test_engine_footprint(tsg_engine* e, uint32_t* lanes, uint32_t* calls, uint32_t* pool_threads);
+
+/* Test hook: the engine's next n segment runs fail before their first
+ * launch (as a failed device allocation would), so a test can check that a
+ * failed call leaves nothing behind on the engine's pooled lanes.  Never used
+ * by tsg_scan_batch. */
+int tsg_test_inject_segment_failures(tsg_engine* e, uint32_t n);
+
 /* The same two pipelines with the CPU model of the GPU passes as the scan
  * stage (tsg_scan_table_model's); tests only, never the product path. */
 int tsg_scan_layer_stream_model(const tsg_ruleset* rs, tsg_read_fn read, void* user, const tsg_feed_opts* opts,

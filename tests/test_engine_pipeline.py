@@ -141,3 +141,41 @@ def test_many_files_result_vector_cpu():
     assert len(got) == n
     hits = [i for i, g in enumerate(got) if g.get("Findings")]
     assert hits == [12345] and got[12345]["FilePath"] == "/f/key.txt"
+
+
+@pytest.mark.gpu
+def test_failed_segment_leaves_lane_clean():
+    """a direct (prologue-staged) small pinned batch whose segment
+    run fails before its first launch must leave nothing staged on the pooled
+    lane: the same engine's next scans -- resident (prologue stages only the
+    offsets) and direct again -- equal a fresh engine's results."""
+    import torch
+    L = _lib.lib()
+    small, small_args = _corpus(200_000, 61)               # <= 1 MiB: the direct (prologue-staged) path
+    big, big_args = _corpus(6_000_000, 62)
+    ref = S.Scanner(None)
+    want_small = ref.ScanBatch(small_args)
+    want_big = ref.ScanBatch(big_args)
+    sc = S.Scanner(None, threads=2)
+    for _ in range(3):
+        _lib.check(L.tsg_test_inject_segment_failures(sc.engine(), 1))
+        with pytest.raises(Exception, match="injected segment failure"):
+            _scan_pinned(sc, small)
+        # resident: the prologue copies the staged offsets only
+        d = torch.from_numpy(np.ascontiguousarray(np.concatenate([big.data[:big.nbytes], np.zeros(64, np.uint8)])))
+        d = d.to("cuda:0")
+        paths, lens, _keep = _lib.pack_paths(big.paths)
+        res = ctypes.c_void_p()
+        _lib.check(L.tsg_scan_batch_resident(sc.engine(), ctypes.c_void_p(d.data_ptr()), big.data.ctypes.data,
+                                             big.offsets.ctypes.data, len(big.paths), paths, lens, None,
+                                             ctypes.byref(res)))
+        try:
+            got = _lib.result_json(res)
+        finally:
+            L.tsg_result_free(res)
+        for s in got:
+            s.pop("Error", None)
+        assert got == want_big
+        got_small, _ = _scan_pinned(sc, small)
+        assert got_small == want_small
+    assert sum(len(w["Findings"]) for w in want_big) > 5

@@ -96,3 +96,29 @@ def test_queue_spread_default_gpu():
     q.close()
     assert got == want
     assert st["calls"] == st["files"] == st["batches"] == len(args) and st["max_batch"] == 1
+
+
+def test_queue_footprint_16_callers_gpu():
+    """the default queue splits callers over up to 8 concurrent
+    batches, each an Engine::scan with its own lane.  16 callers on a fresh
+    engine create at most max_inflight lanes and call contexts, and per-file
+    batches (confirmed inline) start no confirm-pool threads."""
+    import ctypes
+    from trivy_amd import _lib
+    sc = S.Scanner(None)
+    args = _files(51, n_bytes=3_000_000)
+    q = S.ScanQueue(sc)                         # default: 8 batch slots
+    sec, nf = q.probe(args, 16)
+    st = q.stats()
+    q.close()
+    assert sec > 0 and st["files"] == len(args)
+    lanes, calls, threads = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    _lib.check(_lib.lib().tsg_test_engine_footprint(sc.engine(), ctypes.byref(lanes), ctypes.byref(calls),
+                                                    ctypes.byref(threads)))
+    assert 1 <= lanes.value <= 8, lanes.value
+    assert 1 <= calls.value <= 8, calls.value
+    # batches of <= 4 files / 512 KB confirm on the calling thread and start
+    # no pool; a leader that gathered a larger batch starts one of <= 16 threads
+    assert threads.value <= 16 * calls.value, (threads.value, calls.value)
+    print("queue footprint, 16 callers: lanes %d, call contexts %d, pool threads %d, max batch %d"
+          % (lanes.value, calls.value, threads.value, st["max_batch"]))

@@ -9,7 +9,8 @@ WRITE_SIZE is reported as read (exact for streaming stores per the guide;
 K1's writes are keyword bits, hit records and per-chunk counts).
 
   python tools/pmc_traffic.py gpurun_out/<run> > profiles/traffic_c<config>.json
-(bench.py uses it only while K1's build hash -- engine.hip up to its "==== K2" line -- equals its k1_build)
+(bench.py uses it only while K1's build hash -- bench.k1_build: all of K1's device code in engine.hip --
+equals its k1_build; only the timed step's launches are kept)
 """
 import collections
 import csv
@@ -75,6 +76,9 @@ def main():
     kf = k1["tsg_k1_scan"][:n]
     kw = (k1w.get("tsg_k1_scan") or [0.0] * n)[:n]
     out["step_launches"] = n
+    out["k1_fetch_size_kb_per_launch"] = k1["tsg_k1_scan"][:n]
+    out["k1_write_size_kb_per_launch"] = k1w.get("tsg_k1_scan", [])[:n]
+    out["k2_fetch_size_kb_per_launch"] = k1.get("tsg_k2_verify", [])[:n]
     f = sum(kf) / len(kf) * 1024.0 * scale
     w = sum(kw) / len(kw) * 1024.0
     out["traffic_bytes_per_launch"] = f + w

@@ -77,6 +77,9 @@ SIGNATURES = [
     ("tsg_test_go_sort", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     ("tsg_test_readback", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.POINTER(ctypes.c_uint32)]),
+    ("tsg_test_engine_footprint", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                                  ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
+    ("tsg_test_inject_segment_failures", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     ("tsg_scan_host_reference", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                 c_char_pp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_void_p)]),

@@ -132,14 +132,16 @@ namespace {
 // next batch faults them in again (config 5: 19 -> 13.5 thread-ms per 3 GB
 // piece in the findings phase with the heap kept, resident step 18.1 ->
 // 16.6 ms; profiles/r5w_malloc_c5.log).  Once per process, at the first
-// engine: freed heap is kept (trim threshold 1 GiB, top pad 256 MiB) and
-// requests below 32 MiB come from the heap.  TSG_MALLOC_TUNE=0 leaves the
-// allocator alone.
+// engine, and only when the embedding process asks for it (TSG_MALLOC_TUNE=1:
+// the policy is process-wide, so a long-lived embedder -- a trivy server --
+// keeps glibc's defaults unless it opts in; bench.py opts in): freed heap is
+// kept (trim threshold 1 GiB, top pad 256 MiB) and requests below 32 MiB
+// come from the heap.
 void tune_malloc_once() {
   static std::once_flag once;
   std::call_once(once, [] {
     const char* v = std::getenv("TSG_MALLOC_TUNE");
-    if (v && std::atoi(v) == 0) return;
+    if (!v || std::atoi(v) == 0) return;
     mallopt(M_TRIM_THRESHOLD, 1 << 30);
     mallopt(M_TOP_PAD, 256 << 20);
     mallopt(M_MMAP_THRESHOLD, 32 << 20);
@@ -754,6 +756,22 @@ int tsg_test_readback(uint32_t nwords, uint32_t count, uint32_t per_count, uint3
   std::string err;
   if (!tsg::readback_probe(nwords, count, per_count, copied, &err))
     return fail(tsg::device_count() > 0 ? TSG_ERR_HIP : TSG_ERR_NO_DEVICE, err);
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_test_engine_footprint(tsg_engine* e, uint32_t* lanes, uint32_t* calls, uint32_t* pool_threads) {
+  TSG_API_TRY
+  if (!e || !lanes || !calls || !pool_threads) return fail(TSG_ERR_INVALID, "NULL argument");
+  e->eng->footprint(lanes, calls, pool_threads);
+  return TSG_OK;
+  TSG_API_CATCH
+}
+
+int tsg_test_inject_segment_failures(tsg_engine* e, uint32_t n) {
+  TSG_API_TRY
+  if (!e) return fail(TSG_ERR_INVALID, "engine is NULL");
+  e->eng->inject_segment_failures(n);
   return TSG_OK;
   TSG_API_CATCH
 }

@@ -46,6 +46,7 @@ struct Lane;
 struct GpuOut;
 struct CallCtx;
 struct K1Chain;
+struct StageIn;
 
 // One engine = the compiled ruleset's device tables on every selected device.
 // scan() is reentrant: each call takes its own lane (HIP streams + scratch
@@ -79,6 +80,12 @@ class Engine {
   bool strip_cr(const void* d_src, const uint64_t* d_off, uint32_t nfiles, uint64_t total, void* d_dst,
                 uint64_t* d_new_off, uint64_t* out_total, double* ms, std::string* err);
 
+  // Lanes created over all devices, call contexts, and confirm-pool threads
+  // started (test hook: the per-file queue's footprint).
+  void footprint(uint32_t* lanes, uint32_t* calls, uint32_t* pool_threads);
+  // Test hook: the next n run_segment calls fail before their first launch.
+  void inject_segment_failures(uint32_t n) { inject_fail_.store(n); }
+
   const Prefilter& prefilter() const { return pf_; }
   std::shared_ptr<const Ruleset> ruleset() const { return rs_; }
   const std::vector<int>& devices() const { return devices_; }
@@ -90,10 +97,12 @@ class Engine {
   // while_gpu (optional) runs once on the calling thread after the segment's
   // kernels are queued, before their readbacks are; chain (optional) orders
   // the K1 launches of several drivers of one device (K1Chain); defer_copy
-  // leaves the readback in the lane's pinned buffers (GpuOut::finish_copy)
+  // leaves the readback in the lane's pinned buffers (GpuOut::finish_copy);
+  // stage (optional) is a small pinned batch the segment prologue copies in
+  // (used by this call only: nothing of it stays on the pooled lane)
   bool run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data, const uint64_t* d_off_up,
                    ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu = nullptr,
-                   K1Chain* chain = nullptr, bool defer_copy = false);
+                   K1Chain* chain = nullptr, bool defer_copy = false, const StageIn* stage = nullptr);
   void plan_confirm(const Segment& sg, GpuOut* g) const;
   void confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* results, uint64_t* nconf,
                        uint64_t* nfind, bool gpu_in_flight);
@@ -138,6 +147,7 @@ class Engine {
   bool k2_stats_ = false;               // TSG_K2_STATS=1: per-rule K2 counters, printed to stderr at destruction
   int k2_abl_ = 0;                      // TSG_K2_ABL (probe library): K2 trace / no-walk measurement builds
   bool host_profile_ = false;           // TSG_HOST_PROFILE=1: per-segment host confirm breakdown on stderr
+  std::atomic<uint32_t> inject_fail_{0};
   std::mutex k2s_mu_;
   std::vector<unsigned long long> k2s_;  // 4 per rule: hits, past the keyword gate, verify starts, bytes walked
   // resident data: pipeline pieces (TSG_PIECES; r3za config 2: 4 pieces,

@@ -430,7 +430,8 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
   t.lim = min(end, x.offsets[t.f + 1]);
 }
 
-// ==== K2: everything above this line is K1's build hash (bench.k1_build)
+// ==== K2 begin: K2 (from here to '==== K2 end') is outside K1's build hash
+// (bench.py k1_build: the file up to here plus '==== K2 end' .. '==== host side')
 
 // TSG_K2_STATS counters per rule: hits, gated hits, verify starts, verify
 // bytes, the most verify bytes of one hit
@@ -673,6 +674,8 @@ __global__ __launch_bounds__(256) void tsg_k2_verify(
     }
   }
 }
+
+// ==== K2 end: from here to '==== host side' is K1 again (in k1_build)
 
 // K1 v3: the same pass, built around the per-byte cost.
 //  * LDS layout [class map (256 B) | scan table | output meta | output list |
@@ -1207,8 +1210,8 @@ const void* k1_kernel(int abl, bool compressed) {
   }
 }
 
-// ==== host side: everything above this line is the kernels' build hash
-// (bench.py k1_build: a committed traffic measurement applies to that code)
+// ==== host side: K1's build hash (bench.py k1_build) ends here -- a
+// committed traffic measurement applies to that code
 
 template <typename T>
 bool dev_upload(const std::vector<T>& v, T** out, std::string* err) {
@@ -1357,7 +1360,6 @@ constexpr uint64_t kDirectStageBytes = 1u << 20;     // batches up to this size 
 
 struct Lane {
   int device = 0;
-  StageIn stage;                                // set by the driver for the next run_segment (consumed there)
   hipStream_t compute = nullptr, copy = nullptr;
   hipEvent_t ev[4] = {};                        // K1 start/end, K2 start/end (compute stream)
   hipEvent_t ev_sync = nullptr;                 // blocking-sync event (K1Chain drivers)
@@ -1428,8 +1430,17 @@ struct GpuOut {
 };
 
 // One call's host confirm resources.
+// The pool is created at the call's first confirmation that needs it: per-file
+// Scan batches (a few files, confirmed inline on the calling thread) never
+// start one, so the queue's up to max_inflight concurrent batches hold a lane
+// each but no idle confirm threads.
 struct CallCtx {
   std::unique_ptr<ThreadPool> pool;
+  int nt = 1;
+  ThreadPool& get() {
+    if (!pool || pool->size() != nt) pool.reset(new ThreadPool(nt));
+    return *pool;
+  }
 };
 
 // A self-contained sub-batch: files [f0, f0 + in.nfiles) of the call's
@@ -1894,8 +1905,20 @@ CallCtx* Engine::acquire_call() {
     calls_.emplace_back(new CallCtx());
     cc = calls_.back().get();
   }
-  if (!cc->pool || cc->pool->size() != nt) cc->pool.reset(new ThreadPool(nt));
+  cc->nt = nt;                                   // (the pool itself starts on first use: CallCtx::get)
   return cc;
+}
+
+void Engine::footprint(uint32_t* lanes, uint32_t* calls, uint32_t* pool_threads) {
+  *lanes = 0;
+  for (auto& d : dev_) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    *lanes += static_cast<uint32_t>(d->lanes.size());
+  }
+  std::lock_guard<std::mutex> lk(call_mu_);
+  *calls = static_cast<uint32_t>(calls_.size());
+  *pool_threads = 0;
+  for (auto& c : calls_) if (c->pool) *pool_threads += static_cast<uint32_t>(c->pool->size());
 }
 
 void Engine::release_call(CallCtx* cc) {
@@ -1908,8 +1931,13 @@ void Engine::release_call(CallCtx* cc) {
 // compute stream.  Returns when the segment's results are on the host.
 bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const void* d_data_v, const uint64_t* d_off_up,
                          ScanStats* st, GpuOut* out, std::string* err, const std::function<void()>* while_gpu,
-                         K1Chain* chain, bool defer_copy) {
+                         K1Chain* chain, bool defer_copy, const StageIn* stage_in) {
   const BatchInput& in = sg.in;
+  // this call's prologue copies (a small pinned batch, staged offsets): a
+  // local, so nothing staged for one call can outlive it on the pooled lane
+  // (a stage left on the lane by an early return was copied by the
+  // next caller's prologue from a freed pinned buffer)
+  StageIn stage = stage_in ? *stage_in : StageIn();
   HIP_OK(hipSetDevice(dt.device));
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
@@ -1941,10 +1969,15 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     void* off_dev = nullptr;
     HIP_OK(hipHostGetDevicePointer(&off_dev, ln.h_off_pin[0], 0));
     if (!off_dev || nb > 0xffffffffull) { *err = "pinned offsets staging has no device view"; return false; }
-    ln.stage.off_src = static_cast<const uint8_t*>(off_dev);
-    ln.stage.off_dst = reinterpret_cast<uint8_t*>(ln.d_off);
-    ln.stage.off_bytes = nb;
+    stage.off_src = static_cast<const uint8_t*>(off_dev);
+    stage.off_dst = reinterpret_cast<uint8_t*>(ln.d_off);
+    stage.off_bytes = nb;
     d_off = ln.d_off;
+  }
+  // test hook (tsg_test_inject_segment_failures): fail here, after the
+  // offsets were staged and before any launch, as a failed allocation would
+  for (uint32_t k = inject_fail_.load(); k > 0;) {
+    if (inject_fail_.compare_exchange_weak(k, k - 1)) { *err = "injected segment failure (test hook)"; return false; }
   }
   const size_t kw_n = static_cast<size_t>(std::max<uint32_t>(in.nfiles, 1)) * dt.kw_words;
   if (!ensure(&ln.d_kw, &ln.d_kw_cap, kw_n, err)) return false;
@@ -1986,15 +2019,14 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t mx = 0;
       for (int k = 0; k < 4; ++k) { pl.p[k] = ptrs[k]; pl.n[k] = ns[k]; mx = std::max(mx, ns[k]); }
       uint32_t rows = 4;
-      if ((ln.stage.bytes || ln.stage.off_bytes) && attempt == 0) {   // a small pinned batch / offsets: staged by this launch
-        pl.src[0] = ln.stage.src; pl.dst[0] = ln.stage.dst;
-        pl.bytes[0] = static_cast<uint32_t>(ln.stage.bytes); pl.zpad[0] = ln.stage.bytes ? 64 : 0;   // (no pad when only offsets are staged)
-        pl.src[1] = ln.stage.off_src; pl.dst[1] = ln.stage.off_dst;
-        pl.bytes[1] = static_cast<uint32_t>(ln.stage.off_bytes); pl.zpad[1] = 0;
-        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(std::max(ln.stage.bytes, ln.stage.off_bytes) / 16 + 64));
+      if ((stage.bytes || stage.off_bytes) && attempt == 0) {   // a small pinned batch / offsets: staged by this launch
+        pl.src[0] = stage.src; pl.dst[0] = stage.dst;
+        pl.bytes[0] = static_cast<uint32_t>(stage.bytes); pl.zpad[0] = stage.bytes ? 64 : 0;   // (no pad when only offsets are staged)
+        pl.src[1] = stage.off_src; pl.dst[1] = stage.off_dst;
+        pl.bytes[1] = static_cast<uint32_t>(stage.off_bytes); pl.zpad[1] = 0;
+        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(std::max(stage.bytes, stage.off_bytes) / 16 + 64));
         rows = 6;
       }
-      ln.stage = StageIn();
       hipLaunchKernelGGL(tsg_prologue, dim3(std::min<uint32_t>(256, (mx + 255) / 256), rows), dim3(256), 0, s, pl);
       HIP_OK(hipGetLastError());
     }
@@ -2557,7 +2589,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
     work_bytes += in.offsets[work[k] + 1] - in.offsets[work[k]];
   const bool inline_confirm = work.size() <= kInlineConfirmFiles && work_bytes <= kInlineConfirmBytes &&
                               light.size() <= kLightBlock;
-  const int nt = inline_confirm ? 1 : cc.pool->size();
+  const int nt = inline_confirm ? 1 : cc.get().size();
   // while GPU passes are in flight one core stays with each thread driving
   // them (a preempted driver thread stalls its GPU)
   const int active = gpu_in_flight && nt > 1 ? nt - 1 : nt;
@@ -2573,7 +2605,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
     light_us.fetch_add(std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - b).count());
   };
   if (inline_confirm) body(0);
-  else cc.pool->run(body);
+  else cc.get().run(body);
   if (host_profile_) {
     uint64_t ph[5];
     for (int k = 0; k < 5; ++k) ph[k] = g_scan_prof[k].exchange(0);
@@ -2846,6 +2878,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       // kernels have completed (run_segment returns after its D2H)
       if (nxt < segs.size() && !resident && !(ok = upload(nxt, slot ^ 1))) break;
       const void* d_data = resident ? segs[cur].in.d_data : ln->ring[slot];
+      StageIn stage;                     // (direct batches: this segment's prologue copies)
       if (direct) {
         // one small pinned batch: the segment prologue copies it (StageIn)
         const Segment& sg = segs[cur];
@@ -2856,12 +2889,12 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
           e = "pinned offsets staging has no device view";
           break;
         }
-        ln->stage.src = h_dev + sg.b0;
-        ln->stage.dst = ln->ring[slot];
-        ln->stage.bytes = sg.bytes;
-        ln->stage.off_src = static_cast<const uint8_t*>(off_dev);
-        ln->stage.off_dst = reinterpret_cast<uint8_t*>(ln->off_slot[slot]);
-        ln->stage.off_bytes = (sg.in.nfiles + 1) * sizeof(uint64_t);
+        stage.src = h_dev + sg.b0;
+        stage.dst = ln->ring[slot];
+        stage.bytes = sg.bytes;
+        stage.off_src = static_cast<const uint8_t*>(off_dev);
+        stage.off_dst = reinterpret_cast<uint8_t*>(ln->off_slot[slot]);
+        stage.off_bytes = (sg.in.nfiles + 1) * sizeof(uint64_t);
       } else if (!resident) {
         std::string* err = &e;
         auto wait_up = [&]() -> bool {
@@ -2875,7 +2908,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       ScanStats sst;
       const double h_start = ms_since(t_feed0);
       ok = run_segment(*dt, *ln, segs[cur], d_data, resident ? nullptr : ln->off_slot[slot], &sst, &job->out, &e,
-                       &plan_pending, chain_p, /*defer_copy=*/true);
+                       &plan_pending, chain_p, /*defer_copy=*/true, direct ? &stage : nullptr);
       if (!ok) break;
       plan_pending();                    // (a rerun path may not have called it)
       if (host_profile_) {

@@ -1020,17 +1020,36 @@ void SecretVec::resize(size_t n) {
   constexpr size_t kPerThread = 32768;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t nt = std::min<size_t>({add / kPerThread, 8, hw});
+  // exception safety (a Secret() that throws bad_alloc): every element
+  // constructed before the throw is destroyed again before it propagates, so
+  // n_ still describes the live range and a retried resize starts clean
   if (nt <= 1) {
-    for (size_t i = n_; i < n; ++i) new (p_ + i) Secret();
+    size_t i = n_;
+    try {
+      for (; i < n; ++i) new (p_ + i) Secret();
+    } catch (...) {
+      for (size_t k = n_; k < i; ++k) p_[k].~Secret();
+      throw;
+    }
   } else {
     const size_t per = (add + nt - 1) / nt;
+    std::vector<size_t> built(nt, 0);                // elements constructed in each block
     std::atomic<size_t> next{0};
-    run_threads(static_cast<int>(nt), [&] {
-      for (size_t t; (t = next.fetch_add(1)) < nt;) {
-        const size_t a = n_ + t * per, b = std::min(n, a + per);
-        for (size_t i = a; i < b; ++i) new (p_ + i) Secret();
-      }
-    });
+    try {
+      run_threads(static_cast<int>(nt), [&] {
+        for (size_t t; (t = next.fetch_add(1)) < nt;) {
+          const size_t a = n_ + t * per, b = std::min(n, a + per);
+          for (size_t i = a; i < b; ++i) {
+            new (p_ + i) Secret();
+            built[t] = i + 1 - a;
+          }
+        }
+      });
+    } catch (...) {
+      for (size_t t = 0; t < nt; ++t)
+        for (size_t k = 0; k < built[t]; ++k) p_[n_ + t * per + k].~Secret();
+      throw;
+    }
   }
   n_ = n;
 }
