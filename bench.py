@@ -103,6 +103,28 @@ def pick_sample(offsets, target_bytes, seed, large=8 << 20, large_share=0.5):
     return sorted(idx)
 
 
+def pick_parity(offsets, base_idx, share, seed, large=8 << 20):
+    """The parity leg's files: the CPU-baseline sample `base_idx`, every file
+    above `large` bytes, then seeded small files until the set holds `share`
+    of the batch's bytes (>= 50% of the step's bytes)."""
+    n = len(offsets) - 1
+    sizes = np.diff(np.asarray(offsets, dtype=np.int64))
+    total = int(sizes.sum())
+    chosen = np.zeros(n, dtype=bool)
+    chosen[np.asarray(base_idx, dtype=np.int64)] = True
+    chosen |= sizes > large
+    have = int(sizes[chosen].sum())
+    if have < share * total:
+        for i in np.random.default_rng(seed + 1).permutation(n):
+            if chosen[i]:
+                continue
+            chosen[i] = True
+            have += int(sizes[i])
+            if have >= share * total:
+                break
+    return [int(i) for i in np.nonzero(chosen)[0]]
+
+
 def _alloc_pinned(L, n):
     from trivy_amd import _lib
     ptr = ctypes.c_void_p()
@@ -561,6 +583,9 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU baseline workers (default: every core this rank may use, SURVEY 8d's T = nproc)")
     ap.add_argument("--cpu-sample-mb", type=float, default=1200.0)
+    ap.add_argument("--parity-share", type=float, default=0.5,
+                    help="the oracle checks at least this share of the step's bytes (every file above 8 MB, the "
+                         "CPU-baseline sample, then seeded small files); 0 = the CPU-baseline sample only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident comparison leg")
     ap.add_argument("--tree", type=int, default=-1,
@@ -1036,16 +1061,40 @@ def main():
             for k, v in out["per_file"].items():
                 if isinstance(v, dict):
                     v["vs_cpu_baseline_cxx"] = round(v["gbps"] / (nb / cdt / 1e9), 2)
-        out["parity"] = {"sample_files": len(idx), "sample_bytes": nb, "sample_findings": ofind,
-                         "sample_share": round(nb / max(batch.nbytes, 1), 4),
-                         "sample_files_share": round(len(idx) / max(batch.nfiles, 1), 4),
+        # parity beyond the baseline sample: every file above 8 MB and seeded
+        # small files up to --parity-share of the step's bytes, through the
+        # same oracle pool (not part of the baseline timing)
+        pidx = idx
+        pfind, pnb, pdt, pall = ofind, nb, 0.0, set(idx)
+        if args.parity_share > 0 and nb < args.parity_share * batch.nbytes:
+            pidx = pick_parity(batch.offsets, idx, args.parity_share, args.seed)
+            base = set(idx)
+            rest = [i for i in pidx if i not in base]
+            ritems = [(batch.paths[i], batch.file(i), bool(batch.binary[i]) if batch.binary is not None else False)
+                      for i in rest]
+            _, rres, pdt, rnb = cpu_baseline(ritems, procs, cfg_path)
+            del ritems
+            diff += [batch.paths[i] for j, i in enumerate(rest) if rres[j] != gpu_results[i]]
+            pfind += sum(len(r["Findings"]) for r in rres)
+            pnb += rnb
+            pall = set(pidx)
+        sizes = np.diff(batch.offsets.astype(np.int64))
+        out["parity"] = {"sample_files": len(pidx), "sample_bytes": pnb, "sample_findings": pfind,
+                         "sample_share": round(pnb / max(batch.nbytes, 1), 4),
+                         "sample_files_share": round(len(pidx) / max(batch.nfiles, 1), 4),
+                         "files_over_8mb_checked": sum(1 for i in pall if sizes[i] > (8 << 20)),
+                         "files_over_8mb": int((sizes > (8 << 20)).sum()),
+                         "oracle_s": round(dt + pdt, 1),
                          "diff_files": len(diff), "diff_examples": diff[:5], "cxx_diff_files": cdiff,
-                         "note": "the oracle checks this seeded sample of the step's batch (half of it files above "
-                                 "8 MB); the rest of the batch is covered by the GPU parity tests at smaller sizes"}
+                         "note": "the oracle (oracle/secret_oracle.py) checks these files of the step's batch: the "
+                                 "CPU-baseline sample, every file above 8 MB and seeded small files up to "
+                                 "--parity-share of the bytes; cxx_diff_files compares the C++ restatement on the "
+                                 "baseline sample only"}
         failed = bool(diff) or cdiff > 0
         log("cpu baseline %.4f GB/s (oracle, %d procs), %.4f GB/s (C++ restatement, %d threads); "
-            "parity diff files: %d (findings in sample: %d)" % (
-                gbps, procs, nb / cdt / 1e9, procs, len(diff), ofind))
+            "parity: %d files / %.2f GB (%.0f%% of the batch) checked by the oracle in %.0f s, diff files: %d "
+            "(findings in sample: %d)" % (gbps, procs, nb / cdt / 1e9, procs, len(pidx), pnb / 1e9,
+                                          100.0 * pnb / max(batch.nbytes, 1), dt + pdt, len(diff), pfind))
 
     for b in shard_batches:
         b.free()

@@ -71,6 +71,27 @@ int tsg_test_readback(uint32_t nwords, uint32_t count, uint32_t per_count, uint3
  * contexts, and confirm-pool threads started.  Never used by tsg_scan_batch. */
 int tsg_test_engine_footprint(tsg_engine* e, uint32_t* lanes, uint32_t* calls, uint32_t* pool_threads);
 
+/* CPU model of the engine's multi-device segment pipeline (pipeline.h:
+ * DriverPipeline, the code Engine::scan runs its device drivers on) with
+ * simulated devices: `ndevices` drivers, each holding a lane of its device's
+ * pool, pull `nsegments` segments (seg_us of "GPU" work each) and hand them to
+ * the calling thread, which confirms each (confirm_us).  fail_mode 1: driver
+ * fail_device returns an error at its fail_at-th segment (a HIP error); 2: it
+ * throws bad_alloc there; 3: the confirming thread throws at its fail_at-th
+ * segment; 0: no failure.  Returns TSG_OK, or the failure's code and message;
+ * *out tells what ran.  Tests only (tests/test_pipeline_model.py). */
+typedef struct {
+  uint64_t segments_started, segments_pushed, segments_confirmed, segments_confirmed_twice;
+  uint64_t started_after_failure;  /* segments any driver began after the failure */
+  uint32_t lanes_outstanding;      /* lanes not back in their pools when the call returned */
+  uint32_t lanes_created;          /* most lanes a pool had out at once, summed over devices */
+  uint32_t drivers_alive;          /* driver bodies still running when the call returned */
+  double wall_ms, fail_to_return_ms;
+} tsg_model_pipeline_stats;
+int tsg_test_multi_driver_model(uint32_t ndevices, uint32_t nsegments, int32_t fail_device, uint32_t fail_at,
+                                uint32_t fail_mode, uint32_t seg_us, uint32_t confirm_us,
+                                tsg_model_pipeline_stats* out);
+
 /* Test hook: the engine's next n segment runs fail before their first
  * launch (as a failed device allocation would), so a test can check that a
  * failed call leaves nothing behind on the engine's pooled lanes.  Never used

@@ -22,8 +22,11 @@ def oracle_scan_many(items, procs=8, cfg=None):
     """items: [(path, content, binary)] -> oracle types.Secret dicts, in order.
     cfg: an oracle config (so.parse_config(...)) or None for the builtins."""
     order = sorted(range(len(items)), key=lambda j: -len(items[j][1]))
+    # (tens of thousands of small files: a task per file is mostly IPC; the
+    # largest files lead the order, so chunks of neighbours stay balanced)
+    cs = max(1, min(64, len(items) // (procs * 32)))
     with mp.get_context("fork").Pool(procs, initializer=_init, initargs=(cfg,)) as pool:
-        got = pool.map(_scan, [items[j] for j in order], chunksize=1)
+        got = pool.map(_scan, [items[j] for j in order], chunksize=cs)
     out = [None] * len(items)
     for j, r in zip(order, got):
         out[j] = r

@@ -9,7 +9,11 @@
   (a hit every ~4 bytes, far past any workgroup's hit region) goes through the
   shared overflow pool without a K1 blow-up, finds the secret planted after
   the tokens at the right line, and a 4 MB variant equals the host reference;
-* the largest K1 chunk TSG_K1_CHUNK allows gives the default-chunk result.
+* the largest K1 chunk TSG_K1_CHUNK allows, every K1 chunk size, small
+  chunks on a 300 MB batch, files ending in every position of a chunk and the
+  geometric upload tail all equal the oracle on every file (the
+  host confirmer shares scanner.cpp / goregexp.cpp with the product, so those
+  tests also check against oracle/secret_oracle.py, which shares nothing).
 """
 import os
 import random
@@ -24,6 +28,16 @@ from trivy_amd import secret as S
 from workload import synth
 
 pytestmark = pytest.mark.gpu
+
+
+_ORACLE_CACHE = {}
+
+
+def _oracle_all(key, args):
+    """the oracle on every file of `args` (cached per corpus key)"""
+    if key not in _ORACLE_CACHE:
+        _ORACLE_CACHE[key] = oracle_scan_many([(a.FilePath, a.Content, a.Binary) for a in args], procs=16)
+    return _ORACLE_CACHE[key]
 
 
 def _config2_args():
@@ -69,7 +83,9 @@ def test_dense_keywords_gpu():
     import torch
     sc = S.Scanner(None)
     small = [S.ScanArgs("dense/small.txt", _dense(4 << 20)), S.ScanArgs("ok.py", b"x = 1\n" * 100)]
-    assert sc.ScanBatch(small) == S.scan_host_reference(sc, small, threads=16)
+    got_small = sc.ScanBatch(small)
+    assert got_small == S.scan_host_reference(sc, small, threads=16)
+    assert got_small == _oracle_all("dense4", small)
     free0, _ = torch.cuda.mem_get_info(0)
     args = [S.ScanArgs("dense/big.txt", _dense(64 << 20)), S.ScanArgs("ok.py", b"x = 1\n" * 100)]
     got, stats = sc.ScanBatch(args, with_stats=True)
@@ -86,7 +102,8 @@ def test_dense_keywords_gpu():
 def test_largest_k1_chunk_gpu(monkeypatch):
     c = synth.generate(40_000_000, seed=23, sizes="lognormal", plant_rate=2e-3)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
-    want = S.Scanner(None).ScanBatch(args)
+    want = _oracle_all("largest", args)                  # the oracle on every file (was: the default chunk's result)
+    assert S.Scanner(None).ScanBatch(args) == want
     monkeypatch.setenv("TSG_K1_CHUNK", str(1 << 20))     # clamped to the hit record's offset range
     got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
     assert stats["chunk_bytes"] == 8192                  # v3: a wave item spans 64 lanes x 4 chunks
@@ -120,6 +137,7 @@ def test_k1_variants_agree_gpu(monkeypatch, abl, chunk):
     c = synth.generate(24_000_000, seed=31, sizes="loguniform", plant_rate=3e-3)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    assert want == _oracle_all("variants", args)
     assert S.Scanner(None).ScanBatch(args) == want
     monkeypatch.setenv("TSG_K1_ABL", abl)
     monkeypatch.setenv("TSG_K1_CHUNK", chunk)
@@ -138,7 +156,7 @@ def test_small_chunks_large_batch_gpu(monkeypatch, chunk):
     # small-launch values; the result is the host confirmer's
     c = synth.generate(300_000_000, seed=37, sizes="lognormal", plant_rate=1e-3)
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
-    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    want = _oracle_all("small300", args)
     assert sum(len(w["Findings"]) for w in want) > 200
     monkeypatch.setenv("TSG_K1_CHUNK", chunk)
     monkeypatch.setenv("TSG_SEGMENT_BYTES", str(1 << 30))   # one segment (no geometric tail)
@@ -158,7 +176,7 @@ def test_line_numbers_at_chunk_edges_gpu():
     c = synth.generate(40_000_000, seed=41, sizes="small", plant_rate=2e-2, layout="src")
     args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
     got = S.Scanner(None).ScanBatch(args)
-    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    want = _oracle_all("edges", args)
     assert sum(len(w["Findings"]) for w in want) > 8000
     for a, g, w in zip(args, got, want):
         assert g == w, a.FilePath
@@ -173,7 +191,7 @@ def test_geometric_tail_segments_gpu(monkeypatch):
     monkeypatch.setenv("TSG_SEGMENT_MIN", str(4 << 20))
     got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
     assert stats["pieces"] >= 4                          # 30, 15, 7.5, 3.75 + rest (MB)
-    want = S.scan_host_reference(S.Scanner(None), args, threads=16)
+    want = _oracle_all("geometric", args)
     assert sum(len(w["Findings"]) for w in want) > 100
     for a, g, w in zip(args, got, want):
         assert g == w, a.FilePath

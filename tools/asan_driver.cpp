@@ -393,6 +393,19 @@ static int run_concurrency(const std::string& dir, const std::string& pdir) {
     for (auto& t : ts) t.join();
     std::printf("reaper: 6 results of %u files freed from 6 threads\n", m);
   }
+  // 5. the engine's multi-device segment pipeline (pipeline.h) on 8 simulated
+  // devices: no failure, a driver's error, a driver's throw, the confirmer's throw
+  for (uint32_t mode = 0; mode < 4; ++mode) {
+    tsg_model_pipeline_stats ms{};
+    const int rc = tsg_test_multi_driver_model(8, 600, mode ? 5 : -1, 4, mode, 200, 100, &ms);
+    if ((rc == 0) != (mode == 0)) return fail("multi_driver_model outcome");
+    if (ms.lanes_outstanding || ms.drivers_alive || ms.segments_confirmed_twice) return fail("multi_driver_model state");
+    if (mode == 0 && ms.segments_confirmed != 600) return fail("multi_driver_model confirmed");
+    std::printf("multi-driver model, mode %u: rc %d, %llu started, %llu confirmed, %llu started after the failure, "
+                "%.1f ms failure -> return\n", mode, rc, static_cast<unsigned long long>(ms.segments_started),
+                static_cast<unsigned long long>(ms.segments_confirmed),
+                static_cast<unsigned long long>(ms.started_after_failure), ms.fail_to_return_ms);
+  }
   tsg_ruleset_free(rs);
   return 0;
 }

@@ -16,6 +16,14 @@ LIB_PATH = os.path.join(_HERE, os.environ.get("TSG_LIB", "libtrivysecret.so"))
 c_char_pp = ctypes.POINTER(ctypes.c_char_p)
 
 
+class TsgModelPipelineStats(ctypes.Structure):
+    _fields_ = [("segments_started", ctypes.c_uint64), ("segments_pushed", ctypes.c_uint64),
+                ("segments_confirmed", ctypes.c_uint64), ("segments_confirmed_twice", ctypes.c_uint64),
+                ("started_after_failure", ctypes.c_uint64), ("lanes_outstanding", ctypes.c_uint32),
+                ("lanes_created", ctypes.c_uint32), ("drivers_alive", ctypes.c_uint32),
+                ("wall_ms", ctypes.c_double), ("fail_to_return_ms", ctypes.c_double)]
+
+
 class TsgStats(ctypes.Structure):
     _fields_ = [("k1_ms", ctypes.c_double), ("k2_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
                 ("d2h_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
@@ -77,6 +85,9 @@ SIGNATURES = [
     ("tsg_test_go_sort", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     ("tsg_test_readback", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.POINTER(ctypes.c_uint32)]),
+    ("tsg_test_multi_driver_model", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.POINTER(TsgModelPipelineStats)]),
     ("tsg_test_engine_footprint", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                                   ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     ("tsg_test_inject_segment_failures", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),

@@ -52,6 +52,12 @@ int fail(int code, const std::string& m) { g_err = m; return code; }
   }
 }  // namespace
 
+// the C-ABI's error slot for test hooks defined in other files (pipeline_model.cpp)
+namespace tsg {
+int capi_fail(int code, const std::string& m);
+}
+int tsg::capi_fail(int code, const std::string& m) { return fail(code, m); }
+
 struct tsg_ruleset {
   std::shared_ptr<Ruleset> rs;
 };

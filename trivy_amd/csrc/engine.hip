@@ -33,6 +33,7 @@
 
 #include "crstrip.h"
 #include "engine.h"
+#include "pipeline.h"
 #include "threadpool.h"
 
 namespace tsg {
@@ -1689,63 +1690,6 @@ int device_of(const void* p) {
   return a.device;
 }
 
-// Blocking hand-off of finished segments from the device drivers to the confirmer.
-template <typename T>
-class JobQueue {
- public:
-  JobQueue(int producers, size_t cap) : producers_(producers), cap_(cap) {}
-  void push(std::unique_ptr<T> j) {
-    std::unique_lock<std::mutex> lk(mu_);
-    space_.wait(lk, [&] { return q_.size() < cap_ || aborted_; });
-    q_.push_back(std::move(j));
-    ready_.notify_one();
-  }
-  void producer_done() {
-    std::lock_guard<std::mutex> lk(mu_);
-    --producers_;
-    ready_.notify_all();
-  }
-  void abort() {
-    std::lock_guard<std::mutex> lk(mu_);
-    aborted_ = true;
-    space_.notify_all();
-    ready_.notify_all();
-  }
-  bool aborted() {
-    std::lock_guard<std::mutex> lk(mu_);
-    return aborted_;
-  }
-  // nullptr once every producer is done and the queue is drained; with
-  // spin_us > 0 the caller first polls that long (yielding) before it sleeps
-  // on the condition variable (a futex wake-up under a busy pool took ~0.1 ms)
-  std::unique_ptr<T> pop(int* producers_left, int spin_us = 0) {
-    std::unique_lock<std::mutex> lk(mu_);
-    if (spin_us > 0) {
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
-      while (q_.empty() && producers_ != 0 && !aborted_ && std::chrono::steady_clock::now() < until) {
-        lk.unlock();
-        std::this_thread::yield();
-        lk.lock();
-      }
-    }
-    ready_.wait(lk, [&] { return !q_.empty() || producers_ == 0 || aborted_; });
-    *producers_left = producers_;
-    if (q_.empty()) return nullptr;
-    std::unique_ptr<T> j = std::move(q_.front());
-    q_.pop_front();
-    space_.notify_one();
-    return j;
-  }
-
- private:
-  std::mutex mu_;
-  std::condition_variable ready_, space_;
-  std::deque<std::unique_ptr<T>> q_;
-  int producers_;
-  size_t cap_;
-  bool aborted_ = false;
-};
-
 void add_stats(ScanStats* a, const ScanStats& s) {
   a->k1_ms += s.k1_ms; a->k2_ms += s.k2_ms; a->h2d_ms += s.h2d_ms; a->d2h_ms += s.d2h_ms;
   a->hits += s.hits; a->candidates += s.candidates; a->k1_launches += s.k1_launches;
@@ -2788,10 +2732,12 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
     size_t seg = 0;
     GpuOut out;
   };
-  JobQueue<Job> q(static_cast<int>(drivers.size()), 2 * drivers.size() + 2);
-  std::atomic<size_t> next_seg{0};
+  // the segment counter, the job queue and the driver fan-out (pipeline.h;
+  // its failure behaviour is tested on simulated devices by
+  // tsg_test_multi_driver_model)
+  DriverPipeline<Job> pipe(static_cast<int>(drivers.size()), segs.size());
+  JobQueue<Job>& q = pipe.queue();
   std::mutex st_mu;
-  std::string drv_err;
   double gpu_busy = 0;
   auto t_feed0 = std::chrono::steady_clock::now();
   std::atomic<int64_t> feed_end_ns{0};
@@ -2810,7 +2756,8 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       (void)hipGetLastError();
   }
   const bool direct = h_dev != nullptr;
-  auto driver = [&](DeviceTables* dt) {
+  auto driver = [&](int di, std::string* e_out) -> bool {
+    DeviceTables* dt = drivers[di];
     std::string e;
     ScanStats dst;
     auto tb = std::chrono::steady_clock::now();
@@ -2865,14 +2812,14 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       if (!confirmer_idle.load(std::memory_order_acquire)) plan_confirm(segs[pending->seg], &pending->out);
       q.push(std::move(pending));
     };
-    size_t cur = ok ? next_seg.fetch_add(1) : segs.size();
+    size_t cur = ok ? pipe.next_segment() : segs.size();
     int slot = 0;
     if (ok && host_profile_) hipEventRecord(ln->anchor, resident ? ln->compute : ln->copy);
     if (ok && cur < segs.size() && !resident && !direct) ok = upload(cur, slot);
     while (ok && cur < segs.size() && !q.aborted()) {
       // (resident data: the next segment is taken when this one is done, so
       // two drivers take them in order)
-      const size_t nxt = resident ? segs.size() : next_seg.fetch_add(1);
+      const size_t nxt = resident ? segs.size() : pipe.next_segment();
       // the next segment's upload goes behind this one's on the copy stream;
       // its ring slot was last read by the segment before this one, whose
       // kernels have completed (run_segment returns after its D2H)
@@ -2933,7 +2880,7 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       }
       add_stats(&dst, sst);
       pending = std::move(job);
-      cur = resident ? next_seg.fetch_add(1) : nxt;
+      cur = resident ? pipe.next_segment() : nxt;
       slot ^= 1;
     }
     if (ok) plan_pending();
@@ -2953,60 +2900,41 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
       std::lock_guard<std::mutex> lk(st_mu);
       add_stats(st, dst);
       gpu_busy = dual ? std::max(gpu_busy, ms_since(tb)) : gpu_busy + ms_since(tb);
-      if (!ok && drv_err.empty()) drv_err = e.empty() ? "device driver failed" : e;
     }
-    if (!ok) q.abort();
-    q.producer_done();
+    if (!ok) *e_out = e;
+    return ok;
   };
   CallCtx* cc = acquire_call();
-  std::vector<std::thread> threads;
   uint64_t nconf = 0, nfind = 0;
   double host_ms = 0;
-  std::string host_err;
   // one segment on one device (per-file Scan batches, small batches): the
   // driver runs on this thread -- a thread start and hand-off cost more than
   // the segment's GPU passes
   const bool inline_driver = segs.size() == 1 && drivers.size() == 1;
-  try {
-    if (!inline_driver) for (DeviceTables* dt : drivers) threads.emplace_back(driver, dt);
-    // per-file result slots (hundreds of thousands for image layers) are set up
-    // while the first segment's upload and GPU passes run
-    results->clear();
-    results->resize(in.nfiles);
-    if (inline_driver) driver(drivers[0]);
-    if (host_profile_) std::fprintf(stderr, "[tsg tl] %u result slots ready at %.3f ms\n", in.nfiles, ms_since(t_feed0));
-    for (;;) {
-      int left = 0;
-      confirmer_idle.store(true, std::memory_order_release);
-      std::unique_ptr<Job> job = q.pop(&left, pop_spin_us_);
-      confirmer_idle.store(false, std::memory_order_release);
-      if (!job) break;
-      auto th = std::chrono::steady_clock::now();
-      const Segment& sg = segs[job->seg];
-      const double c_start = host_profile_ ? ms_since(t_feed0) : 0.0;
-      // (drivers that block on an event leave every core to the pool)
-      confirm_segment(*cc, sg, job->out, results->data() + sg.f0, &nconf, &nfind, left > 0 && !dual);
-      host_ms += ms_since(th);
-      if (host_profile_) std::fprintf(stderr, "[tsg tl] seg %zu confirm %.3f-%.3f ms\n", job->seg, c_start, ms_since(t_feed0));
-    }
-  } catch (const std::exception& x) {
-    // (bad_alloc in the confirmation, or a driver thread that could not be
-    // started): stop the drivers, join them, fail the call
-    host_err = std::string("host exception: ") + x.what();
-  } catch (...) {
-    host_err = "host exception";
-  }
-  if (!host_err.empty()) {
-    q.abort();
-    for (;;) {                                   // drain what the drivers still hand over
-      int left = 0;
-      if (!q.pop(&left)) break;
-    }
-  }
-  for (auto& t : threads) t.join();
+  std::string run_err;
+  const bool run_ok = pipe.run(
+      inline_driver, driver,
+      [&] {
+        // per-file result slots (hundreds of thousands for image layers) are set up
+        // while the first segment's upload and GPU passes run
+        results->clear();
+        results->resize(in.nfiles);
+        if (host_profile_) std::fprintf(stderr, "[tsg tl] %u result slots ready at %.3f ms\n", in.nfiles, ms_since(t_feed0));
+      },
+      [&](Job& job, int left) {
+        auto th = std::chrono::steady_clock::now();
+        const Segment& sg = segs[job.seg];
+        const double c_start = host_profile_ ? ms_since(t_feed0) : 0.0;
+        confirmer_idle.store(false, std::memory_order_release);
+        // (drivers that block on an event leave every core to the pool)
+        confirm_segment(*cc, sg, job.out, results->data() + sg.f0, &nconf, &nfind, left > 0 && !dual);
+        confirmer_idle.store(true, std::memory_order_release);
+        host_ms += ms_since(th);
+        if (host_profile_) std::fprintf(stderr, "[tsg tl] seg %zu confirm %.3f-%.3f ms\n", job.seg, c_start, ms_since(t_feed0));
+      },
+      pop_spin_us_, &run_err);
   release_call(cc);
-  if (!host_err.empty()) { *err = host_err; return false; }
-  if (!drv_err.empty()) { *err = drv_err; return false; }
+  if (!run_ok) { *err = run_err; return false; }
   st->bytes = total;
   st->files = in.nfiles;
   st->pieces = static_cast<uint32_t>(segs.size());
