@@ -62,8 +62,10 @@ def _oracle_scan(item):
     return _ORACLE.scan(path, content, binary)
 
 
-def cpu_baseline(items, procs, cfg_path=None):
-    """Oracle over `items` [(path, content, binary)] with a process pool."""
+def cpu_baseline(items, procs, cfg_path=None, log=None, what="oracle"):
+    """Oracle over `items` [(path, content, binary)] with a process pool; a
+    progress line every ~20 s through `log` (a silent multi-minute leg looks
+    hung to the GPU runner)."""
     import multiprocessing as mp
     nbytes = sum(len(c) for _, c, _ in items)
     ctx = mp.get_context("fork")
@@ -71,10 +73,14 @@ def cpu_baseline(items, procs, cfg_path=None):
         t0 = time.perf_counter()
         # largest files first (LPT): one 64 MB file is seconds of oracle work
         order = sorted(range(len(items)), key=lambda j: -len(items[j][1]))
-        got = pool.map(_oracle_scan, [items[j] for j in order], chunksize=1)
         res = [None] * len(items)
-        for j, r in zip(order, got):
+        t_log, done_b = t0, 0
+        for j, r in zip(order, pool.imap(_oracle_scan, [items[j] for j in order], chunksize=1)):
             res[j] = r
+            done_b += len(items[j][1])
+            if log is not None and time.perf_counter() - t_log > 20:
+                t_log = time.perf_counter()
+                log("%s: %.2f of %.2f GB checked (%.0f s)" % (what, done_b / 1e9, nbytes / 1e9, t_log - t0))
         dt = time.perf_counter() - t0
     return nbytes / dt / 1e9, res, dt, nbytes
 
@@ -1026,7 +1032,7 @@ def main():
         idx = pick_sample(batch.offsets, int(args.cpu_sample_mb * 1e6), args.seed)
         items = [(batch.paths[i], batch.file(i), bool(batch.binary[i]) if batch.binary is not None else False)
                  for i in idx]
-        gbps, ores, dt, nb = cpu_baseline(items, procs, cfg_path)
+        gbps, ores, dt, nb = cpu_baseline(items, procs, cfg_path, log, "cpu baseline (oracle)")
         diff = [batch.paths[i] for j, i in enumerate(idx) if ores[j] != gpu_results[i]]
         ofind = sum(len(r["Findings"]) for r in ores)
         out["cpu_baseline"] = {
@@ -1072,7 +1078,9 @@ def main():
             rest = [i for i in pidx if i not in base]
             ritems = [(batch.paths[i], batch.file(i), bool(batch.binary[i]) if batch.binary is not None else False)
                       for i in rest]
-            _, rres, pdt, rnb = cpu_baseline(ritems, procs, cfg_path)
+            log("parity: the oracle on %d more files (%.2f GB) to reach %.0f%% of the batch" % (
+                len(rest), sum(len(c) for _, c, _ in ritems) / 1e9, 100 * args.parity_share))
+            _, rres, pdt, rnb = cpu_baseline(ritems, procs, cfg_path, log, "parity (oracle)")
             del ritems
             diff += [batch.paths[i] for j, i in enumerate(rest) if rres[j] != gpu_results[i]]
             pfind += sum(len(r["Findings"]) for r in rres)

@@ -619,9 +619,11 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
     conf_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_conf).count();
   }
   if (prof) {
-    std::fprintf(stderr, "[tsg model] confirm %.1f ms: keywords %.1f, find %.1f, blocks %.1f, findings %.1f, sort %.1f\n",
-                 conf_ns / 1e6, g_scan_prof[0].load() / 1e6, g_scan_prof[1].load() / 1e6, g_scan_prof[2].load() / 1e6,
-                 g_scan_prof[3].load() / 1e6, g_scan_prof[4].load() / 1e6);
+    std::fprintf(stderr, "[tsg model] confirm %.1f ms: keywords %.1f, find %.1f (whole-file find-alls %.1f ms in %llu "
+                 "calls), blocks %.1f, findings %.1f, sort %.1f\n",
+                 conf_ns / 1e6, g_scan_prof[0].load() / 1e6, g_scan_prof[1].load() / 1e6, g_scan_prof[5].load() / 1e6,
+                 static_cast<unsigned long long>(g_scan_prof[7].load()),
+                 g_scan_prof[2].load() / 1e6, g_scan_prof[3].load() / 1e6, g_scan_prof[4].load() / 1e6);
   }
   *out = r;
   return TSG_OK;

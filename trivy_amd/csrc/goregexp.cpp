@@ -798,6 +798,16 @@ inline bool rune_match(const Prog& p, const Inst& in, int32_t c) {
   return false;
 }
 
+// The bit-state backtracker's visited set of one thread (see backtrack()).
+struct VisitStamps {
+  std::vector<uint16_t> stamp;
+  uint16_t gen = 0;
+};
+VisitStamps& visit_stamps() {
+  thread_local VisitStamps v;
+  return v;
+}
+
 class Machine {
  public:
   Machine(const Prog& p, int ncap) : p_(p), ncap_(ncap) {
@@ -874,7 +884,16 @@ class Machine {
   int backtrack(const uint8_t* s, size_t len, size_t pos0, size_t window, Cap* caps_out) {
     const size_t end = std::min(len, pos0 + window);
     const size_t npos = end - pos0 + 1;
-    visited_.assign((p_.inst.size() * npos + 31) / 32, 0u);
+    // visited (pc, pos) pairs: generation stamps in one per-thread array
+    // shared by every Machine of the thread (calls never nest), so a call
+    // clears nothing -- clearing Go's bitmap (program size x window bits,
+    // ~5 KB for config 5's custom rules) was a fifth of a candidate's cost
+    VisitStamps& vs = visit_stamps();
+    const size_t nvis = p_.inst.size() * npos;
+    if (vs.stamp.size() < nvis) { vs.stamp.assign(nvis, 0); vs.gen = 0; }
+    if (++vs.gen == 0) { std::fill(vs.stamp.begin(), vs.stamp.end(), 0); vs.gen = 1; }
+    uint16_t* const stamp = vs.stamp.data();
+    const uint16_t gen = vs.gen;
     const int nc = std::max(ncap_, 2);
     bcap_.assign(nc, -1);
     jobs_.clear();
@@ -888,8 +907,8 @@ class Machine {
       for (;;) {
         if (pc == 0) break;
         const size_t bit = static_cast<size_t>(pc) * npos + (pos - pos0);
-        if (visited_[bit >> 5] & (1u << (bit & 31))) break;
-        visited_[bit >> 5] |= 1u << (bit & 31);
+        if (stamp[bit] == gen) break;
+        stamp[bit] = gen;
         const Inst& in = p_.inst[pc];
         bool fail = false;
         switch (in.op) {
@@ -956,7 +975,6 @@ class Machine {
   std::vector<Frame> stack_;
   struct BJob { uint32_t pc; size_t pos; int slot; Cap old; };   // slot >= 0: a capture restore
   std::vector<BJob> jobs_;
-  std::vector<uint32_t> visited_;
   std::vector<Cap> bcap_;
 
   bool contains(int q, uint32_t pc) const {

@@ -144,11 +144,12 @@ void index_excludes(Ruleset* rs) {
 
 }  // namespace
 
-// Ruleset::AllowPathIndex: the literals of every global allow-path regex's
-// gate (each unit's alternatives expanded, at most kMaxLits per regex; a
-// regex past that or without a gate is always run) in one Aho-Corasick DFA.
-static void build_allow_index(Ruleset* rs) {
-  Ruleset::AllowPathIndex& ix = rs->allow_index;
+// Ruleset::AllowPathIndex: the literals of every global allow rule's path
+// (or, for the match index, text) regex's gate (each unit's alternatives
+// expanded, at most kMaxLits per regex; a regex past that or without a gate
+// is always run) in one Aho-Corasick DFA.
+static void build_allow_index(Ruleset* rs, RegexpPtr AllowRule::*field, Ruleset::AllowPathIndex* ixp) {
+  Ruleset::AllowPathIndex& ix = *ixp;
   ix = Ruleset::AllowPathIndex();
   if (rs->allow_rules.size() > 64) return;
   constexpr size_t kMaxLits = 512, kMaxStates = 4096;
@@ -156,7 +157,7 @@ static void build_allow_index(Ruleset* rs) {
   go[0].fill(-1);
   std::vector<uint64_t> out(1, 0);
   for (size_t j = 0; j < rs->allow_rules.size(); ++j) {
-    const auto& path = rs->allow_rules[j].path;
+    const auto& path = rs->allow_rules[j].*field;
     if (!path) continue;
     std::vector<std::string> lits;
     bool ok = path->has_gate();
@@ -224,7 +225,8 @@ bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
     out->allow_rules = std::move(b_allow);
     out->exclude_block.clear();
     index_excludes(out);
-    build_allow_index(out);
+    build_allow_index(out, &AllowRule::path, &out->allow_index);
+    build_allow_index(out, &AllowRule::regex, &out->allow_match_index);
     return true;
   }
   std::vector<std::string> enable = str_list(cfg->get("enable-builtin-rules"));
@@ -270,15 +272,20 @@ bool build_ruleset(const JValue* cfg, Ruleset* out, std::string* err) {
   for (auto& a : custom_allow) if (!contains(disable_allow, a.id)) out->allow_rules.push_back(a);
   out->exclude_block = std::move(excl);
   index_excludes(out);
-  build_allow_index(out);
+  build_allow_index(out, &AllowRule::path, &out->allow_index);
+  build_allow_index(out, &AllowRule::regex, &out->allow_match_index);
   return true;
 }
 
-bool global_allow_path(const Ruleset& rs, const uint8_t* p, size_t n) {
-  const Ruleset::AllowPathIndex& ix = rs.allow_index;
+namespace {
+// Some global allow rule's `field` regex matches p[0, n) (scanner.go:52-59):
+// the rules whose gate literals occur in the text, found in one pass of the
+// index, are the only ones that can; the plain loop when the index is unusable.
+bool global_allow_indexed(const Ruleset& rs, const Ruleset::AllowPathIndex& ix, RegexpPtr AllowRule::*field,
+                          const uint8_t* p, size_t n) {
   if (!ix.usable) {
     for (const auto& r : rs.allow_rules)
-      if (r.path && r.path->match_string(p, n)) return true;
+      if ((r.*field) && (r.*field)->match_string(p, n)) return true;
     return false;
   }
   uint64_t cand = ix.always;
@@ -290,9 +297,18 @@ bool global_allow_path(const Ruleset& rs, const uint8_t* p, size_t n) {
   while (cand) {                       // a rule none of whose gate literals occurs cannot match
     const int j = __builtin_ctzll(cand);
     cand &= cand - 1;
-    if (rs.allow_rules[j].path->match_string(p, n)) return true;
+    if ((rs.allow_rules[j].*field)->match_string(p, n)) return true;
   }
   return false;
+}
+}  // namespace
+
+bool global_allow_path(const Ruleset& rs, const uint8_t* p, size_t n) {
+  return global_allow_indexed(rs, rs.allow_index, &AllowRule::path, p, n);
+}
+
+bool global_allow_match(const Ruleset& rs, const uint8_t* m, size_t n) {
+  return global_allow_indexed(rs, rs.allow_match_index, &AllowRule::regex, m, n);
 }
 
 // ---------------------------------------------------------------- helpers
@@ -528,7 +544,7 @@ void find_locations(const Ruleset& rs, const Rule& rule, const uint8_t* c, size_
   for (size_t k = 0; k + stride <= m.size(); k += stride) {
     const long s = m[k], e = m[k + 1];
     // AllowLocation (scanner.go:150-153): global then rule allow regexes on the whole match
-    if (allow_match(rs.allow_rules, c + s, e - s) || allow_match(rule.allow_rules, c + s, e - s)) continue;
+    if (global_allow_match(rs, c + s, e - s) || allow_match(rule.allow_rules, c + s, e - s)) continue;
     if (!sub) { locs->push_back({s, e}); continue; }
     for (int gi : rule.secret_groups) {                // scanner.go:155-168
       Loc l{m[k + 2 * gi], m[k + 2 * gi + 1]};
@@ -854,7 +870,7 @@ std::atomic<bool> g_scan_prof_on{false};
 namespace {
 struct Matched { const Rule* rule; Loc loc; };
 }  // namespace
-std::atomic<uint64_t> g_scan_prof[5];
+std::atomic<uint64_t> g_scan_prof[8];   // phase ns [0..4]; [5] ns of whole-file find-alls, [7] their count
 
 namespace {
 struct PhaseClock {
@@ -920,7 +936,14 @@ Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, si
     static const std::vector<uint64_t> kEmpty;
     const std::vector<uint64_t>* use = nullptr;
     if (kind == kPlanCandidates || kind == kPlanCandHostGate) use = starts ? starts : &kEmpty;
-    find_locations(rs, rule, content, len, use, &locs, &out.error);
+    if (pc.on && !use) {
+      const auto tf = std::chrono::steady_clock::now();
+      find_locations(rs, rule, content, len, use, &locs, &out.error);
+      g_scan_prof[5].fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tf).count());
+      g_scan_prof[7].fetch_add(1);
+    } else {
+      find_locations(rs, rule, content, len, use, &locs, &out.error);
+    }
     pc.lap(1);
     if (locs.empty()) continue;
     Blocks lblocks(content, len, rule.exclude_block, plan, rs.rules.size() + rule.exclude_base);

@@ -56,6 +56,7 @@ struct Ruleset {                         // scanner.go:45-49 (Global)
     uint64_t always = 0;         // allow rules with a path regex but no (expandable) gate
     bool usable = false;         // <= 64 allow rules and the automaton fits
   } allow_index;
+  AllowPathIndex allow_match_index;   // the same over the global allow rules' text regexes
 };
 
 // Scanner.AllowPath (scanner.go:205-212): some global allow rule's path regex
@@ -64,6 +65,10 @@ bool global_allow_path(const Ruleset& rs, const uint8_t* path, size_t n);
 inline bool global_allow_path(const Ruleset& rs, const std::string& path) {
   return global_allow_path(rs, reinterpret_cast<const uint8_t*>(path.data()), path.size());
 }
+
+// AllowRules.Allow over the global allow rules (scanner.go:52-54, called from
+// AllowLocation :150-153): some rule's text regex matches the match text.
+bool global_allow_match(const Ruleset& rs, const uint8_t* m, size_t n);
 
 // ParseConfig (already decoded from YAML to JSON) + NewScanner: builtin rules
 // and allow rules, enable/disable filters, custom rules appended
@@ -193,7 +198,7 @@ std::string go_quote(const std::string& s);
 // TSG_HOST_PROFILE: scan_file's time per phase (ns, summed over threads):
 // 0 keyword gate, 1 find_locations, 2 exclude blocks, 3 censor + findings, 4 sort
 extern std::atomic<bool> g_scan_prof_on;
-extern std::atomic<uint64_t> g_scan_prof[5];
+extern std::atomic<uint64_t> g_scan_prof[8];
 Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl = nullptr);
 
