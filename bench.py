@@ -552,7 +552,11 @@ def k1_build(src=None):
     c = src.find(b"\n// ==== host side")
     if min(a, b, c) < 0 or not a < b < c:
         raise RuntimeError("engine.hip lacks the K1 build-hash markers")
-    return hashlib.sha256(src[:a] + src[b:c]).hexdigest()[:16]
+    import re
+    # the measurement builds listed under #ifdef TSG_K1_PROBE exist only in
+    # the probe library: not part of the product's K1
+    k1 = re.sub(rb"#ifdef TSG_K1_PROBE\n.*?#endif[^\n]*\n", b"", src[:a] + src[b:c], flags=re.S)
+    return hashlib.sha256(k1).hexdigest()[:16]
 
 
 def gather_ranks(dist, world, mine):
@@ -562,6 +566,11 @@ def gather_ranks(dist, world, mine):
     got = [None] * world
     dist.all_gather_object(got, mine)
     return got
+
+
+def _segment_balanced():
+    """large-file batches cut into equal segments (engine default; TSG_SEGMENT_BALANCED=0: full segments + rest)"""
+    return os.environ.get("TSG_SEGMENT_BALANCED", "1") != "0"
 
 
 def _segment_bytes():
@@ -823,7 +832,8 @@ def main():
         tj = json.load(open(tpath))
         lay = tj.get("layout", {})
         if (tj.get("k1_build") == k1_build() and lay.get("config") == args.config
-                and lay.get("segment_bytes") == _segment_bytes() and lay.get("chunk_bytes") == stats[-1]["chunk_bytes"]):
+                and lay.get("segment_bytes") == _segment_bytes() and lay.get("chunk_bytes") == stats[-1]["chunk_bytes"]
+                and (args.config not in (2, 4) or lay.get("segment_balanced", False) == _segment_balanced())):
             traffic = round(tj["traffic_over_algorithmic"] * nbytes / segments)
             traffic_src = "%s: %.3f HBM bytes per content byte, K1 dispatches of this layout and build %s (%s)" % (
                 os.path.relpath(tpath, ROOT), tj["traffic_over_algorithmic"], tj["k1_build"], tj.get("source", ""))
@@ -863,6 +873,7 @@ def main():
             "parallelism": "file shards per GPU, no collective (dp%d)" % world,
             "host_confirm_threads": args.threads,
             "segment_bytes": _segment_bytes(),
+            "segment_balanced": _segment_balanced(),
             "config_id": args.config,
             "numa": numa,
         },

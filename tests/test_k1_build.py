@@ -43,6 +43,15 @@ def test_k2_and_host_edits_keep_build_hash(marker):
     assert bench.k1_build(_edit_inside(marker)) == bench.k1_build(SRC)
 
 
+def test_probe_only_variants_keep_build_hash():
+    # the TSG_K1_PROBE variant list exists only in the probe library
+    i = SRC.find(b"#ifdef TSG_K1_PROBE\n    TSG_K1_V3(")
+    assert i > 0
+    j = SRC.find(b"TSG_K1_V3(0)", i)
+    edited = SRC[:j] + b"TSG_K1_V3(7) " + SRC[j:]
+    assert bench.k1_build(edited) == bench.k1_build(SRC)
+
+
 def test_markers_in_order():
     a, b, c = (SRC.find(m) for m in (b"\n// ==== K2 begin", b"\n// ==== K2 end", b"\n// ==== host side"))
     assert 0 < a < b < c

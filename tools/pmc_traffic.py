@@ -58,6 +58,7 @@ def main():
         "k1_build": bench["roofline"].get("k1_build") if bench else None,
         "layout": {"config": bench["config"].get("config_id") if bench else None,
                    "segment_bytes": bench["config"].get("segment_bytes") if bench else None,
+                   "segment_balanced": bench["config"].get("segment_balanced", False) if bench else None,
                    "chunk_bytes": bench["breakdown_ms"].get("chunk_bytes") if bench else None},
         "source": run,
         "bytes_per_launch": bench["roofline"]["bytes_per_launch"] if bench else None,

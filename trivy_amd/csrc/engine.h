@@ -162,6 +162,7 @@ class Engine {
   double last_piece_ = 0.08;
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
   uint64_t segment_min_ = 64ull << 20;   // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1; r4p: 64 MB 53.2 vs 128 MB 52.5)
+  bool balanced_ = true;                // uploaded large-file data: equal segments of <= segment_ (TSG_SEGMENT_BALANCED)
   uint64_t segment_tail_ = 0;           // uploaded data: a short last segment (TSG_SEGMENT_TAIL; 0 = none: the
                                         // rest after the full segments is one launch, K1 keeps its large-launch rate)
   uint64_t segment_ = 4ull << 30;       // uploaded data: bytes per pipeline segment (TSG_SEGMENT_BYTES);

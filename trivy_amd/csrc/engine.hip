@@ -1203,7 +1203,7 @@ const void* k1_kernel(int abl, bool compressed) {
     TSG_K1_V3(80) TSG_K1_V3(144) TSG_K1_V3(208) TSG_K1_V3(272) TSG_K1_V3(400) TSG_K1_V3(448)
     TSG_K1_V3(464) TSG_K1_V3(465) TSG_K1_V3(466) TSG_K1_V3(468) TSG_K1_V3(472) TSG_K1_V3(496) TSG_K1_V3(976) TSG_K1_V3(1488)
     TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4592) TSG_K1_V3(8656) TSG_K1_V3(12752)
-    TSG_K1_V3(4562) TSG_K1_V3(5072) TSG_K1_V3(65536 + 4560) TSG_K1_V3(131072 + 4560) TSG_K1_V3(131072 + 4592)
+    TSG_K1_V3(4561) TSG_K1_V3(4562) TSG_K1_V3(5072) TSG_K1_V3(65536 + 4560) TSG_K1_V3(131072 + 4560) TSG_K1_V3(131072 + 4592)
     TSG_K1_V3(262144 + 464) TSG_K1_V3(262144 + 4592) TSG_K1_V3(262144 + 4560)
 #endif
 #undef TSG_K1_V3
@@ -1735,6 +1735,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const long long v = std::atoll(c);
     if (v >= 4096) e->segment_min_ = static_cast<uint64_t>(v);
   }
+  if (const char* c = std::getenv("TSG_SEGMENT_BALANCED")) e->balanced_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_SEGMENT_TAIL")) {
     const long long v = std::atoll(c);
     if (v >= 0) e->segment_tail_ = static_cast<uint64_t>(v);
@@ -2649,7 +2650,14 @@ bool Engine::scan(const BatchInput& in, SecretVec* results, ScanStats* st, std::
         // are left: a full segment's confirmation then hides behind the next
         // half-size upload; r3t config 5: 4.3+4.3+0.7+... GB left 16 ms after
         // the last upload, the second segment's 25 ms confirmation)
-        if (geometric ? rest >= 2 * segment_ : rest > segment_ + tail) target = in.offsets[f] + segment_;
+        // (large-file batches: the rest is cut into ceil(rest / segment_)
+        // equal segments instead of full segments plus a short remainder, so
+        // every K1 launch runs at its large-launch rate: a 10 GB batch is
+        // 3 x 3.33 GB, not 4 + 4 + 1.4 GB whose last launch ran at ~2.3 TB/s;
+        // TSG_SEGMENT_BALANCED=0 keeps full segments)
+        const uint64_t kleft = (rest + segment_ - 1) / segment_;
+        if (!geometric && balanced_ && tail == 0 && kleft >= 2) target = in.offsets[f] + rest / kleft;
+        else if (geometric ? rest >= 2 * segment_ : rest > segment_ + tail) target = in.offsets[f] + segment_;
         else if (geometric && rest / 2 >= segment_min_) target = in.offsets[f] + rest / 2;
         else if (tail > 0 && rest > 2 * tail) target = total - tail;
         else break;
