@@ -11,6 +11,7 @@
 #   pmc[:NAME[:ARGS]]          tools/pmc_k1.sh passes over bench.py ARGS
 #   traffic[:NAME[:ARGS]]      tools/pmc_traffic.sh (FETCH_SIZE / WRITE_SIZE) over bench.py ARGS
 #   py:NAME:SECONDS:SCRIPT ARGS   python -u SCRIPT ARGS under its own limit
+#   bin:NAME:SECONDS:PROGRAM ARGS a built tool (e.g. tools/load_probe) under its own limit
 #   env:NAME=VALUE             export NAME=VALUE for the following steps ("env:NAME=" unsets it)
 # e.g. tools/gpu_run.sh rd3a tests smoke bench "bench:c1:--config 1" prof
 set -o pipefail
@@ -51,6 +52,10 @@ for STEP in "$@"; do
       bash tools/pmc_traffic.sh $OUT/${NAME:-traffic} $ARGS || exit 1 ;;
     env)
       if [ -n "${REST#*=}" ]; then export "$REST"; else unset "${REST%%=*}"; fi ;;
+    bin)
+      SECS=${ARGS%%:*}; CMD=${ARGS#*:}
+      timeout -k 10 $SECS $CMD > $OUT/$NAME.log 2>&1 || { tail -30 $OUT/$NAME.log; exit 1; }
+      tail -20 $OUT/$NAME.log ;;
     py)
       SECS=${ARGS%%:*}; SCRIPT=${ARGS#*:}
       timeout -k 10 $SECS python -u $SCRIPT > $OUT/$NAME.log 2>&1 || { tail -30 $OUT/$NAME.log; exit 1; }

@@ -19,6 +19,18 @@ layout:
             are live together, with padding in LDS
   rootrep   current + the root row replicated per lane in a transposed
             layout (a root-state lane always reads its own bank)
+  rootskip  (round 6) lanes at the root state skip the
+            transition read (EXEC-masked off: they take the root's next
+            state from a widened class map instead); reported with the class
+            map read that then costs more: a 16-bit map entry per byte value
+            (class and root successor) has ASCII on 64 dwords instead of 32,
+            so bytes 64 apart collide
+  hotphase  (round 6, item 1b) current + the K hottest states' rows shifted
+            by 0-31 dwords of padding, each shift chosen greedily (two sweeps,
+            coordinate descent) to minimise the replayed conflict cycles;
+            trained on half of the waves, reported on the other half
+  qword     rows read as 8-byte units (ds_read_b64: 64 banks, a lane takes
+            two; four classes per unit, so same-state lanes broadcast more)
 
   python tools/lds_bank_sim.py [--mb 64] [--waves 64] [--layouts current,freq,phase]
 """
@@ -65,18 +77,22 @@ def lane_states(nxt, cls, text, starts, length):
     return out, cl
 
 
-def cycles(dwords):
-    """LDS cycles per wave-instruction: dwords (steps, 64) -> mean over steps of the two half-waves' max bank load."""
+def cycles(dwords, active=None):
+    """LDS cycles per wave-instruction: dwords (steps, 64) -> mean over steps of the two half-waves' max bank load.
+    active (optional, same shape): lanes taking part (EXEC); a group with no active lane costs 1 (issue)."""
     tot = 0.0
     for h in range(2):
-        d = np.sort(dwords[:, 32 * h:32 * h + 32], axis=1)
+        d = dwords[:, 32 * h:32 * h + 32]
+        if active is not None:
+            d = np.where(active[:, 32 * h:32 * h + 32], d, -1)
+        d = np.sort(d, axis=1)
         new = np.ones_like(d, dtype=bool)
         new[:, 1:] = d[:, 1:] != d[:, :-1]
-        bank = d % 32
-        rows = np.repeat(np.arange(d.shape[0]), 32).reshape(d.shape)
-        cnt = np.zeros((d.shape[0], 32), dtype=np.int64)
-        np.add.at(cnt, (rows[new], bank[new]), 1)
-        tot += cnt.max(axis=1).mean()
+        new &= d >= 0
+        bank = np.where(d >= 0, d % 32, 0)
+        key = np.arange(d.shape[0])[:, None] * 32 + bank
+        cnt = np.bincount(key[new], minlength=d.shape[0] * 32).reshape(d.shape[0], 32)
+        tot += np.maximum(cnt.max(axis=1), 1).mean()
     return tot
 
 
@@ -100,6 +116,7 @@ def main():
     ap.add_argument("--waves", type=int, default=48)
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--layouts", default="current,freq,phase")
+    ap.add_argument("--hot", type=int, default=30, help="hotphase: states whose rows are shifted")
     args = ap.parse_args()
     from workload import synth
     nxt, cls, fo = dump_dfa()
@@ -108,11 +125,13 @@ def main():
     text = np.asarray(corp.data[:corp.nbytes])
     rng = np.random.default_rng(1)
     nchunks = corp.nbytes // args.chunk - 1
-    waves = []
+    waves, wave_bytes = [], []
     for w in range(args.waves):
         base = int(rng.integers(0, nchunks - 64))
         starts = [(base + i) * args.chunk for i in range(64)]
         waves.append(lane_states(nxt, cls, text, starts, args.chunk))
+        wave_bytes.append(np.stack([text[s:s + args.chunk] for s in starts], axis=1).astype(np.int64))
+    args.wave_bytes = wave_bytes
     # class frequency over the replay (bytes read) and state occupancy
     cfreq = np.bincount(np.concatenate([cl.ravel() for _, cl in waves]), minlength=C)
     sfreq = np.bincount(np.concatenate([st.ravel() for st, _ in waves]), minlength=n)
@@ -130,6 +149,9 @@ def main():
     perm_freq[order] = np.arange(C)                  # class c -> new index by frequency rank
     results = {}
     for name in args.layouts.split(","):
+        if name in ("rootskip", "hotphase", "qword"):
+            extra(name, waves, nxt, cls, fo, S, So, sfreq, args)
+            continue
         perm = perm_id if name == "current" else perm_freq
         phase = None
         if name == "phase":
@@ -154,6 +176,53 @@ def main():
         results[name] = (tot / len(waves), size * 2)
         print("%-8s LDS cycles per transition read (2 groups, 2.0 = conflict-free): %.3f   table %d B" % (
             name, results[name][0], results[name][1]))
+
+
+def extra(name, waves, nxt, cls, fo, S, So, sfreq, args):
+    """the round-6 candidates (module docstring)"""
+    n, C = nxt.shape
+    rows, _ = layout_rows(n, fo, S, So)
+    base_dw = rows // 2                              # a state's row start in dwords
+    if name == "rootskip":
+        tr = cur = cl_cur = cl_wide = 0.0
+        for (st, cl), b in zip(waves, args.wave_bytes):
+            dw = 64 + base_dw[st] + cl // 2
+            cur += cycles(dw)
+            tr += cycles(dw, st != 0)
+            cl_cur += cycles(b // 4)                   # class map of u8 entries: 4 byte values per dword
+            cl_wide += cycles(b // 2)                  # u16 entries (class + root successor): 2 per dword
+        k = len(waves)
+        print("rootskip transition read %.3f (current %.3f); class map read u8 %.3f -> u16 %.3f: net %+.3f LDS "
+              "cycles per byte, plus a compare and a select on the dependent chain" % (
+                  tr / k, cur / k, cl_cur / k, cl_wide / k, (tr - cur + cl_wide - cl_cur) / k))
+    elif name == "qword":
+        tot = 0.0
+        Rq, Rqo = (C + 3) // 4 | 1, ((C + 3) // 4 + 3) | 1
+        qrow = np.where(np.arange(n) < fo, np.arange(n) * Rq, fo * Rq + (np.arange(n) - fo) * Rqo)
+        for st, cl in waves:
+            tot += cycles(qrow[st] + cl // 4)
+        print("qword    LDS cycles per transition read (ds_read_b64, 8-byte units): %.3f  (+2-3 VALU per byte "
+              "to pick the 16-bit entry)" % (tot / len(waves)))
+    elif name == "hotphase":
+        half = len(waves) // 2
+        st_tr = np.concatenate([w[0] for w in waves[:half]])
+        cl_tr = np.concatenate([w[1] for w in waves[:half]]) // 2
+        st_te = np.concatenate([w[0] for w in waves[half:]])
+        cl_te = np.concatenate([w[1] for w in waves[half:]]) // 2
+        cur = base_dw.copy()
+        best = cycles(64 + cur[st_tr] + cl_tr)
+        base_te = cycles(64 + cur[st_te] + cl_te)
+        for sweep in range(2):
+            for s in np.argsort(-sfreq)[:args.hot]:
+                b0, bestd = base_dw[s], cur[s] - base_dw[s]
+                for d in range(32):
+                    cur[s] = b0 + d
+                    c = cycles(64 + cur[st_tr] + cl_tr)
+                    if c < best - 1e-9:
+                        best, bestd = c, d
+                cur[s] = b0 + bestd
+        print("hotphase %d hottest rows shifted: %.3f on held-out waves (current %.3f), padding <= %d B" % (
+            args.hot, cycles(64 + cur[st_te] + cl_te), base_te, args.hot * 31 * 4))
 
 
 if __name__ == "__main__":
