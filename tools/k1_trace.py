@@ -21,8 +21,8 @@ def launches(path):
         i += 4
         wg = a[i:i + 4 * blocks].reshape(blocks, 4).astype(np.int64)
         i += 4 * blocks
-        it = a[i:i + 4 * items].reshape(items, 4).astype(np.int64)
-        i += 4 * items
+        it = a[i:i + 8 * items].reshape(items, 8).astype(np.int64)   # kTraceItemWords (round 6)
+        i += 8 * items
         yield blocks, nchunks, chunk, wg, it
 
 
@@ -41,13 +41,19 @@ def summarise(k, blocks, nchunks, chunk, wg, it):
         k, blocks, nchunks, chunk, nchunks * chunk / 1e6, len(used), span))
     print("  WG entry: spread %.1f us; table loaded after %.1f us (median), last WG ready at %.1f us" % (
         entry.max() - entry.min(), float(np.median(loaded - entry)), loaded.max()))
+    kus = used[:, 2] >> 24
+    setup, loop, kw = rel(used[:, 3], t0), rel(used[:, 4], t0), rel(used[:, 5], t0)
     for ku in (4, 2, 1):
-        m = used[:, 3] == ku
+        m = kus == ku
         if m.any():
             d = dur[m]
             print("  kU=%d: %6d items, duration us p10 %.1f p50 %.1f p90 %.1f max %.1f; starts %.1f-%.1f" % (
                 ku, m.sum(), *np.percentile(d, [10, 50, 90]), d.max(), st[m].min(), st[m].max()))
-    waves = used[:, 2]
+            print("        phases (p50 us): item taken + range set up (file lookup) %.1f, line loop %.1f, outputs "
+                  "drained + keyword bits flushed %.1f, hit buffer flushed %.1f" % (
+                      np.median(setup[m] - st[m]), np.median(loop[m] - setup[m]), np.median(kw[m] - loop[m]),
+                      np.median(en[m] - kw[m])))
+    waves = used[:, 2] & 0xffffff
     first_start, last_end, busy = {}, {}, {}
     for w, s, e in zip(waves, st, en):
         first_start[w] = min(first_start.get(w, 1e18), s)

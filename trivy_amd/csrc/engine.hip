@@ -359,7 +359,14 @@ constexpr int kAblBndRead = 65536, kAblBndNoFlush = 131072;
 // (s_memrealtime, 100 MHz) in the slack half of the deferred-output buffer,
 // copied to $TSG_K1_TRACE_FILE by the probe library (tools/k1_trace.py)
 constexpr int kAblTrace = 262144;
-constexpr uint32_t kTraceItemCap = 1u << 18;
+// measurement (results valid): every item, the first of each wave included,
+// from the global counter (rounds 1-5).  Default since round 6: a wave's
+// first item is its own index in the grid, so the launch does not start with
+// every wave's atomic on one address (the traces put ~37 us of each
+// first-round item there: 4096 same-address atomics serialised in L2)
+constexpr int kAblAtomicFirst = 524288;
+constexpr uint32_t kTraceItemCap = 1u << 17;
+constexpr uint32_t kTraceItemWords = 8;   // [start, end, kU << 24 | wg << 8 | wave, setup done, loop done, flushed, 0, 0]
 
 // One 16-byte word of one stream with file-boundary and stream-end checks.
 template <int kAbl, bool kC>
@@ -924,7 +931,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
   constexpr uint32_t kTabOff = 256;
-  // kAblTrace: [4 per workgroup: entry, table loaded, exit, hw id][4 per item: start, end, wg << 8 | wave, kU]
+  // kAblTrace: [4 per workgroup: entry, table loaded, exit, hw id][kTraceItemWords per item: start, end,
+  // kU << 24 | wg << 8 | wave, range set up (file found), line loop done, outputs drained + keyword bits flushed]
   uint32_t* const trc = obuf + static_cast<size_t>(gridDim.x) * kThreads * kOutSlots;
   if ((kAbl & kAblTrace) && threadIdx.x == 0) {
     trc[4 * blockIdx.x] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
@@ -985,14 +993,24 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
   const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
   if ((kAbl & kAblTrace) && threadIdx.x == 0) trc[4 * blockIdx.x + 1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+  bool first = !(kAbl & kAblAtomicFirst);
   for (;;) {
     unsigned long long item = 0;
     const uint32_t t_item = (kAbl & kAblTrace) ? static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) : 0u;
-    if (lane == 0) {
-      item = atomicAdd(item_ctr, 1u);
-      *x.w_hitcnt = 0;
+    uint32_t t_setup = 0, t_loop = 0, t_kw = 0;    // (kAblTrace)
+    if (first) {
+      // the first round of items: wave w of the grid takes item w (no atomic);
+      // the counter then hands out items W, W + 1, ...
+      item = static_cast<unsigned long long>(blockIdx.x) * kWaves + wid;
+      if (lane == 0) *x.w_hitcnt = 0;
+      first = false;
+    } else {
+      if (lane == 0) {
+        item = atomicAdd(item_ctr, 1u) + ((kAbl & kAblAtomicFirst) ? 0ull : W);
+        *x.w_hitcnt = 0;
+      }
+      item = __shfl(item, 0);
     }
-    item = __shfl(item, 0);
     if (item >= nitems) break;                                 // wave-uniform exit
     __builtin_amdgcn_wave_barrier();
     unsigned long long c0, rend;
@@ -1012,6 +1030,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
       if (x.primary) chunk_file[c] = t.f;            // K2's file lookup: a file at or before the chunk's first byte
       if (t.p < t.end) t.lim = min(t.end, x.offsets[t.f + 1]);
       OutBuf ob{obuf + blockIdx.x * kThreads + threadIdx.x, gridDim.x * kThreads, 0};
+      if (kAbl & kAblTrace) t_setup = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
       constexpr int kW = (kAbl & kAblLine64) ? 4 : 8;     // words per line
       constexpr uint32_t kL = kW * 16;
       v4u cur[kW], nxt[kW];
@@ -1133,6 +1152,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
           }
         }
       }
+      if (kAbl & kAblTrace) t_loop = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
       if (kAbl & kAblDefer) k1_drain<kC>(x, t, ob, S);
       if (kAbl & kAblLoadOnly) {
         t.nl = static_cast<uint32_t>(t.kw1);
@@ -1140,6 +1160,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
       }
       flush_kw(x.kwmask, kw_words, t.f, t.kw0, t.kw1);
       if (x.primary) nl_count[t.ci] = static_cast<uint16_t>(t.nl);   // the range's last chunk
+      if (kAbl & kAblTrace) t_kw = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
     }
     // flush this wave's hit buffer (the wave has reconverged here)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1166,11 +1187,13 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if ((kAbl & kAblTrace) && lane == 0 && item < kTraceItemCap) {
-      uint32_t* r = trc + 4 * gridDim.x + 4 * item;
+      uint32_t* r = trc + 4 * gridDim.x + kTraceItemWords * item;
       r[0] = t_item;
       r[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
-      r[2] = (blockIdx.x << 8) | wid;
-      r[3] = kU;
+      r[2] = (kU << 24) | (blockIdx.x << 8) | wid;
+      r[3] = t_setup;
+      r[4] = t_loop;
+      r[5] = t_kw;
     }
   }
   __syncthreads();
@@ -1205,6 +1228,7 @@ const void* k1_kernel(int abl, bool compressed) {
     TSG_K1_V3(2448) TSG_K1_V3(2512) TSG_K1_V3(4592) TSG_K1_V3(8656) TSG_K1_V3(12752)
     TSG_K1_V3(4561) TSG_K1_V3(4562) TSG_K1_V3(5072) TSG_K1_V3(65536 + 4560) TSG_K1_V3(131072 + 4560) TSG_K1_V3(131072 + 4592)
     TSG_K1_V3(262144 + 464) TSG_K1_V3(262144 + 4592) TSG_K1_V3(262144 + 4560)
+    TSG_K1_V3(524288 + 4560) TSG_K1_V3(524288 + 262144 + 4560) TSG_K1_V3(524288 + 4592)
 #endif
 #undef TSG_K1_V3
     default: return nullptr;
@@ -2195,9 +2219,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       }
       if (k1_abl_ & kAblTrace) {
         // probe builds: the K1 launch's stamps (kAblTrace) appended to
-        // $TSG_K1_TRACE_FILE as [blocks, items, nchunks, chunk][4 x blocks][4 x items] uint32
+        // $TSG_K1_TRACE_FILE as [blocks, items, nchunks, chunk][4 x blocks][kTraceItemWords x items] uint32
         const uint32_t items = static_cast<uint32_t>(std::min<uint64_t>(kTraceItemCap, 3 * (nchunks + 63) / 64 + 64));
-        std::vector<uint32_t> tr(4 + 4 * static_cast<size_t>(blocks) + 4 * static_cast<size_t>(items), 0);
+        std::vector<uint32_t> tr(4 + 4 * static_cast<size_t>(blocks) + kTraceItemWords * static_cast<size_t>(items), 0);
         tr[0] = blocks; tr[1] = items; tr[2] = static_cast<uint32_t>(nchunks); tr[3] = kChunk;
         HIP_OK(hipMemcpy(tr.data() + 4, ln.d_ob + static_cast<size_t>(blocks) * nthr * kOutSlots,
                          (tr.size() - 4) * sizeof(uint32_t), hipMemcpyDeviceToHost));
