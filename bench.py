@@ -603,6 +603,9 @@ def main():
                          "CPU-baseline sample, then seeded small files); 0 = the CPU-baseline sample only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident comparison leg")
+    ap.add_argument("--resident-keep", action="store_true",
+                    help="diagnostic: keep the resident leg's results until its timed steps are done (their frees "
+                         "then run after the timing instead of on the reaper thread beside the next steps)")
     ap.add_argument("--tree", type=int, default=-1,
                     help="1: also measure the `trivy fs` feed over the batch written as a directory tree "
                          "(default: config 1 only)")
@@ -984,15 +987,20 @@ def main():
         res = rstep()
         same = _lib.result_json(res) == gpu_results
         L.tsg_result_free(res)
-        rst, rwall = [], []
+        rst, rwall, kept = [], [], []
         t0 = time.perf_counter()
         for k in range(max(8, args.steps)):
             t1 = time.perf_counter()
             res = rstep()
             rwall.append(time.perf_counter() - t1)
             rst.append(_lib.result_stats(res))
-            L.tsg_result_free(res)
+            if args.resident_keep:
+                kept.append(res)           # diagnostic: results freed after the timed steps
+            else:
+                L.tsg_result_free(res)
         rdt = (time.perf_counter() - t0) / len(rst)
+        for res in kept:
+            L.tsg_result_free(res)
         rmed = float(np.median(rwall))
         rk1 = float(np.mean([s["k1_ms"] for s in rst]))
         out["resident"] = {"gbps": round(batch.nbytes / rdt / 1e9, 2), "ms_per_step": round(rdt * 1e3, 3),
@@ -1004,6 +1012,8 @@ def main():
                            "median_step_ms": round(rmed * 1e3, 3),
                            "gbps_median_step": round(batch.nbytes / rmed / 1e9, 2),
                            "steps": len(rst),
+                           "step_ms": [round(w * 1e3, 2) for w in rwall],
+                           "results_freed_after_timing": bool(args.resident_keep),
                            "note": "the same batch already in HBM (tsg_scan_batch_resident); gbps over the mean "
                                    "step, gbps_median_step over the median one (host-bound configs vary with the "
                                    "box's CPU quota)"}
