@@ -272,15 +272,15 @@ uint32_t tsg_result_num_files(const tsg_result* r) { return r ? static_cast<uint
 int tsg_result_file_path(const tsg_result* r, uint32_t f, const char** path, size_t* len) {
   TSG_API_TRY
   if (!r || f >= r->files.size()) return fail(TSG_ERR_INVALID, "file index out of range");
-  *path = r->files[f].file_path.data();
-  *len = r->files[f].file_path.size();
+  *path = r->files[f].file_path().data();
+  *len = r->files[f].file_path().size();
   return TSG_OK;
   TSG_API_CATCH
 }
 
 uint32_t tsg_result_num_findings(const tsg_result* r, uint32_t f) {
   if (!r || f >= r->files.size()) return 0;
-  return static_cast<uint32_t>(r->files[f].findings.size());
+  return static_cast<uint32_t>(r->files[f].findings().size());
 }
 
 int tsg_result_file_error(const tsg_result* r, uint32_t f) {
@@ -292,9 +292,9 @@ int tsg_result_file_error(const tsg_result* r, uint32_t f) {
 
 int tsg_result_finding(const tsg_result* r, uint32_t f, uint32_t k, tsg_finding* out) {
   TSG_API_TRY
-  if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
+  if (!r || f >= r->files.size() || k >= r->files[f].findings().size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
   const Secret& sec = r->files[f];
-  const FindingRec& x = sec.findings[k];
+  const FindingRec& x = sec.findings()[k];
   const Rule& ru = *x.rule;
   const std::string& sev = Secret::severity(x);
   out->rule_id = ru.id.data(); out->rule_id_len = ru.id.size();
@@ -311,11 +311,11 @@ int tsg_result_finding(const tsg_result* r, uint32_t f, uint32_t k, tsg_finding*
 
 int tsg_result_line(const tsg_result* r, uint32_t f, uint32_t k, uint32_t l, tsg_line* out) {
   TSG_API_TRY
-  if (!r || f >= r->files.size() || k >= r->files[f].findings.size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
+  if (!r || f >= r->files.size() || k >= r->files[f].findings().size() || !out) return fail(TSG_ERR_INVALID, "index out of range");
   const Secret& sec = r->files[f];
-  const FindingRec& x = sec.findings[k];
+  const FindingRec& x = sec.findings()[k];
   if (l >= x.line_count) return fail(TSG_ERR_INVALID, "line index out of range");
-  const LineRec& ln = sec.lines[x.line_begin + l];
+  const LineRec& ln = sec.lines()[x.line_begin + l];
   out->number = ln.number;
   out->content = sec.ptr(ln.content); out->content_len = ln.content.len;
   out->is_cause = ln.is_cause;
@@ -355,7 +355,7 @@ static void json_bytes(std::string* o, const char* data, size_t n) {
   o->push_back('"');
 }
 
-static void json_str(std::string* o, const std::string& s) { json_bytes(o, s.data(), s.size()); }
+static void json_str(std::string* o, std::string_view s) { json_bytes(o, s.data(), s.size()); }
 
 int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
   TSG_API_TRY
@@ -365,10 +365,12 @@ int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
     const Secret& s = r->files[f];
     if (f) o += ",";
     o += "{\"FilePath\":";
-    json_str(&o, s.file_path);
+    json_str(&o, s.file_path());
     o += ",\"Findings\":[";
-    for (size_t k = 0; k < s.findings.size(); ++k) {
-      const FindingRec& x = s.findings[k];
+    const auto sf = s.findings();
+    const auto sl = s.lines();
+    for (size_t k = 0; k < sf.size(); ++k) {
+      const FindingRec& x = sf[k];
       if (k) o += ",";
       o += "{\"RuleID\":"; json_str(&o, x.rule->id);
       o += ",\"Category\":"; json_str(&o, x.rule->category);
@@ -378,7 +380,7 @@ int tsg_result_json(const tsg_result* r, char** json, size_t* len) {
       o += ",\"EndLine\":" + std::to_string(x.end_line);
       o += ",\"Code\":{\"Lines\":[";
       for (uint32_t l = 0; l < x.line_count; ++l) {
-        const LineRec& ln = s.lines[x.line_begin + l];
+        const LineRec& ln = sl[x.line_begin + l];
         if (l) o += ",";
         o += "{\"Number\":" + std::to_string(ln.number);
         o += ",\"Content\":"; json_bytes(&o, s.ptr(ln.content), ln.content.len);
@@ -509,7 +511,7 @@ constexpr size_t kReapMaxQueued = 4;
 void tsg_result_free(tsg_result* r) {
   if (!r) return;
   size_t weight = r->files.size();
-  for (size_t i = 0; i < r->files.size() && weight < kReapInlineFiles; ++i) weight += r->files[i].findings.size();
+  for (size_t i = 0; i < r->files.size() && weight < kReapInlineFiles; ++i) weight += r->files[i].findings().size();
   if (weight < kReapInlineFiles) { delete r; return; }
   {
     std::lock_guard<std::mutex> lk(g_reaper_mu);
@@ -603,7 +605,7 @@ int tsg_scan_table_model(const tsg_ruleset* rs, const uint8_t* data, const uint6
       // as the engine's confirmer: no candidate, no host-evaluated rule -> only
       // the global allow-path outcome (scanner.go:381-386)
       const std::string p = path_of(paths, path_lens, f);
-      if (global_allow_path(*rs->rs, p)) r->files[f].file_path = p;
+      if (global_allow_path(*rs->rs, p)) r->files[f] = Secret::path_only(p.data(), p.size());
       continue;
     }
     std::vector<std::vector<uint64_t>> tmp = r->cands[f];
@@ -800,13 +802,9 @@ int tsg_result_from_json(const char* json, size_t len, tsg_result** out) {
   auto sget = [](const JValue* o, const char* k) { const JValue* v = o ? o->get(k) : nullptr; return v ? v->as_string() : std::string(); };
   auto iget = [](const JValue* o, const char* k) { const JValue* v = o ? o->get(k) : nullptr; return v && v->kind == JValue::Num ? static_cast<int>(v->num) : 0; };
   auto bget = [](const JValue* o, const char* k) { const JValue* v = o ? o->get(k) : nullptr; return v && v->kind == JValue::Bool && v->b; };
-  auto put = [](Secret* s, const std::string& v) {
-    StrRef ref{static_cast<uint32_t>(s->arena.size()), static_cast<uint32_t>(v.size())};
-    s->arena += v;
-    return ref;
-  };
+  auto put = [](SecretBuilder* s, const std::string& v) { return s->put(v.data(), v.size()); };
   for (const auto& js : doc.arr) {
-    Secret s;
+    SecretBuilder s;
     s.file_path = sget(&js, "FilePath");
     const JValue* fs = js.get("Findings");
     if (fs && fs->kind == JValue::Arr) {
@@ -840,7 +838,7 @@ int tsg_result_from_json(const char* json, size_t len, tsg_result** out) {
         s.findings.push_back(f);
       }
     }
-    r->files.push_back(std::move(s));
+    r->files.push_back(Secret::build(s));
   }
   *out = r;
   return TSG_OK;
@@ -854,7 +852,7 @@ int tsg_result_to_proto(const tsg_result* r, size_t file, const tsg_layer* layer
   const Secret& s = r->files[file];
   std::vector<LayerRef> refs;
   if (layers) {
-    for (size_t k = 0; k < s.findings.size(); ++k)
+    for (size_t k = 0; k < s.findings().size(); ++k)
       refs.push_back(LayerRef{cstr(layers[k].digest), cstr(layers[k].diff_id), cstr(layers[k].created_by)});
   }
   std::string msg, err;
@@ -1464,7 +1462,7 @@ int tsg_queue_probe(tsg_queue* q, const uint8_t* data, const uint64_t* offsets, 
         if (!bad.exchange(true)) first_err = err;
         break;
       }
-      nf += sec.findings.size();
+      nf += sec.findings().size();
     }
   };
   const auto t0 = std::chrono::steady_clock::now();

@@ -2433,7 +2433,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         // no candidates, no host-evaluated rule: only the global allow-path outcome remains
         const char* p = in.paths[f];
         const size_t pn = in.path_lens ? in.path_lens[f] : std::strlen(p);
-        if (global_allow_path(rs, reinterpret_cast<const uint8_t*>(p), pn)) results[f].file_path.assign(p, pn);
+        if (global_allow_path(rs, reinterpret_cast<const uint8_t*>(p), pn)) results[f] = Secret::path_only(p, pn);
       }
     }
   };
@@ -2486,7 +2486,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         prefilter_variant_file(pf_, content, len, &vc, &vg);
         plan_from_candidates(pf_, &vc, &plan);
         Secret s = scan_file(rs, std::move(path), content, len, binary, &plan);
-        my_find += s.findings.size();
+        my_find += s.findings().size();
         results[f] = std::move(s);
         continue;
       }
@@ -2538,7 +2538,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       const auto tp1 = prof ? std::chrono::steady_clock::now() : tp0;
       Secret s = scan_file(rs, std::move(path), content, len, binary, &plan, &nls);
       const auto tp2 = prof ? std::chrono::steady_clock::now() : tp0;
-      my_find += s.findings.size();
+      my_find += s.findings().size();
       results[f] = std::move(s);
       if (prof) {
         const auto tp3 = std::chrono::steady_clock::now();

@@ -375,7 +375,7 @@ void encode_finding(const MFinding& m, const std::vector<LayerRef>& refs, Enc* e
   } else {
     e->open('[');
     for (uint32_t l = 0; l < f.line_count; ++l) {
-      const LineRec& ln = s.lines[f.line_begin + l];
+      const LineRec& ln = s.lines()[f.line_begin + l];
       const std::string content(s.ptr(ln.content), ln.content.len);
       e->elem();
       e->open('{');
@@ -554,13 +554,13 @@ bool report_json(const std::vector<const SecretVec*>& layers, const std::vector<
   for (size_t li = 0; li < layers.size(); ++li) {
     std::vector<const Secret*> secs;
     for (const Secret& s : *layers[li])
-      if (!s.findings.empty()) secs.push_back(&s);
+      if (!s.findings().empty()) secs.push_back(&s);
     if (!opt.layers_sorted)
-      GoSort<const Secret*>(&secs, [&secs](size_t i, size_t j) { return secs[i]->file_path < secs[j]->file_path; }).run();
+      GoSort<const Secret*>(&secs, [&secs](size_t i, size_t j) { return secs[i]->file_path() < secs[j]->file_path(); }).run();
     for (const Secret* s : secs) {
       MSecret ns;
-      ns.path = s->file_path;
-      for (const FindingRec& f : s->findings) ns.findings.push_back({s, &f, static_cast<int>(li)});
+      ns.path = std::string(s->file_path());
+      for (const FindingRec& f : s->findings()) ns.findings.push_back({s, &f, static_cast<int>(li)});
       auto& fs = ns.findings;
       if (!opt.layers_sorted) {
         GoSort<MFinding>(&fs, [&fs](size_t i, size_t j) {
@@ -588,10 +588,10 @@ bool report_json(const std::vector<const SecretVec*>& layers, const std::vector<
   // artifact name (local/scan.go:487-496)
   std::vector<MSecret> all;
   for (auto& kv : merged) all.push_back(std::move(kv.second));
-  if (image_config && !image_config->findings.empty()) {
+  if (image_config && !image_config->findings().empty()) {
     MSecret cs;
     cs.path = opt.artifact_name;
-    for (const FindingRec& f : image_config->findings) cs.findings.push_back({image_config, &f, -1});
+    for (const FindingRec& f : image_config->findings()) cs.findings.push_back({image_config, &f, -1});
     all.push_back(std::move(cs));
   }
   // --- the report document

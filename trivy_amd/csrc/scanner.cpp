@@ -714,7 +714,7 @@ StrRef put(std::string* arena, const std::string& v) {
 }
 
 // scanner.go:475-558 on the (virtual) censored buffer; appends to `out`.
-void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, Secret* out) {
+void to_finding(const Rule& rule, Loc loc, const CensoredView& cv, SecretBuilder* out) {
   FindingRec f;
   f.rule = &rule;
   const size_t n = cv.size();
@@ -892,8 +892,10 @@ struct PhaseClock {
 Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl) {
   PhaseClock pc;
-  Secret out;
-  if (global_allow_path(rs, path)) { out.file_path = std::move(path); return out; }   // scanner.go:381-386
+  if (global_allow_path(rs, path)) return Secret::path_only(path.data(), path.size());   // scanner.go:381-386
+  thread_local SecretBuilder out_tl;             // (per-thread: no allocation per file once warm)
+  SecretBuilder& out = out_tl;
+  out.clear();
   std::string lower;
   bool have_lower = false;
   auto lowered = [&]() -> const std::string& {
@@ -954,14 +956,15 @@ Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, si
     }
     pc.lap(2);
   }
-  if (matched.empty()) return out;                    // types.Secret{}
+  if (matched.empty()) {                              // types.Secret{}
+    Secret empty;
+    empty.error = out.error;
+    return empty;
+  }
   std::vector<Loc>& spans = spans_tl;
   spans.clear();
   for (const auto& m : matched) spans.push_back(m.loc);
   CensoredView cv(content, len, spans, nl_tl, nl);
-  out.findings.reserve(matched.size());
-  out.lines.reserve(matched.size() * 5);
-  out.arena.reserve(matched.size() * 640);        // match line + up to 5 code lines of <= 100 bytes
   for (const auto& m : matched) {
     to_finding(*m.rule, m.loc, cv, &out);
     if (binary) {                                     // scanner.go:440-444
@@ -979,8 +982,44 @@ Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, si
     return ar.compare(fs[i].match.off, fs[i].match.len, ar, fs[j].match.off, fs[j].match.len) < 0;
   }).run();
   out.file_path = std::move(path);            // (by value: callers pass a temporary)
+  Secret res = Secret::build(out);
   pc.lap(4);
-  return out;
+  return res;
+}
+
+Secret Secret::build(const SecretBuilder& b) {
+  Secret s;
+  s.error = b.error;
+  if (b.file_path.empty() && b.findings.empty()) return s;
+  const size_t nf = b.findings.size(), nl = b.lines.size();
+  const size_t bytes = kHdr + nf * sizeof(FindingRec) + nl * sizeof(LineRec) + b.file_path.size() + b.arena.size();
+  char* blk = static_cast<char*>(std::malloc(bytes));
+  if (!blk) throw std::bad_alloc();
+  Hdr h{static_cast<uint32_t>(nf), static_cast<uint32_t>(nl), static_cast<uint32_t>(b.file_path.size()),
+        static_cast<uint32_t>(b.arena.size())};
+  std::memcpy(blk, &h, kHdr);
+  char* q = blk + kHdr;
+  if (nf) std::memcpy(q, b.findings.data(), nf * sizeof(FindingRec));
+  q += nf * sizeof(FindingRec);
+  if (nl) std::memcpy(q, b.lines.data(), nl * sizeof(LineRec));
+  q += nl * sizeof(LineRec);
+  if (!b.file_path.empty()) std::memcpy(q, b.file_path.data(), b.file_path.size());
+  q += b.file_path.size();
+  if (!b.arena.empty()) std::memcpy(q, b.arena.data(), b.arena.size());
+  s.blk_ = blk;
+  return s;
+}
+
+Secret Secret::path_only(const char* p, size_t n) {
+  Secret s;
+  if (n == 0) return s;
+  char* blk = static_cast<char*>(std::malloc(kHdr + n));
+  if (!blk) throw std::bad_alloc();
+  Hdr h{0, 0, static_cast<uint32_t>(n), 0};
+  std::memcpy(blk, &h, kHdr);
+  std::memcpy(blk + kHdr, p, n);
+  s.blk_ = blk;
+  return s;
 }
 
 }  // namespace tsg

@@ -8,6 +8,8 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <string_view>
+#include <cstdlib>
 #include <vector>
 
 #include "goregexp.h"
@@ -93,22 +95,91 @@ struct FindingRec {                      // types.SecretFinding (secret.go:10-20
   uint32_t line_begin = 0, line_count = 0;
 };
 
-struct Secret {                          // types.Secret
+// A read-only view of a contiguous array inside a Secret's block.
+template <typename T>
+struct PodView {
+  const T* p = nullptr;
+  size_t n = 0;
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const T& operator[](size_t i) const { return p[i]; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+  const T& back() const { return p[n - 1]; }
+};
+
+// A Secret under construction (scan_file, the JSON / protobuf decoders):
+// growable parts, turned into one compact Secret by build().
+struct SecretBuilder {
   std::string file_path;
   std::string arena;
   std::vector<FindingRec> findings;
   std::vector<LineRec> lines;
+  int error = 0;
+  void clear() { file_path.clear(); arena.clear(); findings.clear(); lines.clear(); error = 0; }
+  StrRef put(const char* p, size_t n) {
+    StrRef r{static_cast<uint32_t>(arena.size()), static_cast<uint32_t>(n)};
+    arena.append(p, n);
+    return r;
+  }
+};
+
+// types.Secret, compact: a file's path, findings, code lines and their text
+// live in ONE heap block (none for the empty Secret{} that most files get), so
+// a result of hundreds of thousands of files is freed with one free per
+// finding file -- round 5 kept four containers per Secret (120 bytes a slot,
+// four frees per finding file): a config-5 result took 15-23 ms to free, on
+// the reaper beside the next resident step or inline when the reaper lagged.
+class Secret {
+ public:
   int error = 0;                         // nonzero: the reference would panic on this file
-  const char* ptr(StrRef r) const { return arena.data() + r.off; }
+  Secret() = default;
+  Secret(Secret&& o) noexcept : error(o.error), blk_(o.blk_) { o.blk_ = nullptr; o.error = 0; }
+  Secret& operator=(Secret&& o) noexcept {
+    if (this != &o) {
+      release();
+      blk_ = o.blk_; error = o.error;
+      o.blk_ = nullptr; o.error = 0;
+    }
+    return *this;
+  }
+  Secret(const Secret&) = delete;
+  Secret& operator=(const Secret&) = delete;
+  ~Secret() { release(); }
+
+  static Secret build(const SecretBuilder& b);
+  static Secret path_only(const char* p, size_t n);   // Secret{FilePath} (a globally allowed path)
+
+  std::string_view file_path() const {
+    return blk_ ? std::string_view(path_data(), hdr()->plen) : std::string_view();
+  }
+  PodView<FindingRec> findings() const {
+    return blk_ ? PodView<FindingRec>{reinterpret_cast<const FindingRec*>(blk_ + kHdr), hdr()->nf} : PodView<FindingRec>{};
+  }
+  PodView<LineRec> lines() const {
+    return blk_ ? PodView<LineRec>{reinterpret_cast<const LineRec*>(blk_ + kHdr + hdr()->nf * sizeof(FindingRec)), hdr()->nl}
+                : PodView<LineRec>{};
+  }
+  const char* ptr(StrRef r) const { return text_data() + r.off; }
   static const std::string& severity(const FindingRec& f) {
     static const std::string kUnknown = "UNKNOWN";
     return f.rule->severity.empty() ? kUnknown : f.rule->severity;
   }
+
+ private:
+  struct Hdr { uint32_t nf, nl, plen, tlen; };
+  static constexpr size_t kHdr = 16;
+  static_assert(sizeof(Hdr) == kHdr && alignof(FindingRec) <= kHdr, "block layout");
+  char* blk_ = nullptr;                   // [Hdr][FindingRec x nf][LineRec x nl][path][text]
+  const Hdr* hdr() const { return reinterpret_cast<const Hdr*>(blk_); }
+  const char* path_data() const { return blk_ + kHdr + hdr()->nf * sizeof(FindingRec) + hdr()->nl * sizeof(LineRec); }
+  const char* text_data() const { return path_data() + hdr()->plen; }
+  void release() { std::free(blk_); blk_ = nullptr; }
 };
 
 // The per-file results of a batch (one Secret per file).  A vector whose
 // resize default-constructs large ranges on several threads: a batch of
-// image-layer files holds hundreds of thousands of Secrets (120 bytes each),
+// image-layer files holds hundreds of thousands of Secrets (16 bytes each; 120 until round 5),
 // and constructing them on one thread before the first segment's
 // confirmation cost 2.7 ms of a 7.9 ms resident config-3 step (page faults
 // and stores of ~29 MB; profiles/rd4o_bench_c3prof.log).

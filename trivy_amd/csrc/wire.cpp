@@ -110,11 +110,7 @@ struct Reader {
   }
 };
 
-StrRef put(Secret* s, const uint8_t* p, size_t n) {
-  StrRef r{static_cast<uint32_t>(s->arena.size()), static_cast<uint32_t>(n)};
-  s->arena.append(reinterpret_cast<const char*>(p), n);
-  return r;
-}
+StrRef put(SecretBuilder* s, const uint8_t* p, size_t n) { return s->put(reinterpret_cast<const char*>(p), n); }
 
 bool read_string(Reader* r, uint32_t wt, std::string* out) {
   const uint8_t* s;
@@ -130,9 +126,12 @@ bool secret_to_proto(const Secret& sec, const std::vector<LayerRef>* layer_of_fi
                      std::string* err) {
   Enc e{err};
   std::string o;
-  if (!e.str(&o, 1, sec.file_path, "Secret.filepath")) return false;
-  for (size_t k = 0; k < sec.findings.size(); ++k) {
-    const FindingRec& f = sec.findings[k];
+  const std::string_view fp = sec.file_path();
+  if (!e.str(&o, 1, fp.data(), fp.size(), "Secret.filepath")) return false;
+  const auto sf = sec.findings();
+  const auto sl = sec.lines();
+  for (size_t k = 0; k < sf.size(); ++k) {
+    const FindingRec& f = sf[k];
     std::string fm;
     if (!e.str(&fm, 1, f.rule->id, "SecretFinding.rule_id") || !e.str(&fm, 2, f.rule->category, "SecretFinding.category") ||
         !e.str(&fm, 3, Secret::severity(f), "SecretFinding.severity") || !e.str(&fm, 4, f.rule->title, "SecretFinding.title"))
@@ -141,7 +140,7 @@ bool secret_to_proto(const Secret& sec, const std::vector<LayerRef>* layer_of_fi
     e.i32(&fm, 6, f.end_line);
     std::string code;                        // ConvertToRPCCode: always a message
     for (uint32_t l = 0; l < f.line_count; ++l) {
-      const LineRec& ln = sec.lines[f.line_begin + l];
+      const LineRec& ln = sl[f.line_begin + l];
       std::string lm;
       e.i32(&lm, 1, ln.number);
       if (!e.str(&lm, 2, sec.ptr(ln.content), ln.content.len, "Line.content")) return false;
@@ -171,6 +170,7 @@ bool secret_to_proto(const Secret& sec, const std::vector<LayerRef>* layer_of_fi
 bool secret_from_proto(const uint8_t* data, size_t len, std::deque<Rule>* rules, Secret* out,
                        std::vector<LayerRef>* layers, std::string* err) {
   *out = Secret();
+  SecretBuilder sb;
   layers->clear();
   Reader r{data, len};
   auto bad = [&](const char* what) { *err = std::string("proto: cannot parse ") + what; return false; };
@@ -178,7 +178,7 @@ bool secret_from_proto(const uint8_t* data, size_t len, std::deque<Rule>* rules,
     const uint64_t key = r.varint();
     const uint32_t f = static_cast<uint32_t>(key >> 3), wt = static_cast<uint32_t>(key & 7);
     if (f == 1) {
-      if (!read_string(&r, wt, &out->file_path)) return bad("Secret.filepath");
+      if (!read_string(&r, wt, &sb.file_path)) return bad("Secret.filepath");
     } else if (f == 2 && wt == 2) {
       const uint8_t* s;
       size_t l;
@@ -234,7 +234,7 @@ bool secret_from_proto(const uint8_t* data, size_t len, std::deque<Rule>* rules,
               // the result model keeps Highlighted == Content, Annotation "" and
               // Truncated false (all the scanner produces, scanner.go:538-545)
               if (!lm.ok || !ann.empty() || trunc || hl != content) { ok = false; break; }
-              ln.content = put(out, reinterpret_cast<const uint8_t*>(content.data()), content.size());
+              ln.content = put(&sb, reinterpret_cast<const uint8_t*>(content.data()), content.size());
               lines.push_back(ln);
             }
             ok = ok && cm.ok;
@@ -264,18 +264,20 @@ bool secret_from_proto(const uint8_t* data, size_t len, std::deque<Rule>* rules,
       rule.severity = sev;
       rules->push_back(rule);
       fr.rule = &rules->back();
-      fr.match = put(out, reinterpret_cast<const uint8_t*>(match.data()), match.size());
-      fr.line_begin = static_cast<uint32_t>(out->lines.size());
-      for (const LineRec& ln : lines) out->lines.push_back(ln);
+      fr.match = put(&sb, reinterpret_cast<const uint8_t*>(match.data()), match.size());
+      fr.line_begin = static_cast<uint32_t>(sb.lines.size());
+      for (const LineRec& ln : lines) sb.lines.push_back(ln);
       fr.line_count = static_cast<uint32_t>(lines.size());
-      out->findings.push_back(fr);
+      sb.findings.push_back(fr);
       layers->push_back(lr);
     } else {
       r.skip(wt);
     }
     if (!r.ok) return bad("Secret");
   }
-  return r.ok || bad("Secret");
+  if (!r.ok) return bad("Secret");
+  *out = Secret::build(sb);
+  return true;
 }
 
 }  // namespace tsg
