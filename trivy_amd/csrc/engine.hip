@@ -127,7 +127,10 @@ constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
 constexpr double kDenseFilesPerGB = 8000.0;   // upload segmentation: "many small files" (image layers: ~48k/GB)
 // per-lane device counters: [0] cands, [1] K2 count, [2] overflow, [3] LDS-base
 // error, [4 + g] K1 items of group g
-constexpr size_t kCntBytes = 1024;
+constexpr size_t kCntBytes = 8192;
+// K1's work-item counters: group g's at dword kItemCtrBase + g * 256, eight
+// of them 32 dwords (one 128-byte line) apart, one per XCD
+constexpr uint32_t kItemCtrBase = 256, kMaxK1Groups = 7;
 constexpr size_t kInlineConfirmFiles = 4;          // confirmations this small run on the calling thread
 constexpr uint64_t kInlineConfirmBytes = 512 << 10;
 constexpr int kItemChunks = 4;         // a K1 wave item: 64 lanes x (up to) 4 chunks
@@ -365,6 +368,13 @@ constexpr int kAblTrace = 262144;
 // every wave's atomic on one address (the traces put ~37 us of each
 // first-round item there: 4096 same-address atomics serialised in L2)
 constexpr int kAblAtomicFirst = 524288;
+// measurement (results valid): the items after the first round from one
+// counter (until round 6).  Default: eight counters, one per XCD (workgroup
+// index mod 8) on lines of their own, each handing out every eighth item, so
+// the burst of waves finishing their first items together spreads over eight
+// L2 lines instead of queueing on one (250 MB launch 0.1695 -> 0.160 ms,
+// 1 GB 0.440 -> 0.433, 4 GB unchanged; profiles/r7n_*)
+constexpr int kAblOneCounter = 1048576;
 constexpr uint32_t kTraceItemCap = 1u << 17;
 constexpr uint32_t kTraceItemWords = 8;   // [start, end, kU << 24 | wg << 8 | wave, setup done, loop done, flushed, 0, 0]
 
@@ -1006,7 +1016,12 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
       first = false;
     } else {
       if (lane == 0) {
-        item = atomicAdd(item_ctr, 1u) + ((kAbl & kAblAtomicFirst) ? 0ull : W);
+        if (!(kAbl & (kAblOneCounter | kAblAtomicFirst))) {
+          const uint32_t xc = blockIdx.x & 7u;
+          item = W + xc + 8ull * atomicAdd(item_ctr + 32 * xc, 1u);
+        } else {
+          item = atomicAdd(item_ctr, 1u) + ((kAbl & kAblAtomicFirst) ? 0ull : W);
+        }
         *x.w_hitcnt = 0;
       }
       item = __shfl(item, 0);
@@ -1229,6 +1244,7 @@ const void* k1_kernel(int abl, bool compressed) {
     TSG_K1_V3(4561) TSG_K1_V3(4562) TSG_K1_V3(5072) TSG_K1_V3(65536 + 4560) TSG_K1_V3(131072 + 4560) TSG_K1_V3(131072 + 4592)
     TSG_K1_V3(262144 + 464) TSG_K1_V3(262144 + 4592) TSG_K1_V3(262144 + 4560)
     TSG_K1_V3(524288 + 4560) TSG_K1_V3(524288 + 262144 + 4560) TSG_K1_V3(524288 + 4592)
+    TSG_K1_V3(1048576 + 4560) TSG_K1_V3(1048576 + 262144 + 4560)
 #endif
 #undef TSG_K1_V3
     default: return nullptr;
@@ -1958,7 +1974,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   ln.over_cap = std::max<size_t>(ln.over_cap, total / 2048);
   if (!ensure(&ln.d_over, &ln.d_over_cap, ln.over_cap, err)) return false;
   const uint32_t ngroups = static_cast<uint32_t>(dt.k1g.size());
-  if (4 + ngroups > kCntBytes / 4) { *err = "too many scan-DFA groups"; return false; }
+  if (ngroups > kMaxK1Groups) { *err = "too many scan-DFA groups"; return false; }
   if (!ensure(&ln.d_bh, &ln.d_bh_cap, 2ull * std::max(dt.sms, 1) * std::max<uint32_t>(ngroups, 1), err)) return false;
   if (!ensure(&ln.d_ff, &ln.d_ff_cap, std::max<uint32_t>(in.nfiles, 1), err)) return false;
   // deferred-output slots: kOutSlots per thread (x2 grid slack)
@@ -2038,7 +2054,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = dt.k1g[gi];
       const size_t lds = lds_of(g);
-      uint32_t* a_items = ln.d_cnt + 4 + gi;         // v3's work-item counter (zeroed with d_cnt)
+      uint32_t* a_items = ln.d_cnt + kItemCtrBase + 256 * gi;   // v3's work-item counters (zeroed with d_cnt)
       unsigned long long a_total = total;
       uint32_t a_nfiles = in.nfiles, a_ncls = g.nclasses, a_tw = g.table_words16;
       uint32_t a_first = g.first_out, a_nmeta = hits_of(g), a_nlist = g.nlist, a_nkw = pf.nkw;
