@@ -987,6 +987,11 @@ def main():
         res = rstep()
         same = _lib.result_json(res) == gpu_results
         L.tsg_result_free(res)
+        # untimed warm-up of the resident layout (its pieces and K1Chain lanes
+        # differ from the pinned step's; r7q: the first two timed steps ran
+        # 7.0 / 6.2 ms against a 5.4 ms median)
+        for _ in range(max(2, args.warmup)):
+            L.tsg_result_free(rstep())
         rst, rwall, kept = [], [], []
         t0 = time.perf_counter()
         for k in range(max(8, args.steps)):

@@ -114,7 +114,8 @@ def test_largest_k1_chunk_gpu(monkeypatch):
 def test_k1_probe_variants_agree_gpu():
     # the K1 measurement builds whose layout bits keep results valid (no
     # deferred outputs, unrolled loop, 128-B register lines, temporal loads,
-    # single-buffered lines, the boundary-line builds) live in the probe library
+    # single-buffered lines, the boundary-line builds, the start-state bypass,
+    # the memory re-read fold-special check) live in the probe library
     # (libtrivysecret_probe.so, python -m trivy_amd.build --probe); one child
     # process loads it and checks each against the host confirmer
     import subprocess
@@ -123,10 +124,11 @@ def test_k1_probe_variants_agree_gpu():
     assert os.path.exists(probe), "build the probe library: python -m trivy_amd.build --probe"
     env = dict(os.environ, TSG_LIB="libtrivysecret_probe.so")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_k1_probe_variants.py"),
-                        "16:4096,0:8192,2512:1024,2448:2048,464:2048,464:512,8656:1024,12752:2048"],
+                        "16:4096,0:8192,2512:1024,2448:2048,464:2048,464:512,8656:1024,12752:2048,"
+                        "2101712:2048,4198864:1024"],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert r.stdout.count("agree") == 8, r.stdout
+    assert r.stdout.count("agree") == 10, r.stdout
 
 
 @pytest.mark.parametrize("abl,chunk", [("4560", "2048"), ("4560", "1024"), ("4560", "4096"), ("4560", "512"),

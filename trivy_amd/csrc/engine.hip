@@ -375,6 +375,18 @@ constexpr int kAblAtomicFirst = 524288;
 // L2 lines instead of queueing on one (250 MB launch 0.1695 -> 0.160 ms,
 // 1 GB 0.440 -> 0.433, 4 GB unchanged; profiles/r7n_*)
 constexpr int kAblOneCounter = 1048576;
+// layout bit (results valid; VERDICT r5 item 1a, root bypass): bit 0 of the
+// LDS class map (classes are stored doubled, so it is free) flags the classes
+// that keep the start state at the start state; a lane at the start state on
+// such a byte skips its transition read (it drops out of that ds_read under
+// EXEC, so fewer lanes contend for the banks).  The class map stays one byte
+// per entry: tools/lds_bank_sim.py prices the transition read 5.50 -> 4.61
+// LDS cycles per byte with no change to the class read.
+constexpr int kAblRootSkip = 2097152;
+// measurement (results valid): fast lines with a C4 / C5 / E2 lead byte are
+// checked for the fold-special sequences by re-reading the line from memory
+// byte by byte (rounds 4-5) instead of word by word (k1_line_special_words)
+constexpr int kAblSpecialMem = 4194304;
 constexpr uint32_t kTraceItemCap = 1u << 17;
 constexpr uint32_t kTraceItemWords = 8;   // [start, end, kU << 24 | wg << 8 | wave, setup done, loop done, flushed, 0, 0]
 
@@ -415,7 +427,7 @@ __device__ __forceinline__ void k1_word_slow(const K1Ctx& x, K1Stream& t, const 
       const uint32_t c4 = x.cls[b];
       t.s = k1c_next(t.s, c4, __builtin_amdgcn_perm(0u, c4, 0u));
     } else {
-      t.s = k1_step(x.next, t.s, x.cls[b]);
+      t.s = k1_step(x.next, t.s, (kAbl & kAblRootSkip) ? (x.cls[b] & 0xfeu) : x.cls[b]);
     }
     if (q >= t.emit) {
       t.nl += (b == 0x0au);
@@ -762,6 +774,47 @@ __device__ __noinline__ bool k1_line_special(const uint8_t* __restrict__ p, uint
   return hit;
 }
 
+// The same test with the line's words loaded together (round 6; the call
+// site's line is 16-byte aligned): one L2 round trip per 16 bytes, the next
+// word's load in flight, instead of one dependent byte load per byte.  The byte loop above took ~20-35 us per line under a
+// loaded memory system with the whole wave waiting: in a 17 MB file of
+// config-2-like text with a stray lead byte every ~40 KB (synth's 0.05% of
+// files with invalid UTF-8) every 8 KiB item ran ~450 us longer, and such a
+// file's items set the launch's end (2.5 GB launch 1.02 ms, the slowest
+// items 0.9-1.0 ms against a median of 0.56; profiles/r7u_*).  Out of line:
+// the test inlined on the line's registers pushed K1 to 128 VGPRs with 32
+// spilled (4 GB launch 1.16 -> 2.07 ms, profiles/r7v_*).  Per dword w (pw: the
+// dword before it) a byte ends a sequence when it and its one or two
+// predecessors all match, i.e. when the OR of their XORs with the sequence
+// bytes is a zero byte: funnel shifts give the predecessors, and one
+// any-zero-byte test per sequence (exact as an any-byte test) decides.
+__device__ __forceinline__ uint32_t k1_any_zero(uint32_t x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+__device__ __noinline__ bool k1_line_special_words(const uint8_t* __restrict__ p, uint32_t p12, uint32_t n) {
+  uint32_t pw = ((p12 & 0xffu) << 24) | ((p12 & 0xff00u) << 8);   // byte 3: the byte before the line, byte 2: the one before that
+  uint32_t hit = 0;
+  // one word in flight ahead of the one tested, rolled: a callee with many
+  // live VGPRs makes the call site save K1's registers (8 words loaded at once
+  // left K1 with 32 VGPRs spilled)
+  v4u nx = *reinterpret_cast<const v4u*>(p);
+#pragma unroll 1
+  for (uint32_t o = 0; o < n; o += 16) {
+    const v4u cw = nx;
+    if (o + 16 < n) nx = *reinterpret_cast<const v4u*>(p + o + 16);
+    const uint32_t d[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t w = d[j];
+      const uint32_t p1 = __builtin_amdgcn_alignbit(w, pw, 24);   // byte k: byte k - 1
+      const uint32_t p2 = __builtin_amdgcn_alignbit(w, pw, 16);   // byte k: byte k - 2
+      hit |= k1_any_zero((w ^ 0xB0B0B0B0u) | (p1 ^ 0xC4C4C4C4u))                          // U+0130 C4 B0
+           | k1_any_zero((w ^ 0xBFBFBFBFu) | (p1 ^ 0xC5C5C5C5u))                          // U+017F C5 BF
+           | k1_any_zero((w ^ 0xAAAAAAAAu) | (p1 ^ 0x84848484u) | (p2 ^ 0xE2E2E2E2u));   // U+212A E2 84 AA
+      pw = w;
+    }
+  }
+  return hit != 0;
+}
+
 // Can a line (plus the two bytes before it, p12) hold one of those
 // sequences at all: does it contain a lead byte C4 / C5 / E2?  Exact as an
 // any-byte test (a borrow can only flag bytes above a zero byte), run on the
@@ -810,6 +863,10 @@ __device__ __forceinline__ void k1_word_v3(const K1Ctx& x, K1Stream& t, OutBuf& 
   for (int k = 0; k < 16; ++k) {
     if constexpr (kC) s = k1c_next(s, c2[k], __builtin_amdgcn_perm(0u, c2[k], 0u));   // K1c: class * 4 in every byte
     else if (kAbl & kAblPtrAddr) s = *reinterpret_cast<const uint16_t*>(smem + kTabOff + (s << 2) + c2[k]);
+    else if (kAbl & kAblRootSkip) {
+      // (s | flag ^ 1) == 0: at the start state (row offset 0) on a self-loop class
+      if ((s | ((c2[k] & 1u) ^ 1u)) != 0u) s = k1_lds16((s << 2) + (c2[k] & 0xfeu) + kTabOff);
+    }
     else s = k1_lds16((s << 2) + c2[k] + kTabOff);
     st[k] = s;
   }
@@ -967,7 +1024,11 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const uint4* src = reinterpret_cast<const uint4*>(g_next);
     uint4* dst = reinterpret_cast<uint4*>(smem + kTabOff);
     for (uint32_t i = threadIdx.x; i < padded / 16; i += blockDim.x) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) smem[i] = g_cls[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+      uint32_t c = g_cls[i];
+      if (!kC && (kAbl & kAblRootSkip) && g_next[c >> 1] == 0) c |= 1u;   // row 0 = the start state's row
+      smem[i] = static_cast<uint8_t>(c);
+    }
     if (!kC) {
       uint32_t* s_list = reinterpret_cast<uint32_t*>(smem + list_off);
       for (uint32_t i = threadIdx.x; i < nlist; i += blockDim.x) s_list[i] = g_list[i];
@@ -1084,7 +1145,9 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
 #pragma unroll
                 for (int i = 0; i < kW; ++i)
                   lead |= k1_has_lead(cur[i].x) | k1_has_lead(cur[i].y) | k1_has_lead(cur[i].z) | k1_has_lead(cur[i].w);
-                if (lead && k1_line_special(data + t.p, t.p12, kL)) atomicOr(&x.fflags[t.f], 1u);
+                if (lead && ((kAbl & kAblSpecialMem) ? k1_line_special(data + t.p, t.p12, kL)
+                                                     : k1_line_special_words(data + t.p, t.p12, kL)))
+                  atomicOr(&x.fflags[t.f], 1u);
               }
             }
             if (kAbl & kAblRolled) {
@@ -1245,6 +1308,7 @@ const void* k1_kernel(int abl, bool compressed) {
     TSG_K1_V3(262144 + 464) TSG_K1_V3(262144 + 4592) TSG_K1_V3(262144 + 4560)
     TSG_K1_V3(524288 + 4560) TSG_K1_V3(524288 + 262144 + 4560) TSG_K1_V3(524288 + 4592)
     TSG_K1_V3(1048576 + 4560) TSG_K1_V3(1048576 + 262144 + 4560)
+    TSG_K1_V3(2097152 + 4560) TSG_K1_V3(4194304 + 4560) TSG_K1_V3(4194304 + 262144 + 4560)
 #endif
 #undef TSG_K1_V3
     default: return nullptr;
