@@ -149,6 +149,25 @@ def test_k1_variants_agree_gpu(monkeypatch, abl, chunk):
     assert sum(len(w["Findings"]) for w in want) > 20
 
 
+@pytest.mark.parametrize("chunk,rounds", [("1024", "0"), ("4096", "0"), ("128", "0"), ("512", "0")])
+def test_k1_top8_schedule_gpu(monkeypatch, chunk, rounds):
+    # the kU = 8 bulk level (TSG_K1_TOP8, launches of >= 2 GiB) forced onto a
+    # 24 MB batch: with no tail rounds every wave item is 64 lanes x 8 chunks
+    # (4096-B chunks: a 2 MiB item, the hit record's offset limit; the levels
+    # below it run in every launch of >= 2 GiB, bench.py's resident leg and
+    # same_findings)
+    c = synth.generate(24_000_000, seed=31, sizes="loguniform", plant_rate=3e-3)
+    args = [S.ScanArgs(c.paths[i], c.file(i)) for i in range(len(c.paths))]
+    want = _oracle_all("variants", args)
+    monkeypatch.setenv("TSG_K1_TOP8", "2")
+    monkeypatch.setenv("TSG_K1_CHUNK", chunk)
+    monkeypatch.setenv("TSG_K1_TAIL_ROUNDS", rounds)
+    got, stats = S.Scanner(None).ScanBatch(args, with_stats=True)
+    assert stats["chunk_bytes"] == int(chunk)
+    assert got == want
+    assert sum(len(w["Findings"]) for w in want) > 20
+
+
 @pytest.mark.parametrize("chunk", ["256", "128"])
 def test_small_chunks_large_batch_gpu(monkeypatch, chunk):
     # the chunk sizes the per-launch policy picks for small launches (128-512

@@ -127,6 +127,10 @@ class Engine {
   // whose results are invalid.
   int k1_abl_ = 4560;
   uint32_t k1_tail_rounds_ = 1;         // v3 guided schedule: grid rounds of 2- and of 1-chunk ranges (TSG_K1_TAIL_ROUNDS)
+  // launches of >= 2 GiB: 1 KiB chunks with 8-chunk bulk ranges, then rounds
+  // of 4-, 2- and 1-chunk ranges (TSG_K1_TOP8=1; 2: the kU = 8 level in every
+  // launch, for tests), instead of 2 KiB chunks
+  int k1_top8_ = 1;
   // drivers per device for resident batches (TSG_RESIDENT_DRIVERS; 2 =
   // K1Chain).  Round 4 chained the second driver's K1 behind the first's K2:
   // no gain (config 2 1530 vs 1528 GB/s).  Chained behind the first's K1

@@ -1056,15 +1056,29 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   // rounds of kU = 2 and as many of kU = 1, so the waves that take the last
   // items finish after a short item and the launch has no long tail
   // (measured r2u, 4 GB: 1.29 ms without the short rounds, 1.21 with one
-  // round each, 1.24 / 1.27 with two / four).
+  // round each, 1.24 / 1.27 with two / four).  With bit 8 of tail_rounds
+  // (round 6, launches of >= 2 GiB at half the chunk) the bulk is kU = 8 and
+  // kU = 4 gets `tail_rounds` rounds too: the same bulk ranges, the last
+  // round's ranges half as long.
+  const uint32_t rounds = tail_rounds & 0xffu;
+  const bool top8 = (tail_rounds & 0x100u) != 0;
   const unsigned long long W = static_cast<unsigned long long>(gridDim.x) * kWaves;
-  const unsigned long long n1 = min(nchunks, W * 64 * tail_rounds);
-  const unsigned long long n2 = min(nchunks - n1, W * 128 * tail_rounds);
-  const unsigned long long n4 = nchunks - n1 - n2;
-  const unsigned long long i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
-  const unsigned long long nitems = i4 + i2 + (n1 + 63) / 64;
+  const unsigned long long n1 = min(nchunks, W * 64 * rounds);
+  const unsigned long long n2 = min(nchunks - n1, W * 128 * rounds);
+  const unsigned long long n4 = top8 ? min(nchunks - n1 - n2, W * 256 * rounds) : nchunks - n1 - n2;
+  const unsigned long long n8 = nchunks - n1 - n2 - n4;
+  const unsigned long long i8 = (n8 + 511) / 512, i4 = (n4 + 255) / 256, i2 = (n2 + 127) / 128;
+  const unsigned long long nitems = i8 + i4 + i2 + (n1 + 63) / 64;
   if ((kAbl & kAblTrace) && threadIdx.x == 0) trc[4 * blockIdx.x + 1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
   bool first = !(kAbl & kAblAtomicFirst);
+  // the next item from the counters (lane 0)
+  auto take = [&]() -> unsigned long long {
+    if (!(kAbl & (kAblOneCounter | kAblAtomicFirst))) {
+      const uint32_t xc = blockIdx.x & 7u;
+      return W + xc + 8ull * atomicAdd(item_ctr + 32 * xc, 1u);
+    }
+    return atomicAdd(item_ctr, 1u) + ((kAbl & kAblAtomicFirst) ? 0ull : W);
+  };
   for (;;) {
     unsigned long long item = 0;
     const uint32_t t_item = (kAbl & kAblTrace) ? static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) : 0u;
@@ -1077,12 +1091,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
       first = false;
     } else {
       if (lane == 0) {
-        if (!(kAbl & (kAblOneCounter | kAblAtomicFirst))) {
-          const uint32_t xc = blockIdx.x & 7u;
-          item = W + xc + 8ull * atomicAdd(item_ctr + 32 * xc, 1u);
-        } else {
-          item = atomicAdd(item_ctr, 1u) + ((kAbl & kAblAtomicFirst) ? 0ull : W);
-        }
+        item = take();
         *x.w_hitcnt = 0;
       }
       item = __shfl(item, 0);
@@ -1091,10 +1100,11 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     __builtin_amdgcn_wave_barrier();
     unsigned long long c0, rend;
     uint32_t kU;
-    if (item < i4) { kU = 4; c0 = item * 256; rend = n4; }
-    else if (item < i4 + i2) { kU = 2; c0 = n4 + (item - i4) * 128; rend = n4 + n2; }
-    else { kU = 1; c0 = n4 + n2 + (item - i4 - i2) * 64; rend = nchunks; }
-    x.item_base = c0 * static_cast<unsigned long long>(chunk);   // hit offsets < 256 chunks (k1_max_chunk(4))
+    if (item < i8) { kU = 8; c0 = item * 512; rend = n8; }
+    else if (item < i8 + i4) { kU = 4; c0 = n8 + (item - i8) * 256; rend = n8 + n4; }
+    else if (item < i8 + i4 + i2) { kU = 2; c0 = n8 + n4 + (item - i8 - i4) * 128; rend = n8 + n4 + n2; }
+    else { kU = 1; c0 = n8 + n4 + n2 + (item - i8 - i4 - i2) * 64; rend = nchunks; }
+    x.item_base = c0 * static_cast<unsigned long long>(chunk);   // hit offsets < 64 * kU chunks (k1_max_chunk(kU), host-checked)
     const unsigned long long c = c0 + lane * kU;                 // the lane's first chunk
     if (c < rend) {
       K1Stream t;
@@ -1347,8 +1357,8 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // short (round 5: a 250 MB launch 0.249 -> 0.231 ms with 512-B chunks against
 // 1 KiB, 1 GB 0.583 -> 0.529 ms, profiles/r5a_*; a 77 MB launch used 147 of
 // 256 CUs with 512-B chunks; a 15 KB file's launch took 22 us at 256 B).
-uint32_t k1_chunk_for(uint64_t bytes, uint32_t lanes) {
-  if (bytes >= (2ull << 30)) return 2048;
+uint32_t k1_chunk_for(uint64_t bytes, uint32_t lanes, int top8) {
+  if (bytes >= (2ull << 30)) return top8 ? 1024 : 2048;   // (top8 != 0)   // (top8: the same bulk ranges of 8 KiB per lane)
   const uint64_t per = (bytes / std::max<uint32_t>(lanes, 1)) & ~uint64_t(127);
   return static_cast<uint32_t>(std::min<uint64_t>(512, std::max<uint64_t>(128, per)));
 }
@@ -1858,6 +1868,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
     const int v = std::atoi(c);
     if (v >= 0 && v <= 16) e->k1_tail_rounds_ = static_cast<uint32_t>(v);
   }
+  if (const char* c = std::getenv("TSG_K1_TOP8")) e->k1_top8_ = std::max(0, std::min(2, std::atoi(c)));
   if (const char* c = std::getenv("TSG_K2_HITS_PER_THREAD")) {
     const int v = std::atoi(c);
     if (v >= 1 && v <= 64) e->k2_hits_per_thread_ = static_cast<uint32_t>(v);
@@ -1991,8 +2002,12 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
-  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u);
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u, k1_top8_);
   if (kChunk > k1_max_chunk(kItemChunks) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
+  // the kU = 8 bulk level (TSG_K1_TOP8) for launches of >= 2 GiB (2: any
+  // launch, for tests), while an 8-chunk wave item fits the hit record's
+  // offset bits
+  const bool top8 = (k1_top8_ == 2 || (k1_top8_ == 1 && total >= (2ull << 30))) && kChunk <= k1_max_chunk(8);
   if ((k1_abl_ & kAblNoLoad) && total < (1u << 20) + 64) { *err = "TSG_K1_ABL no-load build needs a batch of >= 1 MiB"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
@@ -2136,7 +2151,7 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       uint32_t* a_ocnt = ln.d_cnt + 2;
       uint32_t a_ocap = static_cast<uint32_t>(std::min<size_t>(ln.over_cap, 0xffffffffu));
       uint32_t a_rcap = region_cap;
-      uint32_t a_tail = k1_tail_rounds_;
+      uint32_t a_tail = k1_tail_rounds_ | (top8 ? 0x100u : 0u);
       void* args[] = {&a_data, &a_total, &d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
