@@ -163,6 +163,7 @@ class Engine {
   // files gains nothing from more pieces (profiles/r5t_resident_pieces.log)
   uint32_t pieces_ = 5;
   double first_piece_ = 0.1;
+  double first_piece_few_ = 0.2;        // the first piece's share when a batch makes 3 pieces (TSG_FIRST_PIECE_FEW)
   double last_piece_ = 0.08;
   uint64_t min_piece_ = 256ull << 20;   // resident data: smaller batches run as one piece (TSG_MIN_PIECE_BYTES)
   uint64_t segment_min_ = 64ull << 20;   // uploaded data: smallest segment of the geometric tail (TSG_SEGMENT_MIN; r3s: 128 MB 51.5 vs 256 MB 48.8 GB/s on config 1; r4p: 64 MB 53.2 vs 128 MB 52.5)
