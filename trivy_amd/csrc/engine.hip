@@ -1349,18 +1349,27 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 }
 
 // Default K1 chunk for a launch of `bytes` on `lanes` lanes (CUs x 1024).  K1
-// walks ranges of 1-4 chunks per lane (guided schedule): its chunk is the
-// '\n'-count granularity and the last round's range.  2 KiB for launches of 2
-// GiB and more (measured r2r: 3.34 vs 3.21 TB/s at 4 GB); below, the chunk
-// that gives every lane about one (128 B - 512 B): a lane walks ~13 MB/s
-// whatever the load, so a small launch is as fast as its lanes' ranges are
-// short (round 5: a 250 MB launch 0.249 -> 0.231 ms with 512-B chunks against
-// 1 KiB, 1 GB 0.583 -> 0.529 ms, profiles/r5a_*; a 77 MB launch used 147 of
-// 256 CUs with 512-B chunks; a 15 KB file's launch took 22 us at 256 B).
+// walks ranges of 1-4 chunks per lane (guided schedule; 1-8 with top8): its
+// chunk is the '\n'-count granularity and the last round's range.  1 KiB
+// for launches of 2 GiB and more with top8 (2 KiB without: measured r2r,
+// 3.34 vs 3.21 TB/s at 4 GB against 1 KiB with 4-chunk ranges).  Below 2 GiB a
+// lane walks ~13 MB/s whatever the load, so a small launch is as fast as its
+// lanes' ranges are short and evenly dealt (round 5: a 250 MB launch 0.249 ->
+// 0.231 ms with 512-B chunks against 1 KiB, 1 GB 0.583 -> 0.529 ms).  Round 6
+// (profiles/r8h_*, config-1 files): the chunk that fits the launch in exactly
+// one round of one-chunk ranges when one of <= 512 B does (100 MB: 384 B,
+// 0.079 ms, against 0.096 with 256 B; 125 MB: 512 B, 0.097 against 0.111 with
+// the rounded-down 384 B, whose 1.24 chunks per lane left a second round of
+// 2-chunk ranges); 256 B up to 512 MB (150 MB 0.126 -> 0.104 ms against 512 B,
+// 200 MB 0.135 -> 0.121, 300 MB 0.176 -> 0.162, 400 MB equal, 500 MB 0.253 ->
+// 0.235); 512 B above (600 MB equal, 800 MB 0.331 against 0.341 with 256 B,
+// 1.5 GB 0.551 against 0.58).
 uint32_t k1_chunk_for(uint64_t bytes, uint32_t lanes, int top8) {
-  if (bytes >= (2ull << 30)) return top8 ? 1024 : 2048;   // (top8 != 0)   // (top8: the same bulk ranges of 8 KiB per lane)
-  const uint64_t per = (bytes / std::max<uint32_t>(lanes, 1)) & ~uint64_t(127);
-  return static_cast<uint32_t>(std::min<uint64_t>(512, std::max<uint64_t>(128, per)));
+  if (bytes >= (2ull << 30)) return top8 ? 1024 : 2048;   // (top8 != 0)
+  const uint64_t l = std::max<uint32_t>(lanes, 1);
+  const uint64_t one_round = ((bytes + l - 1) / l + 127) & ~uint64_t(127);   // chunks <= lanes
+  if (one_round <= 512) return static_cast<uint32_t>(std::max<uint64_t>(128, one_round));
+  return bytes <= (512ull << 20) ? 256 : 512;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
