@@ -506,7 +506,7 @@ def launch_ranks(n, argv, dry=False):
     if not dry:
         import torch
         have = torch.cuda.device_count()
-        if have < n:
+        if have < n and not _share_devices():
             print("[bench] --gpus %d needs %d GPUs, %d visible" % (n, n, have), file=sys.stderr, flush=True)
             return 2
     with socket.socket() as s:
@@ -566,6 +566,11 @@ def gather_ranks(dist, world, mine):
     got = [None] * world
     dist.all_gather_object(got, mine)
     return got
+
+
+def _share_devices():
+    """rehearsal of the N-rank path on fewer GPUs (TSG_BENCH_SHARE_DEVICES=1): never a metric run"""
+    return os.environ.get("TSG_BENCH_SHARE_DEVICES", "0") == "1"
 
 
 def _segment_balanced():
@@ -655,7 +660,7 @@ def main():
         return
 
     import torch
-    if torch.cuda.device_count() <= local_rank:
+    if torch.cuda.device_count() <= local_rank and not _share_devices():
         print("[bench] rank %d needs HIP device %d, %d visible" % (rank, local_rank, torch.cuda.device_count()),
               file=sys.stderr, flush=True)
         sys.exit(2)
@@ -669,7 +674,9 @@ def main():
             print("[bench]", *a, file=sys.stderr, flush=True)
 
     L = _lib.lib()
-    device = local_rank
+    # (TSG_BENCH_SHARE_DEVICES=1, rehearsal only: ranks beyond the visible
+    # devices share them round-robin, so the N-rank path runs on a 1-GPU box)
+    device = local_rank % torch.cuda.device_count() if _share_devices() else local_rank
     torch.cuda.set_device(device)
     numa = numa_bind(device)
     cores, cores_detail = available_cores()
@@ -858,6 +865,8 @@ def main():
         "value": round(value, 3),
         "unit": "GB/s",
         "n_gpus": world,
+        **({"rehearsal": "TSG_BENCH_SHARE_DEVICES=1: ranks share %d device(s); not a metric run"
+                         % torch.cuda.device_count()} if _share_devices() else {}),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
