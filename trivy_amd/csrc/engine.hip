@@ -2015,12 +2015,16 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   const uint64_t total = in.offsets[in.nfiles];
   const uint8_t* d_data = static_cast<const uint8_t*>(d_data_v);
   if ((reinterpret_cast<uintptr_t>(d_data) & 15) != 0) { *err = "device data must be 16-byte aligned"; return false; }
-  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u, k1_top8_);
+  // top8 for uploaded segments only: HBM-resident pieces, whose K1 runs beside
+  // the previous piece's K2 (K1Chain), ran slower with it (config 2 resident
+  // 5.55 vs 6.06-6.65 ms per step, K1 3.72 vs 3.80 ms, profiles/r8l_*)
+  const int top8_req = sg.in.d_data ? 0 : k1_top8_;
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u, top8_req);
   if (kChunk > k1_max_chunk(kItemChunks) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   // the kU = 8 bulk level (TSG_K1_TOP8) for launches of >= 2 GiB (2: any
   // launch, for tests), while an 8-chunk wave item fits the hit record's
   // offset bits
-  const bool top8 = (k1_top8_ == 2 || (k1_top8_ == 1 && total >= (2ull << 30))) && kChunk <= k1_max_chunk(8);
+  const bool top8 = (top8_req == 2 || (top8_req == 1 && total >= (2ull << 30))) && kChunk <= k1_max_chunk(8);
   if ((k1_abl_ & kAblNoLoad) && total < (1u << 20) + 64) { *err = "TSG_K1_ABL no-load build needs a batch of >= 1 MiB"; return false; }
   st->chunk_bytes = kChunk;
   out->chunk = kChunk;
