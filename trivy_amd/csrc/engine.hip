@@ -2584,7 +2584,8 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         }
       }
       const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
-      std::string path = in.path_lens ? std::string(in.paths[f], in.path_lens[f]) : std::string(in.paths[f]);
+      const char* path_p = in.paths[f];
+      const size_t path_n = in.path_lens ? in.path_lens[f] : std::strlen(path_p);
       const uint8_t* content = in.h_data + in.offsets[f];
       const size_t len = in.offsets[f + 1] - in.offsets[f];
       const bool binary = in.binary ? in.binary[f] != 0 : false;
@@ -2597,7 +2598,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
         std::vector<uint8_t> vg;
         prefilter_variant_file(pf_, content, len, &vc, &vg);
         plan_from_candidates(pf_, &vc, &plan);
-        Secret s = scan_file(rs, std::move(path), content, len, binary, &plan);
+        Secret s = scan_file(rs, path_p, path_n, content, len, binary, &plan);
         my_find += s.findings().size();
         results[f] = std::move(s);
         continue;
@@ -2648,7 +2649,7 @@ void Engine::confirm_segment(CallCtx& cc, const Segment& sg, GpuOut& g, Secret* 
       nls.file_off = in.offsets[f];
       nls.chunk = g.chunk;
       const auto tp1 = prof ? std::chrono::steady_clock::now() : tp0;
-      Secret s = scan_file(rs, std::move(path), content, len, binary, &plan, &nls);
+      Secret s = scan_file(rs, path_p, path_n, content, len, binary, &plan, &nls);
       const auto tp2 = prof ? std::chrono::steady_clock::now() : tp0;
       my_find += s.findings().size();
       results[f] = std::move(s);

@@ -891,11 +891,23 @@ struct PhaseClock {
 
 Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl) {
+  return scan_file(rs, path.data(), path.size(), content, len, binary, plan, nl);
+}
+
+// (the path by pointer and length: it is copied into the per-thread builder,
+// whose buffer is reused from file to file -- the engine's confirm pool made a
+// std::string of every confirmed file's path, a heap allocation and a free per
+// file once paths pass 15 bytes)
+Secret scan_file(const Ruleset& rs, const char* path_p, size_t path_n, const uint8_t* content, size_t len,
+                 bool binary, const FilePlan* plan, const NlSource* nl) {
   PhaseClock pc;
-  if (global_allow_path(rs, path)) return Secret::path_only(path.data(), path.size());   // scanner.go:381-386
+  if (global_allow_path(rs, reinterpret_cast<const uint8_t*>(path_p), path_n))
+    return Secret::path_only(path_p, path_n);    // scanner.go:381-386
   thread_local SecretBuilder out_tl;             // (per-thread: no allocation per file once warm)
   SecretBuilder& out = out_tl;
   out.clear();
+  out.file_path.assign(path_p, path_n);
+  const std::string& path = out.file_path;
   std::string lower;
   bool have_lower = false;
   auto lowered = [&]() -> const std::string& {
@@ -981,7 +993,6 @@ Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, si
     if (fs[i].rule->id != fs[j].rule->id) return fs[i].rule->id < fs[j].rule->id;
     return ar.compare(fs[i].match.off, fs[i].match.len, ar, fs[j].match.off, fs[j].match.len) < 0;
   }).run();
-  out.file_path = std::move(path);            // (by value: callers pass a temporary)
   Secret res = Secret::build(out);
   pc.lap(4);
   return res;

@@ -272,6 +272,8 @@ extern std::atomic<bool> g_scan_prof_on;
 extern std::atomic<uint64_t> g_scan_prof[8];
 Secret scan_file(const Ruleset& rs, std::string path, const uint8_t* content, size_t len,
                  bool binary, const FilePlan* plan, const NlSource* nl = nullptr);
+Secret scan_file(const Ruleset& rs, const char* path, size_t path_len, const uint8_t* content, size_t len,
+                 bool binary, const FilePlan* plan, const NlSource* nl = nullptr);
 
 // Exact Go FindAll(Submatch)Index restricted to candidate start offsets.
 // `starts` must be a sorted superset of every position where an anchored
