@@ -138,7 +138,8 @@ class Engine {
   // leaves the critical chain: config 2 1632 -> 1862 GB/s, 1 GB of config-1
   // files 482 -> 570 (profiles/r5p_resident_variants.log).
   int resident_drivers_ = 2;
-  int chain_k1_ = 1;                    // K1Chain: 0 = next K1 after this K2, 1 = after this K1, 2 = no wait (TSG_CHAIN_K1)
+  int chain_k1_ = 1;
+  bool readback_dma_ = false;           // K1Chain pieces read back by DMA copies instead of tsg_readback (TSG_READBACK_DMA)                    // K1Chain: 0 = next K1 after this K2, 1 = after this K1, 2 = no wait (TSG_CHAIN_K1)
   // K1Chain drivers poll their readback event yielding instead of sleeping
   // 10 us (TSG_POLL_YIELD), and the confirmer polls the job queue up to
   // pop_spin_us_ before it sleeps (TSG_POP_SPIN_US): a wake-up under the busy

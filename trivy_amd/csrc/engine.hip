@@ -982,8 +982,12 @@ __device__ __forceinline__ void k1_word_c(const K1Ctx& x, K1Stream& t, OutBuf& o
   t.p += 16;
 }
 
+// At most 120 VGPRs (allocated in 8s): 4 K1 waves per SIMD then leave 32 per
+// lane free, room for the readback kernel (8 VGPRs) of the previous resident
+// piece on the same CUs while this K1 runs; at 121-128 they fill the register
+// file and that readback waits for the whole K1 launch (round 6)
 template <int kThreads, int kAbl, bool kC>
-__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
+__attribute__((amdgpu_num_vgpr(120))) __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const uint8_t* __restrict__ data, unsigned long long total,
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
@@ -1872,6 +1876,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_K2_ABL")) e->k2_abl_ = std::atoi(c) & (kK2Trace | kK2NoWalk);   // probe library builds
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::max(0, std::min(2, std::atoi(c)));
+  if (const char* c = std::getenv("TSG_READBACK_DMA")) e->readback_dma_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_CONFIRM_PREFETCH")) e->confirm_prefetch_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POLL_YIELD")) e->poll_yield_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POP_SPIN_US")) e->pop_spin_us_ = std::max(0, std::min(std::atoi(c), 100000));
@@ -2243,13 +2248,26 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
           !ensure_pinned(&ln.rb_ff, in.nfiles * sizeof(uint32_t), err) ||
           !ensure_pinned(&ln.rb_nl, nchunks * sizeof(uint16_t), err) ||
           !ensure_pinned(&ln.rb_cands, ln.cand_cap * sizeof(CandDev), err)) return false;
-      Readbacks rb;
-      rb.add(ln.d_bh, ln.rb_bh, nregions);
-      rb.add(ln.d_cnt, ln.rb_c2, 4);
-      rb.add(ln.d_ff, ln.rb_ff, in.nfiles);
-      rb.add(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2);
-      rb.add(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4);
-      if (!rb.launch(s, err)) return false;
+      if (chain && readback_dma_) {
+        // K1Chain: the next piece's K1 (other driver) holds every CU's
+        // register file until its launch ends, so a readback kernel queued
+        // behind this K2 waited for it (0.7-0.85 ms per resident piece,
+        // profiles/r8o_*); copies on the DMA engines need no CU.  The
+        // candidates go whole (the buffer's capacity, not the count).
+        HIP_OK(hipMemcpyAsync(ln.rb_bh.p, ln.d_bh, nregions * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(ln.rb_c2.p, ln.d_cnt, 16, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(ln.rb_ff.p, ln.d_ff, in.nfiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(ln.rb_nl.p, ln.d_nl, ((nchunks + 1) / 2) * 4, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(ln.rb_cands.p, ln.d_cands, ln.cand_cap * sizeof(CandDev), hipMemcpyDeviceToHost, s));
+      } else {
+        Readbacks rb;
+        rb.add(ln.d_bh, ln.rb_bh, nregions);
+        rb.add(ln.d_cnt, ln.rb_c2, 4);
+        rb.add(ln.d_ff, ln.rb_ff, in.nfiles);
+        rb.add(ln.d_nl, ln.rb_nl, (nchunks + 1) / 2);
+        rb.add(ln.d_cands, ln.rb_cands, ln.cand_cap * (sizeof(CandDev) / 4), ln.d_cnt + 1, sizeof(CandDev) / 4);
+        if (!rb.launch(s, err)) return false;
+      }
       if (chain) {
         // polled with short sleeps: a blocking-sync event woke its driver
         // 0.3-1.2 ms after the passes ended (profiles/rd5e_bench_c2prof.log)
