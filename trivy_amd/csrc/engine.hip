@@ -982,12 +982,8 @@ __device__ __forceinline__ void k1_word_c(const K1Ctx& x, K1Stream& t, OutBuf& o
   t.p += 16;
 }
 
-// At most 120 VGPRs (allocated in 8s): 4 K1 waves per SIMD then leave 32 per
-// lane free, room for the readback kernel (8 VGPRs) of the previous resident
-// piece on the same CUs while this K1 runs; at 121-128 they fill the register
-// file and that readback waits for the whole K1 launch (round 6)
 template <int kThreads, int kAbl, bool kC>
-__attribute__((amdgpu_num_vgpr(120))) __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
+__global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     const uint8_t* __restrict__ data, unsigned long long total,
     const uint64_t* __restrict__ offsets, uint32_t nfiles,
     const uint16_t* __restrict__ g_next, const uint8_t* __restrict__ g_cls,
