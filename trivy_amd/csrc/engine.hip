@@ -1873,6 +1873,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::max(0, std::min(2, std::atoi(c)));
   if (const char* c = std::getenv("TSG_READBACK_DMA")) e->readback_dma_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_K1_RESERVE_CUS")) e->k1_reserve_cus_ = static_cast<uint32_t>(std::max(0, std::min(64, std::atoi(c))));
   if (const char* c = std::getenv("TSG_CONFIRM_PREFETCH")) e->confirm_prefetch_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POLL_YIELD")) e->poll_yield_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POP_SPIN_US")) e->pop_spin_us_ = std::max(0, std::min(std::atoi(c), 100000));
@@ -2085,7 +2086,13 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
     const uint64_t want_blocks = (nchunks + nthr - 1) / nthr;
     // one resident workgroup per CU (the LDS table takes most of the CU's
     // 160 KiB): a grid of exactly one workgroup per CU, waves take items
-    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms)));
+    // K1Chain (resident pieces): k1_reserve_cus_ CUs left out of the grid, so
+    // the previous piece's K2 and readback kernels, queued behind its K1 and
+    // ready while this K1 runs, find a CU at once -- K1's 1024 threads x 122
+    // VGPRs fill a CU's register file, and those kernels otherwise waited for
+    // the whole launch (0.8 ms per piece, profiles/r8o_*, r9d_*)
+    const uint32_t reserve = chain && sms > 2 * k1_reserve_cus_ ? k1_reserve_cus_ : 0u;
+    const uint32_t blocks = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, sms - reserve)));
     st->k1_blocks = blocks;
     st->k1_threads = nthr;
     st->table_in_lds = 1;
