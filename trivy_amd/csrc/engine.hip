@@ -1364,12 +1364,17 @@ bool ensure(T** p, size_t* cap, size_t n, std::string* err) {
 // 200 MB 0.135 -> 0.121, 300 MB 0.176 -> 0.162, 400 MB equal, 500 MB 0.253 ->
 // 0.235); 512 B above (600 MB equal, 800 MB 0.331 against 0.341 with 256 B,
 // 1.5 GB 0.551 against 0.58).
-uint32_t k1_chunk_for(uint64_t bytes, uint32_t lanes, int top8) {
+// Resident pieces keep 512 B there: a piece's per-chunk '\n' counts are read
+// back and summed by the confirmation after its K2, on the step's critical
+// path for the last piece, and 256-B chunks double them (1 GB of config-1
+// files in three resident pieces: 1.45-1.46 ms per step at 512 B, 1.58 at
+// 256, profiles/r9h_*).
+uint32_t k1_chunk_for(uint64_t bytes, uint32_t lanes, int top8, bool resident) {
   if (bytes >= (2ull << 30)) return top8 ? 1024 : 2048;   // (top8 != 0)
   const uint64_t l = std::max<uint32_t>(lanes, 1);
   const uint64_t one_round = ((bytes + l - 1) / l + 127) & ~uint64_t(127);   // chunks <= lanes
   if (one_round <= 512) return static_cast<uint32_t>(std::max<uint64_t>(128, one_round));
-  return bytes <= (512ull << 20) ? 256 : 512;
+  return bytes <= (512ull << 20) && !resident ? 256 : 512;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -2021,7 +2026,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   // the previous piece's K2 (K1Chain), ran slower with it (config 2 resident
   // 5.55 vs 6.06-6.65 ms per step, K1 3.72 vs 3.80 ms, profiles/r8l_*)
   const int top8_req = sg.in.d_data ? 0 : k1_top8_;
-  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u, top8_req);
+  const uint32_t kChunk = chunk_ ? chunk_ : k1_chunk_for(total, static_cast<uint32_t>(std::max(dt.sms, 1)) * 1024u, top8_req,
+                                                         sg.in.d_data != nullptr);
   if (kChunk > k1_max_chunk(kItemChunks) || kChunk % 128 != 0) { *err = "K1 chunk exceeds the hit record's offset range"; return false; }
   // the kU = 8 bulk level (TSG_K1_TOP8) for launches of >= 2 GiB (2: any
   // launch, for tests), while an 8-chunk wave item fits the hit record's
