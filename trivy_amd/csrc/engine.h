@@ -140,7 +140,8 @@ class Engine {
   int resident_drivers_ = 2;
   int chain_k1_ = 1;
   uint32_t k1_reserve_cus_ = 0;         // K1Chain pieces: CUs left out of K1's grid for the previous piece's K2 / readback (TSG_K1_RESERVE_CUS)
-  bool readback_dma_ = false;           // K1Chain pieces read back by DMA copies instead of tsg_readback (TSG_READBACK_DMA)                    // K1Chain: 0 = next K1 after this K2, 1 = after this K1, 2 = no wait (TSG_CHAIN_K1)
+  bool readback_dma_ = false;
+  bool file_index_ = true;              // K1 range starts' files from a per-64-KiB index (TSG_K1_FILE_INDEX)           // K1Chain pieces read back by DMA copies instead of tsg_readback (TSG_READBACK_DMA)                    // K1Chain: 0 = next K1 after this K2, 1 = after this K1, 2 = no wait (TSG_CHAIN_K1)
   // K1Chain drivers poll their readback event yielding instead of sleeping
   // 10 us (TSG_POLL_YIELD), and the confirmer polls the job queue up to
   // pop_spin_us_ before it sleeps (TSG_POP_SPIN_US): a wake-up under the busy

@@ -121,6 +121,33 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ off, ui
   return f;
 }
 
+// K1's file index (round 6): fidx[b] = file_of(b << kFidxShift) for every
+// 64 KiB block of the launch, built by tsg_file_index before K1, so a range
+// start's file is a binary search between two neighbouring entries (0-3
+// dependent loads for large files) instead of over every file (11-19): the
+// items after a wave's first took ~9 us to set up under K1's memory load
+// against ~3 us for the first (profiles/r7z_k1_trace_c2_step.txt).
+constexpr uint32_t kFidxShift = 16;
+__global__ __launch_bounds__(256) void tsg_file_index(const uint64_t* __restrict__ off, uint32_t nfiles,
+                                                      uint32_t* __restrict__ fidx, uint32_t nblk) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b < nblk) fidx[b] = file_of(off, nfiles, static_cast<uint64_t>(b) << kFidxShift);
+}
+// file_of(off, nfiles, pos) for pos < off[nfiles], searched between the index
+// entries of pos's block and the next one (file_of is monotonic in pos)
+__device__ __forceinline__ uint32_t file_of_idx(const uint64_t* __restrict__ off, uint32_t nfiles,
+                                                const uint32_t* __restrict__ fidx, uint64_t pos) {
+  const uint64_t b = pos >> kFidxShift;
+  uint32_t lo = fidx[b], hi = min(fidx[b + 1], nfiles);
+  while (lo < hi) {
+    const uint32_t m = (lo + hi + 1) >> 1;
+    if (off[m] <= pos) lo = m; else hi = m - 1;
+  }
+  uint32_t f = lo;
+  while (f < nfiles && off[f + 1] <= pos) ++f;
+  return f;
+}
+
 constexpr uint32_t kWaveHits = kK1WaveHits;   // largest per-wave LDS hit buffer (entries of 4 bytes: offset in item << 11 | anchor)
 constexpr uint32_t kAnchorBits = 11;   // anchors per ruleset < 2048 (checked on the host)
 constexpr uint32_t kMaxWaves = 16;     // K1 workgroups are at most 1024 threads
@@ -212,6 +239,7 @@ struct K1Ctx {
   uint32_t chunk;
   const uint64_t* __restrict__ offsets;
   uint32_t nfiles;
+  const uint32_t* __restrict__ fidx;   // the launch's file index (tsg_file_index), or nullptr
   const uint16_t* next;   // pre-multiplied: next[s + c] is the next state's row offset
   const uint8_t* cls;     // byte -> class * 2
   uint32_t first_out;     // row offset (dwords) of the first state with outputs
@@ -456,7 +484,7 @@ __device__ __forceinline__ void k1_init(const K1Ctx& x, K1Stream& t, unsigned lo
   t.ci = 0;
   const unsigned long long end = t.end;
   if (c0 >= end) { t.p = t.lim = end; t.f = 0; return; }
-  t.f = file_of(x.offsets, x.nfiles, t.p);
+  t.f = x.fidx ? file_of_idx(x.offsets, x.nfiles, x.fidx, t.p) : file_of(x.offsets, x.nfiles, t.p);
   t.lim = min(end, x.offsets[t.f + 1]);
 }
 
@@ -994,7 +1022,8 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
     unsigned long long* __restrict__ hits, uint32_t* __restrict__ block_hits, uint32_t region_cap,
     unsigned long long* __restrict__ over, uint32_t* __restrict__ over_cnt, uint32_t over_cap,
     uint16_t* __restrict__ nl_count, uint32_t* __restrict__ chunk_file, uint32_t* __restrict__ fflags,
-    uint32_t* __restrict__ item_ctr, uint32_t* __restrict__ obuf, uint32_t tail_rounds) {
+    uint32_t* __restrict__ item_ctr, uint32_t* __restrict__ obuf, uint32_t tail_rounds,
+    const uint32_t* __restrict__ fidx) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kThreads / 64;
   constexpr uint32_t kTabOff = 256;
@@ -1036,7 +1065,7 @@ __global__ __launch_bounds__(kThreads) void tsg_k1_scan_v3(
   }
   K1Ctx x;
   x.data = data; x.total = total; x.chunk = chunk;
-  x.offsets = offsets; x.nfiles = nfiles;
+  x.offsets = offsets; x.nfiles = nfiles; x.fidx = fidx;
   x.next = reinterpret_cast<const uint16_t*>(smem + kTabOff);
   x.cls = smem;
   x.first_out = first_out; x.nclasses = nclasses; x.wave_hits = wave_hits;
@@ -1517,6 +1546,7 @@ struct Lane {
   uint32_t* d_cf = nullptr; size_t d_cf_cap = 0;   // per K1 chunk: a file at or before its first byte (K2's file lookup)
   uint32_t* d_ff = nullptr; size_t d_ff_cap = 0;
   uint32_t* d_ob = nullptr; size_t d_ob_cap = 0;    // K1 v3 deferred-output slots (kOutSlots per thread)
+  uint32_t* d_fidx = nullptr; size_t d_fidx_cap = 0;   // K1's file index (tsg_file_index): one entry per 64 KiB
   unsigned long long* d_k2s = nullptr;              // TSG_K2_STATS: per-rule K2 counters (4 per rule)
   unsigned int* d_cnt = nullptr;
   uint8_t* d_cr = nullptr; size_t d_cr_cap = 0;     // CR strip scratch (crstrip.hip)
@@ -1606,7 +1636,7 @@ Lane::~Lane() {
   if (copy) hipStreamSynchronize(copy);
   for (uint64_t* h : h_off_pin) if (h) hipHostFree(h);
   for (PinnedBuf* b : {&rb_bh, &rb_c2, &rb_cands, &rb_ff, &rb_nl}) if (b->p) hipHostFree(b->p);
-  void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_cf, d_ff, d_ob, d_cnt, d_k2s, d_cr};
+  void* ps[] = {ring[0], ring[1], off_slot[0], off_slot[1], d_off, d_kw, d_hits, d_over, d_bh, d_cands, d_nl, d_cf, d_ff, d_ob, d_cnt, d_k2s, d_cr, d_fidx};
   for (void* p : ps) if (p) hipFree(p);
   for (auto& e : ev) if (e) hipEventDestroy(e);
   if (ev_sync) hipEventDestroy(ev_sync);
@@ -1878,6 +1908,7 @@ std::unique_ptr<Engine> Engine::create(std::shared_ptr<const Ruleset> rs, const 
   if (const char* c = std::getenv("TSG_RESIDENT_DRIVERS")) e->resident_drivers_ = std::max(1, std::atoi(c));
   if (const char* c = std::getenv("TSG_CHAIN_K1")) e->chain_k1_ = std::max(0, std::min(2, std::atoi(c)));
   if (const char* c = std::getenv("TSG_READBACK_DMA")) e->readback_dma_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("TSG_K1_FILE_INDEX")) e->file_index_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_K1_RESERVE_CUS")) e->k1_reserve_cus_ = static_cast<uint32_t>(std::max(0, std::min(64, std::atoi(c))));
   if (const char* c = std::getenv("TSG_CONFIRM_PREFETCH")) e->confirm_prefetch_ = std::atoi(c) != 0;
   if (const char* c = std::getenv("TSG_POLL_YIELD")) e->poll_yield_ = std::atoi(c) != 0;
@@ -2084,6 +2115,9 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
   // deferred-output slots: kOutSlots per thread (x2 grid slack)
   if (!ensure(&ln.d_ob, &ln.d_ob_cap, static_cast<size_t>(std::max(dt.sms, 1)) * 1024 * 2 * kOutSlots, err))
     return false;
+  // K1's file index: entries for blocks 0 .. (total - 1) >> 16, plus one
+  const uint32_t nfidx = total ? static_cast<uint32_t>(((total - 1) >> kFidxShift) + 2) : 0u;
+  if (file_index_ && nfidx && !ensure(&ln.d_fidx, &ln.d_fidx_cap, nfidx, err)) return false;
 
   const uint32_t sms = static_cast<uint32_t>(dt.sms);
   const Prefilter& pf = pf_;
@@ -2160,6 +2194,13 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       if (chain->last && chain_k1_ != 2) HIP_OK(hipStreamWaitEvent(s, chain->last, 0));   // (2: no wait, K1s overlap)
     }
     HIP_OK(hipEventRecord(ln.ev[0], s));
+    const uint32_t* a_fidx = nullptr;
+    if (file_index_ && nfidx && nchunks > 0) {          // (inside K1's timed window)
+      hipLaunchKernelGGL(tsg_file_index, dim3((nfidx + 255) / 256), dim3(256), 0, s, static_cast<const uint64_t*>(d_off),
+                         in.nfiles, ln.d_fidx, nfidx);
+      HIP_OK(hipGetLastError());
+      a_fidx = ln.d_fidx;
+    }
     uint32_t launches = 0;
     for (uint32_t gi = 0; gi < ngroups && nchunks > 0; ++gi) {
       const K1Group& g = dt.k1g[gi];
@@ -2186,7 +2227,8 @@ bool Engine::run_segment(DeviceTables& dt, Lane& ln, const Segment& sg, const vo
       void* args[] = {&a_data, &a_total, &d_off, &a_nfiles, &a_next, &a_cls, &a_ncls, &a_tw, &a_first,
                       &a_meta, &a_nmeta, &a_list, &a_nlist, &a_nkw, &a_warm, &a_chunk, &a_nchunks,
                       &ln.d_kw, &a_kww, &a_kwbase, &a_primary, &a_hits, &a_bh, &a_rcap,
-                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_cf, &ln.d_ff, &a_items, &ln.d_ob, &a_tail};
+                      &ln.d_over, &a_ocnt, &a_ocap, &ln.d_nl, &ln.d_cf, &ln.d_ff, &a_items, &ln.d_ob, &a_tail,
+                      &a_fidx};
       HIP_OK(hipLaunchKernel(k1_kernel(k1_abl_, g.compressed), dim3(blocks), dim3(nthr), args, lds, s));
       ++launches;
     }
